@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Headline benchmark: images/sec (whole node), 64x64x3 DCGAN, bs=128 per GPU.
+
+``python bench.py --gpus N --steps K --warmup W`` runs the full reference-semantics
+DCGAN training step (G fwd, D(real)+D(fake) fwd, 3 losses, D/G backward, gradient
+all-reduce over RCCL when N>1, two TF-Adam updates) on synthetic images of the BASELINE
+shape with random-init weights. For N>1 it is launched one rank per GPU by
+``torch.distributed.run``. W untimed warmup steps, then EXACTLY K timed steps between a
+barrier + device sync on both sides; the per-rank time is MAX-reduced over ranks and
+rank 0 prints one JSON line. ``value`` = N * batch * K / max_time (weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_VALUE = None  # the reference publishes no number ("published": {})
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
+    p.add_argument("--output_size", type=int, default=64)
+    p.add_argument("--c_dim", type=int, default=3)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--engine", default="hip", choices=["hip", "reference"])
+    p.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip engine)")
+    p.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if rank == 0:
+            print("bench.py: --gpus %d but WORLD_SIZE=%d (launch with torch.distributed.run)" % (args.gpus, world),
+                  file=sys.stderr)
+        sys.exit(2)
+
+    from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    from distributed_tensorflow_for_dcgan_amd.engine.factory import build_engine
+
+    device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    pg = D.init_distributed(world, rank, device)
+    cfg = DCGANConfig(output_size=args.output_size, c_dim=args.c_dim)
+    eng = build_engine(cfg, args.batch_size, device, engine=args.engine, dtype=args.dtype, seed=args.seed,
+                       rank=rank, world=world, graph=bool(args.graph), allreduce_dtype=args.allreduce_dtype)
+    gen = torch.Generator(device="cpu").manual_seed(args.seed + 1000 * rank)
+    real = (torch.rand(args.batch_size, cfg.output_size, cfg.output_size, cfg.c_dim, generator=gen) * 2 - 1)
+    real = real.to(device)
+    eng.set_synthetic_batch(real)
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.train_step()
+    sync()
+    D.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.train_step()
+    sync()
+    D.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt = D.max_over_ranks(dt, device)
+    losses = eng.last_losses()
+    imgs = args.gpus * args.batch_size * args.steps
+    value = imgs / dt
+    ms = dt / args.steps * 1e3
+    if rank == 0:
+        res = {
+            "metric": "images/sec (whole node), 64x64 DCGAN bs=128/GPU at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": getattr(eng, "dtype_name", args.dtype),
+            "data": "synthetic (uniform[-1,1] images of shape [B,%d,%d,%d]; random-init weights)"
+                    % (cfg.output_size, cfg.output_size, cfg.c_dim),
+            "config": {"model": "DCGAN-%dx%dx%d (G 5,135,363 / D 4,316,545 params)"
+                       % (cfg.output_size, cfg.output_size, cfg.c_dim),
+                       "global_batch": args.batch_size * args.gpus, "per_gpu_batch": args.batch_size,
+                       "seq_len": None, "parallelism": "dp%d" % args.gpus, "engine": eng.name,
+                       "hip_graph": bool(getattr(eng, "graph_enabled", False)),
+                       "gflop_per_image": round(cfg.flops_per_image() / 1e9, 4),
+                       "tflops_achieved": round(value * cfg.flops_per_image() / 1e12, 2),
+                       "last_losses": {k: round(float(v), 5) for k, v in losses.items()}},
+        }
+        print(json.dumps(res), flush=True)
+    D.shutdown()
+
+
+if __name__ == "__main__":
+    main()

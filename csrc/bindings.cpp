@@ -1,0 +1,425 @@
+// Python bindings of the native runtime: a recorded "Program" of kernel launches.
+//
+// The training step is static (fixed shapes, fixed buffers), so the Python engine records it
+// ONCE as a list of fully-bound launch closures (pointers, grids, phase tables resolved at
+// build time) and then replays ranges of it with one Python->C++ call per range. A range can be
+// captured into a hipGraph by the caller (torch.cuda.graph) or replayed eagerly; either way
+// there is no per-launch Python work in the steady state. Each op carries a stream slot (0 =
+// compute, 1.. = side streams) and event ops express cross-stream dependencies, so
+// gradient all-reduces can overlap backward compute.
+//
+// No torch headers: pointers are passed as integers (tensor.data_ptr()), streams as the raw
+// hipStream_t integer (torch.cuda.Stream.cuda_stream). Built with hipcc for gfx950.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hip/kernels.h"
+
+namespace py = pybind11;
+using namespace dcg;
+
+#define HIPCHECK(x)                                                                             \
+  do {                                                                                          \
+    hipError_t e__ = (x);                                                                       \
+    if (e__ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e__)); \
+  } while (0)
+
+template <class T>
+static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+struct Op {
+  std::string name;
+  int stream;  // slot
+  std::function<int(hipStream_t)> fn;
+};
+
+class Program {
+ public:
+  ~Program() {
+    for (void* p : dev_allocs_) (void)hipFree(p);
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+  }
+
+  int size() const { return (int)ops_.size(); }
+  std::string name(int i) const { return ops_.at(i).name; }
+
+  void run(std::vector<uintptr_t> streams, int begin, int end) {
+    if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
+    for (int i = begin; i < end; ++i) {
+      const Op& op = ops_[i];
+      if (op.stream >= (int)streams.size()) throw std::runtime_error("op " + op.name + ": missing stream slot");
+      const int rc = op.fn(reinterpret_cast<hipStream_t>(streams[op.stream]));
+      if (rc != 0) throw std::runtime_error("op " + std::to_string(i) + " (" + op.name + ") failed: rc=" +
+                                            std::to_string(rc) + " " + hipGetErrorString((hipError_t)rc));
+    }
+  }
+
+  // ------------------------------------------------------------------ events
+  int new_event() {
+    hipEvent_t e;
+    HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    events_.push_back(e);
+    return (int)events_.size() - 1;
+  }
+  int record(int ev, int stream) {
+    hipEvent_t e = events_.at(ev);
+    return add("record", stream, [e](hipStream_t s) { return (int)hipEventRecord(e, s); });
+  }
+  int wait(int ev, int stream) {
+    hipEvent_t e = events_.at(ev);
+    return add("wait", stream, [e](hipStream_t s) { return (int)hipStreamWaitEvent(s, e, 0); });
+  }
+  int memset(uintptr_t ptr, size_t bytes, int stream) {
+    void* p = reinterpret_cast<void*>(ptr);
+    return add("memset", stream, [p, bytes](hipStream_t s) { return (int)hipMemsetAsync(p, 0, bytes, s); });
+  }
+  int copy(uintptr_t dst, uintptr_t src, size_t bytes, int stream) {
+    void* d = reinterpret_cast<void*>(dst);
+    const void* sp = reinterpret_cast<const void*>(src);
+    return add("copy", stream, [d, sp, bytes](hipStream_t s) {
+      return (int)hipMemcpyAsync(d, sp, bytes, hipMemcpyDeviceToDevice, s);
+    });
+  }
+
+  // ------------------------------------------------------------------ implicit GEMM conv
+  // mode 0 conv (stride-2 TF SAME), 1 deconv (conv_transpose, 4 sub-pixel phases), 2 plain GEMM
+  int igemm(std::string name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win, int Kc,
+            int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
+            uintptr_t bias, int act, float leak, uintptr_t stats, int stream) {
+    int bm = 0, bn = 0;
+    if (dcg_igemm_tile(cfg, &bm, &bn)) throw std::runtime_error("bad igemm cfg");
+    std::vector<IGemmPhase> ph;
+    IGemmArgs a{};
+    a.A = P<const bf16>(A); a.Bn = Bn; a.H = Hin; a.W = Win; a.Kc = Kc;
+    a.Bw = P<const bf16>(Bw); a.N = N;
+    a.C = P<void>(C); a.out_f32 = out_f32; a.outH = Hout; a.outW = Wout; a.ldc = ldc; a.cofs = cofs;
+    a.bias = P<const float>(bias); a.act = act; a.leak = leak; a.stats = P<float>(stats);
+    size_t a_elems, b_elems;
+    if (mode == 0) {
+      a.sstride = 2; a.plain = 0; a.ostride = 1;
+      IGemmPhase p{};
+      p.Hq = Hout; p.Wq = Wout; p.M = Bn * Hout * Wout;
+      p.iy0_off = -pad_y; p.ix0_off = -pad_x; p.oy_off = 0; p.ox_off = 0;
+      p.ntaps = 25;
+      for (int t = 0; t < 25; ++t) { p.dy[t] = (signed char)(t / 5); p.dx[t] = (signed char)(t % 5); p.wtap[t] = (short)t; }
+      p.fd_hw = fastdiv_make(Hout * Wout); p.fd_w = fastdiv_make(Wout);
+      ph.push_back(p);
+      a_elems = (size_t)Bn * Hin * Win * Kc; b_elems = (size_t)25 * N * Kc;
+    } else if (mode == 1) {
+      a.sstride = 1; a.plain = 0; a.ostride = 2;
+      for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+          IGemmPhase p{};
+          p.Hq = (Hout - py + 1) / 2; p.Wq = (Wout - px + 1) / 2; p.M = Bn * p.Hq * p.Wq;
+          const int kys = (py + pad_y) & 1, kxs = (px + pad_x) & 1;
+          p.iy0_off = (py + pad_y - kys) / 2; p.ix0_off = (px + pad_x - kxs) / 2;
+          p.oy_off = py; p.ox_off = px;
+          int n = 0;
+          for (int ty = 0; kys + 2 * ty < 5; ++ty)
+            for (int tx = 0; kxs + 2 * tx < 5; ++tx) {
+              p.dy[n] = (signed char)(-ty); p.dx[n] = (signed char)(-tx);
+              p.wtap[n] = (short)((kys + 2 * ty) * 5 + kxs + 2 * tx);
+              ++n;
+            }
+          p.ntaps = n;
+          p.fd_hw = fastdiv_make(p.Hq * p.Wq); p.fd_w = fastdiv_make(p.Wq);
+          if (p.M > 0) ph.push_back(p);
+        }
+      a_elems = (size_t)Bn * Hin * Win * Kc; b_elems = (size_t)25 * N * Kc;
+    } else if (mode == 2) {
+      a.sstride = 1; a.plain = 1; a.ostride = 1;
+      IGemmPhase p{};
+      p.Hq = 1; p.Wq = 1; p.M = Bn * Hout * Wout; p.ntaps = 1;
+      p.fd_hw = fastdiv_make(1); p.fd_w = fastdiv_make(1);
+      ph.push_back(p);
+      a_elems = (size_t)p.M * Kc; b_elems = (size_t)N * Kc;
+    } else {
+      throw std::runtime_error("bad igemm mode");
+    }
+    if (a_elems * 2 >= 0x80000000ull || b_elems * 2 >= 0x80000000ull)
+      throw std::runtime_error("igemm operand exceeds the 2 GiB buffer-descriptor range");
+    a.a_bytes = (uint32_t)(a_elems * 2); a.b_bytes = (uint32_t)(b_elems * 2);
+    a.nphases = (int)ph.size();
+    int maxM = 0;
+    for (auto& p : ph) maxM = std::max(maxM, p.M);
+    const int mtiles = (maxM + bm - 1) / bm, ntiles = (N + bn - 1) / bn;
+    a.mtiles = mtiles;
+    void* dph = nullptr;
+    HIPCHECK(hipMalloc(&dph, ph.size() * sizeof(IGemmPhase)));
+    HIPCHECK(hipMemcpy(dph, ph.data(), ph.size() * sizeof(IGemmPhase), hipMemcpyHostToDevice));
+    dev_allocs_.push_back(dph);
+    a.ph = reinterpret_cast<const IGemmPhase*>(dph);
+    last_mtiles_ = mtiles;
+    last_nphases_ = a.nphases;
+    return add(name, stream, [a, cfg, mtiles, ntiles](hipStream_t s) {
+      return dcg_igemm_launch(&a, cfg, mtiles, ntiles, s);
+    });
+  }
+  int last_mtiles() const { return last_mtiles_; }
+  int last_nphases() const { return last_nphases_; }
+
+  // ------------------------------------------------------------------ weight gradient
+  // mode 0 conv/deconv gather (25 taps), 2 plain (1 tap). out: [splits][taps][Mc][Nc] fp32 slabs,
+  // then reduced into dst (fp32, scaled) by a fused split-K reduce op.
+  int wgrad(std::string name, int mode, uintptr_t G, int Hg, int Wg, int Mc, uintptr_t Dm, int Bn, int Hd, int Wd,
+            int Nc, int pad, int cfg, int splits, uintptr_t slabs, uintptr_t dst, size_t dst_elems, float scale,
+            int stream) {
+    WGradArgs a{};
+    a.G = P<const bf16>(G); a.Hg = Hg; a.Wg = Wg; a.Mc = Mc;
+    a.Dm = P<const bf16>(Dm); a.Nc = Nc;
+    a.K = Bn * Hd * Wd; a.plain = mode == 2; a.pl = pad; a.ntaps = mode == 2 ? 1 : 25;
+    a.out = P<float>(slabs);
+    const int KT = (a.K + 63) / 64;
+    a.kt_per_split = (KT + splits - 1) / splits;
+    const size_t g_elems = mode == 2 ? (size_t)a.K * Mc : (size_t)Bn * Hg * Wg * Mc;
+    const size_t d_elems = (size_t)a.K * Nc;
+    if (g_elems * 2 >= 0x80000000ull || d_elems * 2 >= 0x80000000ull)
+      throw std::runtime_error("wgrad operand exceeds the 2 GiB buffer-descriptor range");
+    a.g_bytes = (uint32_t)(g_elems * 2); a.d_bytes = (uint32_t)(d_elems * 2);
+    a.fd_hw = fastdiv_make(Hd * Wd); a.fd_w = fastdiv_make(Wd); a.Hd = Hd; a.Wd = Wd;
+    const size_t n = (size_t)a.ntaps * Mc * Nc;
+    if (dst_elems > n) throw std::runtime_error("wgrad dst larger than result");
+    float* slab = P<float>(slabs);
+    float* d = P<float>(dst);
+    add(name, stream, [a, cfg, splits](hipStream_t s) { return dcg_wgrad_launch(&a, cfg, splits, s); });
+    // plain mode may carry padded rows (im2col K padding): reduce only the first dst_elems of
+    // each slab's leading part -- rows are m-major so the valid prefix is contiguous.
+    return add(name + ".reduce", stream, [slab, splits, n, d, dst_elems, scale](hipStream_t s) {
+      if (dst_elems == n) return dcg_splitk_reduce(slab, splits, n, d, scale, s);
+      // strided variant: reduce the whole slab into itself (slab 0) then copy the valid prefix
+      int rc = dcg_splitk_reduce(slab, splits, n, slab, scale, s);
+      if (rc) return rc;
+      return (int)hipMemcpyAsync(d, slab, dst_elems * sizeof(float), hipMemcpyDeviceToDevice, s);
+    });
+  }
+
+  // ------------------------------------------------------------------ BN / activations
+  int colstats(std::string name, int mode, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
+               int act, float leak, int R, int C, int rows_per_block, int rows_per_group, uintptr_t part,
+               int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_colstats(mode, P<const bf16>(x), P<const bf16>(dy), P<const bf16>(y), P<const float>(mean),
+                          P<const float>(rstd), act, leak, R, C, rows_per_block, rows_per_group, P<float>(part), s);
+    });
+  }
+  int bn_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, double count, uintptr_t gamma,
+                  uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
+                  uintptr_t ema_mean, uintptr_t ema_var, float decay, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_bn_finalize(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+                             P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
+                             P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, s);
+    });
+  }
+  int bn_coef_eval(std::string name, int C, uintptr_t gamma, uintptr_t beta, float eps, uintptr_t mean,
+                   uintptr_t var, float debias, uintptr_t scale, uintptr_t shift, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_bn_coef_eval(C, P<const float>(gamma), P<const float>(beta), eps, P<const float>(mean),
+                              P<const float>(var), debias, P<float>(scale), P<float>(shift), s);
+    });
+  }
+  int bn_apply_act(std::string name, uintptr_t x, uintptr_t y, uintptr_t scale, uintptr_t shift, int R, int C,
+                   int rows_per_group, int act, float leak, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_bn_apply_act(P<const bf16>(x), P<bf16>(y), P<const float>(scale), P<const float>(shift), R, C,
+                              rows_per_group, act, leak, s);
+    });
+  }
+  int bn_bwd_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, float count, uintptr_t gamma,
+                      uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
+                      int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_bn_bwd_finalize(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+                                 P<const float>(mean), P<const float>(rstd), P<float>(dgamma), P<float>(dbeta),
+                                 P<float>(coef), s);
+    });
+  }
+  int bn_bwd_apply(std::string name, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t coef, uintptr_t dx, int R,
+                   int C, int rows_per_group, int act, float leak, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_bn_bwd_apply(P<const bf16>(dy), P<const bf16>(y), P<const bf16>(x), P<const float>(coef),
+                              P<bf16>(dx), R, C, rows_per_group, act, leak, s);
+    });
+  }
+  int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_act_bwd(P<const bf16>(dy), P<const bf16>(y), P<bf16>(dx), n, act, leak, s);
+    });
+  }
+  int sum_partials(std::string name, uintptr_t part, int Pn, int stride, int C, uintptr_t dst, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_sum_partials(P<const float>(part), Pn, stride, C, P<float>(dst), s);
+    });
+  }
+  int colsum_small(std::string name, uintptr_t x, int R, int C, uintptr_t part, int blocks, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_colsum_small(P<const bf16>(x), R, C, P<float>(part), blocks, s);
+    });
+  }
+
+  // ------------------------------------------------------------------ heads, losses, optimiser
+  int gan_loss(std::string name, uintptr_t logits, int B, uintptr_t out, uintptr_t dl_d, uintptr_t dl_g,
+               uintptr_t prob, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_gan_loss(P<const float>(logits), B, P<float>(out), P<float>(dl_d), P<float>(dl_g),
+                          P<float>(prob), s);
+    });
+  }
+  int linear_fwd(std::string name, uintptr_t z, uintptr_t W, uintptr_t b, uintptr_t out, int B, int K, int N,
+                 int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_linear_fwd(P<const float>(z), P<const float>(W), P<const float>(b), P<bf16>(out), B, K, N, s);
+    });
+  }
+  int linear_wgrad(std::string name, uintptr_t z, uintptr_t dh, uintptr_t dW, uintptr_t db, int B, int K, int N,
+                   int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_linear_wgrad(P<const float>(z), P<const bf16>(dh), P<float>(dW), P<float>(db), B, K, N, s);
+    });
+  }
+  int gemv_head(std::string name, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int R, int K, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_gemv_head(P<const bf16>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, s);
+    });
+  }
+  int head_dgrad(std::string name, uintptr_t dl, uintptr_t w, uintptr_t dx, int R, int K, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_head_dgrad(P<const float>(dl), P<const float>(w), P<bf16>(dx), R, K, s);
+    });
+  }
+  int head_wgrad(std::string name, uintptr_t x, uintptr_t dl, uintptr_t part, int R, int K, int splits,
+                 uintptr_t dW, uintptr_t db, int stream) {
+    add(name, stream, [=](hipStream_t s) {
+      return dcg_head_wgrad(P<const bf16>(x), P<const float>(dl), P<float>(part), R, K, splits, s);
+    });
+    add(name + ".reduce", stream, [=](hipStream_t s) {
+      return dcg_splitk_reduce(P<const float>(part), splits, (size_t)K, P<float>(dW), 1.f, s);
+    });
+    return add(name + ".bias", stream, [=](hipStream_t s) { return dcg_sum_vec(P<const float>(dl), R, P<float>(db), s); });
+  }
+  int adam(std::string name, uintptr_t w, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers, size_t n, float lr,
+           float b1, float b2, float eps, float gscale, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_adam(P<float>(w), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers), n, lr, b1,
+                      b2, eps, gscale, s);
+    });
+  }
+  int step_end(std::string name, uintptr_t pd, uintptr_t pg, float b1d, float b2d, float b1g, float b2g,
+               uintptr_t step, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_step_end(P<float>(pd), P<float>(pg), b1d, b2d, b1g, b2g, P<unsigned long long>(step), s);
+    });
+  }
+  int pack(std::string name, uintptr_t src, int T, int A, int Bd, uintptr_t nat, uintptr_t tr, int st, int sb, int sa,
+           int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_pack(P<const float>(src), T, A, Bd, P<bf16>(nat), P<bf16>(tr), st, sb, sa, s);
+    });
+  }
+  int philox_uniform(std::string name, uintptr_t out, size_t n, uint64_t seed, uintptr_t step, uint64_t stream_id,
+                     float lo, float hi, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_philox_uniform(P<float>(out), n, seed, P<const unsigned long long>(step), stream_id, lo, hi, s);
+    });
+  }
+  int im2col_s2(std::string name, uintptr_t src, uintptr_t dst, int Bn, int H, int W, int C, int Ho, int Wo, int pl_y,
+                int pl_x, int Kpad, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_im2col_s2(P<const bf16>(src), P<bf16>(dst), Bn, H, W, C, Ho, Wo, pl_y, pl_x, Kpad, s);
+    });
+  }
+  int cast_to_bf16(std::string name, uintptr_t src, int src_dtype, uintptr_t dst, size_t n, float scale, float shift,
+                   int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_cast_to_bf16(P<const void>(src), src_dtype, P<bf16>(dst), n, scale, shift, s);
+    });
+  }
+  int cast_bf16_f32(std::string name, uintptr_t src, uintptr_t dst, size_t n, int stream) {
+    return add(name, stream, [=](hipStream_t s) { return dcg_cast_bf16_f32(P<const bf16>(src), P<float>(dst), n, s); });
+  }
+  int splitk_reduce(std::string name, uintptr_t src, int splits, size_t n, uintptr_t dst, float scale, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return dcg_splitk_reduce(P<const float>(src), splits, n, P<float>(dst), scale, s);
+    });
+  }
+
+ private:
+  int add(const std::string& name, int stream, std::function<int(hipStream_t)> fn) {
+    ops_.push_back(Op{name, stream, std::move(fn)});
+    return (int)ops_.size() - 1;
+  }
+  std::vector<Op> ops_;
+  std::vector<void*> dev_allocs_;
+  std::vector<hipEvent_t> events_;
+  int last_mtiles_ = 0, last_nphases_ = 0;
+};
+
+static py::tuple igemm_tile(int cfg) {
+  int bm = 0, bn = 0;
+  if (dcg_igemm_tile(cfg, &bm, &bn)) throw std::runtime_error("bad cfg");
+  return py::make_tuple(bm, bn);
+}
+static py::tuple wgrad_tile(int cfg) {
+  int bm = 0, bn = 0;
+  if (dcg_wgrad_tile(cfg, &bm, &bn)) throw std::runtime_error("bad cfg");
+  return py::make_tuple(bm, bn);
+}
+
+static std::string device_arch() {
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess) return "";
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return "";
+  return std::string(prop.gcnArchName);
+}
+
+PYBIND11_MODULE(_dcgan_hip, m) {
+  m.doc() = "gfx950 (MI355X) kernel library + recorded launch programs for the DCGAN framework";
+  m.def("igemm_tile", &igemm_tile);
+  m.def("wgrad_tile", &wgrad_tile);
+  m.def("device_arch", &device_arch);
+  m.attr("built_for") = "gfx950";
+  py::class_<Program>(m, "Program")
+      .def(py::init<>())
+      .def("size", &Program::size)
+      .def("name", &Program::name)
+      .def("run", &Program::run, py::arg("streams"), py::arg("begin") = 0, py::arg("end") = -1)
+      .def("new_event", &Program::new_event)
+      .def("record", &Program::record)
+      .def("wait", &Program::wait)
+      .def("memset", &Program::memset)
+      .def("copy", &Program::copy)
+      .def("igemm", &Program::igemm)
+      .def("last_mtiles", &Program::last_mtiles)
+      .def("last_nphases", &Program::last_nphases)
+      .def("wgrad", &Program::wgrad)
+      .def("colstats", &Program::colstats)
+      .def("bn_finalize", &Program::bn_finalize)
+      .def("bn_coef_eval", &Program::bn_coef_eval)
+      .def("bn_apply_act", &Program::bn_apply_act)
+      .def("bn_bwd_finalize", &Program::bn_bwd_finalize)
+      .def("bn_bwd_apply", &Program::bn_bwd_apply)
+      .def("act_bwd", &Program::act_bwd)
+      .def("sum_partials", &Program::sum_partials)
+      .def("colsum_small", &Program::colsum_small)
+      .def("gan_loss", &Program::gan_loss)
+      .def("linear_fwd", &Program::linear_fwd)
+      .def("linear_wgrad", &Program::linear_wgrad)
+      .def("gemv_head", &Program::gemv_head)
+      .def("head_dgrad", &Program::head_dgrad)
+      .def("head_wgrad", &Program::head_wgrad)
+      .def("adam", &Program::adam)
+      .def("step_end", &Program::step_end)
+      .def("pack", &Program::pack)
+      .def("philox_uniform", &Program::philox_uniform)
+      .def("im2col_s2", &Program::im2col_s2)
+      .def("cast_to_bf16", &Program::cast_to_bf16)
+      .def("cast_bf16_f32", &Program::cast_bf16_f32)
+      .def("splitk_reduce", &Program::splitk_reduce);
+}

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Build the native extensions in-tree (no JIT cache, no hipify, gfx950 only).
+
+* ``_dcgan_hip``: the HIP kernel library (csrc/hip/*.hip, hipcc --offload-arch=gfx950) +
+  pybind11 bindings of the recorded launch ``Program`` (csrc/bindings.cpp).
+* ``_dcgan_host``: host-side C++ runtime -- TFRecord reader/writer (CRC32C), tf.train.Example
+  parsing, multi-threaded shuffling loader with a pinned ring buffer (csrc/host/*.cpp).
+
+Objects are cached in build/ keyed by source mtime; the .so files land next to the Python
+package so they travel with the repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "distributed_tensorflow_for_dcgan_amd")
+BUILD = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("DCGAN_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes():
+    import pybind11
+    return [pybind11.get_include(), sysconfig.get_paths()["include"]]
+
+
+def _newer(src_list, dst) -> bool:
+    if not os.path.exists(dst):
+        return True
+    t = os.path.getmtime(dst)
+    return any(os.path.getmtime(s) > t for s in src_list)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed (%d): %s\n%s" % (r.returncode, " ".join(cmd), r.stdout))
+    return r.stdout
+
+
+def build_hip(verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hdrs = [os.path.join(CSRC, "hip", h) for h in os.listdir(os.path.join(CSRC, "hip")) if h.endswith(".h")]
+    srcs = sorted(os.path.join(CSRC, "hip", f) for f in os.listdir(os.path.join(CSRC, "hip")) if f.endswith(".hip"))
+    common = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC]
+    jobs_list = []
+    objs = []
+    for s in srcs:
+        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer([s] + hdrs, o):
+            jobs_list.append([HIPCC] + common + ["-c", s, "-o", o])
+    binding = os.path.join(CSRC, "bindings.cpp")
+    bo = os.path.join(BUILD, "bindings.o")
+    objs.append(bo)
+    if _newer([binding] + hdrs, bo):
+        inc = []
+        for i in _py_includes():
+            inc += ["-I", i]
+        jobs_list.append([HIPCC, "-O2", "-fPIC", "-std=c++17", "-I", CSRC] + inc + ["-c", binding, "-o", bo])
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for out in ex.map(_run, jobs_list):
+            if verbose and out.strip():
+                print(out)
+    so = os.path.join(PKG, "_dcgan_hip" + _ext_suffix())
+    if _newer(objs, so):
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", so])
+    return so
+
+
+def build_host(verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hsrc = os.path.join(CSRC, "host")
+    srcs = sorted(os.path.join(hsrc, f) for f in os.listdir(hsrc) if f.endswith(".cpp"))
+    hdrs = [os.path.join(hsrc, f) for f in os.listdir(hsrc) if f.endswith(".h")]
+    so = os.path.join(PKG, "_dcgan_host" + _ext_suffix())
+    if not srcs:
+        return ""
+    if _newer(srcs + hdrs, so):
+        inc = []
+        for i in _py_includes():
+            inc += ["-I", i]
+        flags = ["-O3", "-fPIC", "-std=c++17", "-shared", "-pthread", "-I", hsrc]
+        if os.environ.get("DCGAN_HOST_SANITIZE"):
+            flags = ["-O1", "-g", "-fPIC", "-std=c++17", "-shared", "-pthread", "-I", hsrc,
+                     "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
+        _run(["g++"] + flags + inc + srcs + ["-o", so])
+    return so
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    verbose = "-v" in argv
+    built = []
+    if "--host-only" not in argv:
+        built.append(build_hip(verbose))
+    if "--hip-only" not in argv:
+        h = build_host(verbose)
+        if h:
+            built.append(h)
+    for b in built:
+        print("built", os.path.relpath(b, ROOT))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,325 @@
+// BatchNorm (TF batch_norm_with_global_normalization semantics) and
+// activation kernels for gfx950, NHWC bf16 activations, fp32 statistics.
+//
+// Forward:  conv epilogue (igemm) or bn_stats -> per-tile partial sum / sum^2
+//           -> bn_finalize (fp64 combine, biased variance, EMA update of the moving averages,
+//              scale = gamma*rsqrt(var+eps), shift = beta - mean*scale)
+//           -> bn_apply_act (y = act(x*scale + shift), 8 x bf16 per thread)
+// Backward: bn_bwd_reduce (partials of sum g and sum g*xhat, g = dy*act'(y))
+//           -> bn_bwd_finalize (d gamma, d beta into the flat fp32 gradient; per-group coefs)
+//           -> bn_bwd_apply (dx = a*g + c*x + d, bf16)
+// Every reduction is two-stage with fixed order -> bitwise deterministic, no float atomics.
+// "groups" split the rows into equal contiguous parts with independent statistics, which is
+// how D(real) and D(fake) run as one 2B batch with the reference's per-call BN statistics.
+#include "kernels.h"
+
+namespace dcg {
+
+__device__ __forceinline__ void load8(const bf16* p, float* f) {
+  const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+  const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
+}
+
+__device__ __forceinline__ void store8(bf16* p, const float* f) {
+  bf16x8 b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (bf16)f[i];
+  *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, b);
+}
+
+// ---------------------------------------------------------------- column partial sums
+// mode 0: (sum x, sum x^2)            -- BN forward statistics
+// mode 1: (sum g, sum g*xhat)         -- BN backward, g = dy*act'(y), xhat = (x-mean)*rstd
+// mode 2: (sum x, 0)                  -- plain column sums (bias gradients)
+// Block: 256 threads = (C/8) channel vectors x LANES row lanes; each block covers
+// rows_per_block rows and writes one partial row pair [2][C].
+__global__ __launch_bounds__(256) void colstats_kernel(int mode, const bf16* __restrict__ x,
+                                                       const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       int act, float leak, int R, int C, int rows_per_block,
+                                                       int rows_per_group, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int CV = C / 8;
+  const int lanes = 256 / CV;  // row lanes (C <= 2048)
+  const int cv = threadIdx.x % CV, rl = threadIdx.x / CV;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(R, r0 + rows_per_block);
+  const int g = r0 / rows_per_group;
+  float s[8], s2[8], mu[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; s2[i] = 0.f; mu[i] = 0.f; rs[i] = 0.f; }
+  if (mode == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { mu[i] = mean[g * C + cv * 8 + i]; rs[i] = rstd[g * C + cv * 8 + i]; }
+  }
+  if (rl < lanes) {
+    for (int r = r0 + rl; r < r1; r += lanes) {
+      float xv[8];
+      load8(x + (size_t)r * C + cv * 8, xv);
+      if (mode == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { s[i] += xv[i]; s2[i] += xv[i] * xv[i]; }
+      } else if (mode == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[i] += xv[i];
+      } else {
+        float dv[8], yv[8];
+        load8(dy + (size_t)r * C + cv * 8, dv);
+        load8(y + (size_t)r * C + cv * 8, yv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float gv = dv[i] * act_grad_from_out(yv[i], act, leak);
+          s[i] += gv;
+          s2[i] += gv * (xv[i] - mu[i]) * rs[i];
+        }
+      }
+    }
+  }
+  // reduce over row lanes through LDS: red[lanes][C][2]
+  if (rl < lanes) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(rl * C + cv * 8 + i) * 2 + 0] = s[i];
+      red[(rl * C + cv * 8 + i) * 2 + 1] = s2[i];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes; ++l) { a += red[(l * C + c) * 2]; b += red[(l * C + c) * 2 + 1]; }
+    part[(size_t)blockIdx.x * 2 * C + c] = a;
+    part[(size_t)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
+// ---------------------------------------------------------------- BN forward finalize
+// part: [P][2][C], partials of group g are [g*ppg, (g+1)*ppg). count = rows per group.
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int ppg, int groups, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                   float* __restrict__ scale_out, float* __restrict__ shift_out,
+                                   float* __restrict__ ema_mean, float* __restrict__ ema_var, float decay) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= groups * C) return;
+  const int g = idx / C, c = idx - g * C;
+  double s = 0.0, s2 = 0.0;
+  for (int p = g * ppg; p < (g + 1) * ppg; ++p) {
+    s += (double)part[(size_t)p * 2 * C + c];
+    s2 += (double)part[(size_t)p * 2 * C + C + c];
+  }
+  const double m = s / count;
+  double v = s2 / count - m * m;
+  if (v < 0.0) v = 0.0;
+  const float mf = (float)m, vf = (float)v;
+  const float r = rsqrtf(vf + eps);
+  mean_out[idx] = mf;
+  rstd_out[idx] = r;
+  const float sc = gamma[c] * r;
+  scale_out[idx] = sc;
+  shift_out[idx] = beta[c] - mf * sc;
+  if (ema_mean) {
+    // TF ExponentialMovingAverage: shadow -= (1 - decay) * (shadow - value), slot = group
+    const float a = 1.f - decay;
+    ema_mean[idx] -= a * (ema_mean[idx] - mf);
+    ema_var[idx] -= a * (ema_var[idx] - vf);
+  }
+}
+
+// inference-mode BN coefficients from moving averages (sampler, distriubted_model.py:46-47)
+__global__ void bn_coef_eval_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    float eps, const float* __restrict__ mean, const float* __restrict__ var,
+                                    float debias, float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float m = mean[c] * debias, v = var[c] * debias;
+  const float sc = gamma[c] * rsqrtf(v + eps);
+  scale_out[c] = sc;
+  shift_out[c] = beta[c] - m * sc;
+}
+
+// ---------------------------------------------------------------- BN apply + activation
+__global__ __launch_bounds__(256) void bn_apply_act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int R, int C,
+                                                           int rows_per_group, int act, float leak) {
+  const size_t nv = (size_t)R * C / 8;
+  for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
+    const size_t e = v * 8;
+    const int r = (int)(e / C), c = (int)(e - (size_t)r * C);
+    const int g = r / rows_per_group;
+    float xv[8];
+    load8(x + e, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      xv[i] = apply_act(xv[i] * scale[g * C + c + i] + shift[g * C + c + i], act, leak);
+    store8(y + e, xv);
+  }
+}
+
+// ---------------------------------------------------------------- BN backward finalize
+// part: [P][2][C] (sum g, sum g*xhat). Writes dgamma/dbeta (sum over groups) when non-null and
+// the per-(group, channel) affine coefficients of dx = A*g + Bc*x + D.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int ppg, int groups, int C, float count,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float dg = 0.f, db = 0.f;
+  for (int g = 0; g < groups; ++g) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int p = g * ppg; p < (g + 1) * ppg; ++p) {
+      s1 += part[(size_t)p * 2 * C + c];
+      s2 += part[(size_t)p * 2 * C + C + c];
+    }
+    dg += s2;
+    db += s1;
+    const float r = rstd[g * C + c], mu = mean[g * C + c];
+    const float a = gamma[c] * r;
+    const float c2 = -a * s2 / count;  // multiplies xhat
+    const float b = -a * s1 / count;
+    coef[(g * C + c) * 3 + 0] = a;
+    coef[(g * C + c) * 3 + 1] = c2 * r;             // * x
+    coef[(g * C + c) * 3 + 2] = b - c2 * mu * r;    // constant
+  }
+  if (dgamma) dgamma[c] = dg;
+  if (dbeta) dbeta[c] = db;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                           const bf16* __restrict__ x,
+                                                           const float* __restrict__ coef, bf16* __restrict__ dx,
+                                                           int R, int C, int rows_per_group, int act, float leak) {
+  const size_t nv = (size_t)R * C / 8;
+  for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
+    const size_t e = v * 8;
+    const int r = (int)(e / C), c = (int)(e - (size_t)r * C);
+    const int g = r / rows_per_group;
+    float dv[8], yv[8], xv[8];
+    load8(dy + e, dv);
+    load8(y + e, yv);
+    load8(x + e, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float* cf = coef + (g * C + c + i) * 3;
+      const float gv = dv[i] * act_grad_from_out(yv[i], act, leak);
+      dv[i] = cf[0] * gv + cf[1] * xv[i] + cf[2];
+    }
+    store8(dx + e, dv);
+  }
+}
+
+// ---------------------------------------------------------------- activation backward (no BN)
+// dx = dy * act'(y); n elements (any count), scalar tail
+__global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                      bf16* __restrict__ dx, size_t n, int act, float leak) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dx[i] = (bf16)((float)dy[i] * act_grad_from_out((float)y[i], act, leak));
+}
+
+// sum over partial rows -> dst[C]
+__global__ void sum_partials_kernel(const float* __restrict__ part, int P, int stride, int C, float* __restrict__ dst) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * stride + c];
+  dst[c] = s;
+}
+
+// column sums for a small channel count (C <= 16), e.g. dbias of a 3-channel image gradient
+__global__ __launch_bounds__(256) void colsum_small_kernel(const bf16* __restrict__ x, int R, int C,
+                                                           float* __restrict__ part) {
+  __shared__ float red[256][17];
+  float s[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = 0.f;
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < R; r += gridDim.x * 256)
+    for (int c = 0; c < C; ++c) s[c] += (float)x[(size_t)r * C + c];
+  for (int c = 0; c < C; ++c) red[threadIdx.x][c] = s[c];
+  __syncthreads();
+  if (threadIdx.x < C) {
+    float a = 0.f;
+    for (int t = 0; t < 256; ++t) a += red[t][threadIdx.x];
+    part[blockIdx.x * C + threadIdx.x] = a;
+  }
+}
+
+}  // namespace dcg
+
+using namespace dcg;
+
+static inline unsigned ew_blocks(size_t nvec) {
+  size_t b = (nvec + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (unsigned)(b ? b : 1);
+}
+
+extern "C" int dcg_colstats(int mode, const bf16* x, const bf16* dy, const bf16* y, const float* mean,
+                            const float* rstd, int act, float leak, int R, int C, int rows_per_block,
+                            int rows_per_group, float* part, hipStream_t s) {
+  if (C % 8 || C > 2048) return -2;
+  const int P = (R + rows_per_block - 1) / rows_per_block;
+  const int lanes = 256 / (C / 8);
+  const size_t shm = (size_t)lanes * C * 2 * sizeof(float);
+  hipLaunchKernelGGL(colstats_kernel, dim3(P), dim3(256), shm, s, mode, x, dy, y, mean, rstd, act, leak, R, C,
+                     rows_per_block, rows_per_group, part);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_bn_finalize(const float* part, int ppg, int groups, int C, double count, const float* gamma,
+                               const float* beta, float eps, float* mean, float* rstd, float* scale, float* shift,
+                               float* ema_mean, float* ema_var, float decay, hipStream_t s) {
+  const int n = groups * C;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, ppg, groups, C, count, gamma,
+                     beta, eps, mean, rstd, scale, shift, ema_mean, ema_var, decay);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_bn_coef_eval(int C, const float* gamma, const float* beta, float eps, const float* mean,
+                                const float* var, float debias, float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_coef_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, eps, mean, var,
+                     debias, scale, shift);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_bn_apply_act(const bf16* x, bf16* y, const float* scale, const float* shift, int R, int C,
+                                int rows_per_group, int act, float leak, hipStream_t s) {
+  if (C % 8) return -2;
+  hipLaunchKernelGGL(bn_apply_act_kernel, dim3(ew_blocks((size_t)R * C / 8)), dim3(256), 0, s, x, y, scale, shift,
+                     R, C, rows_per_group, act, leak);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_bn_bwd_finalize(const float* part, int ppg, int groups, int C, float count, const float* gamma,
+                                   const float* mean, const float* rstd, float* dgamma, float* dbeta, float* coef,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, ppg, groups, C, count,
+                     gamma, mean, rstd, dgamma, dbeta, coef);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_bn_bwd_apply(const bf16* dy, const bf16* y, const bf16* x, const float* coef, bf16* dx, int R,
+                                int C, int rows_per_group, int act, float leak, hipStream_t s) {
+  if (C % 8) return -2;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks((size_t)R * C / 8)), dim3(256), 0, s, dy, y, x, coef, dx,
+                     R, C, rows_per_group, act, leak);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t n, int act, float leak, hipStream_t s) {
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, dy, y, dx, n, act, leak);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_sum_partials(const float* part, int P, int stride, int C, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, stride, C, dst);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_colsum_small(const bf16* x, int R, int C, float* part, int blocks, hipStream_t s) {
+  if (C > 16) return -2;
+  hipLaunchKernelGGL(colsum_small_kernel, dim3(blocks), dim3(256), 0, s, x, R, C, part);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,90 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels of this framework.
+// Wave = 64 lanes. bf16 MFMA fragments use the v_mfma_f32_16x16x32_bf16 lane maps:
+//   A: lane l holds A[row l&15][k = 8*(l>>4) + j], j = 0..7
+//   B: lane l holds B[k = 8*(l>>4) + j][col l&15]
+//   C: lane l holds C[row 4*(l>>4) + r][col l&15], r = 0..3
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+namespace dcg {
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float apply_act(float v, int act, float leak) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LRELU: return fmaxf(v, leak * v);
+    case ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
+// derivative of the activation expressed through its OUTPUT y (valid for relu, lrelu, tanh)
+__device__ __forceinline__ float act_grad_from_out(float y, int act, float leak) {
+  switch (act) {
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_LRELU: return y > 0.f ? 1.f : leak;
+    case ACT_TANH: return 1.f - y * y;
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// 16-byte buffer load; an offset >= the descriptor's byte count returns zeros (HW range check).
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+
+constexpr uint32_t OOB = 0x80000000u;  // any offset past the descriptor size
+
+// Unsigned division by a runtime-invariant divisor (round-up multiply method, exact for all
+// 32-bit n). Host computes {mul, shift} with fastdiv_make().
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  if (f.d == 1) return n;
+  uint32_t t = __umulhi(n, f.mul);
+  return (t + ((n - t) >> 1)) >> f.shr;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace dcg
+
+// host helper
+static inline dcg::FastDiv fastdiv_make(uint32_t d) {
+  dcg::FastDiv f;
+  f.d = d;
+  if (d <= 1) { f.mul = 0; f.shr = 0; f.d = 1; return f; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  // mul = floor(2^32 * (2^l - d) / d) + 1
+  uint64_t m = ((((uint64_t)1 << l) - d) << 32) / d + 1;
+  f.mul = (uint32_t)m;
+  f.shr = l - 1;
+  return f;
+}

@@ -1,0 +1,271 @@
+// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC, bf16 in / fp32 acc.
+//
+// One kernel family covers every conv-shaped op of the DCGAN step:
+//   * TF-'SAME' stride-2 5x5 conv (D forward, G dgrad)          mode "conv":   25 taps, sstride 2
+//   * TF-'SAME' stride-2 5x5 conv_transpose (G forward, D dgrad) mode "deconv": sub-pixel phase
+//     decomposition -> 4 dense convs with 3x3 / 3x2 / 2x3 / 2x2 taps (no zero-insertion, no 4x
+//     wasted MACs); the phase is blockIdx.z and each phase scatters to its output pixels.
+//   * plain GEMM C[M][N] = A[M][K] . Bt[N][K]                    mode "plain" (im2col'd 3-channel
+//     layers, 1 tap).
+// GEMM view: rows m = output pixels of one phase, cols n = output channels, k = (tap, channel).
+// Weights are pre-packed bf16 [25][N][Kc] (k contiguous per output channel), so both operands
+// are "K-contiguous rows" and every fragment is one 16-byte ds_read_b128.
+//
+// Block = 256 threads (4 waves, WM x WN wave grid), tile BM x BN x 64. Register-staged double
+// buffer: the next K-tile's global loads are issued before the current tile's MFMAs and written
+// to the other LDS buffer after them (one barrier per K-tile). LDS rows are 128 B with a
+// chunk ^= (row & 7) XOR swizzle (conflict-free ds_read_b128 for the 16x16x32 A/B maps).
+// A-operand gathers use buffer loads whose out-of-range offset returns zeros, which implements
+// the conv zero padding with no branches.
+//
+// Fused epilogue: + bias, per-channel BN partial statistics (sum, sum of squares over the
+// tile's rows, written per (M-tile, phase) for a deterministic finalize), activation
+// (relu / lrelu / tanh), bf16 or fp32 store with the phase's pixel scatter, optional channel
+// offset (writes into a slice of a wider tensor).
+#include "kernels.h"
+
+namespace dcg {
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_CH = BM * 8, B_CH = BN * 8;
+  constexpr int A_PT = (A_CH + 255) / 256, B_PT = (B_CH + 255) / 256;
+  constexpr int STAGE = (BM + BN) * 8;  // 16-byte units per stage
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(FM >= 1 && FN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) u32x4 lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int phase = blockIdx.z;
+  const IGemmPhase* ph = p.ph + phase;
+  const int M = ph->M;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if (m0 >= M) {  // phase with fewer rows (odd output sizes): its stats slot must still be defined
+    if (p.stats) {
+      float* dst = p.stats + (size_t)(blockIdx.x * p.nphases + phase) * 2 * p.N;
+      for (int nl = threadIdx.x; nl < BN; nl += 256)
+        if (n0 + nl < p.N) { dst[n0 + nl] = 0.f; dst[p.N + n0 + nl] = 0.f; }
+    }
+    return;
+  }
+  const int Kc = p.Kc, N = p.N;
+  const int ntaps = p.plain ? 1 : ph->ntaps;
+  const int kt_per_tap = (Kc + BK - 1) / BK;
+  const int KT = ntaps * kt_per_tap;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, p.b_bytes);
+
+  // ---- per-thread A rows (fixed for the whole K loop)
+  int a_bh[A_PT], a_iy[A_PT], a_ix[A_PT];
+  bool a_ok[A_PT];
+  const int chunk = tid & 7;
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i) {
+    const int r = (tid + 256 * i) >> 3;
+    const int m = m0 + r;
+    a_ok[i] = (r < BM) && (m < M);
+    if (p.plain) {
+      a_bh[i] = m; a_iy[i] = 0; a_ix[i] = 0;
+    } else {
+      const uint32_t b = fdiv((uint32_t)m, ph->fd_hw);
+      const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph->Hq * ph->Wq);
+      const uint32_t qy = fdiv(rem, ph->fd_w);
+      const uint32_t qx = rem - qy * (uint32_t)ph->Wq;
+      a_bh[i] = (int)b * p.H;
+      a_iy[i] = (int)qy * p.sstride + ph->iy0_off;
+      a_ix[i] = (int)qx * p.sstride + ph->ix0_off;
+    }
+  }
+
+  u32x4 ra_reg[A_PT], rb_reg[B_PT];
+
+  auto load_tile = [&](int kt) {
+    const int ti = kt / kt_per_tap;
+    const int c0 = (kt - ti * kt_per_tap) * BK;
+    const int cc = c0 + chunk * 8;
+    const bool kval = cc < Kc;
+    int dy = 0, dx = 0, wt = 0;
+    if (!p.plain) { dy = ph->dy[ti]; dx = ph->dx[ti]; wt = ph->wtap[ti]; }
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      uint32_t off = OOB;
+      if (p.plain) {
+        if (a_ok[i] && kval) off = (uint32_t)(a_bh[i] * Kc + cc) * 2u;
+      } else {
+        const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
+        if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+          off = (uint32_t)(((a_bh[i] + iy) * p.W + ix) * Kc + cc) * 2u;
+      }
+      ra_reg[i] = buf_load16(ra, off);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) {
+      const int r = (tid + 256 * i) >> 3;
+      const int n = n0 + r;
+      uint32_t off = OOB;
+      if (r < BN && n < N && kval) off = (uint32_t)((wt * N + n) * Kc + cc) * 2u;
+      rb_reg[i] = buf_load16(rb, off);
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    u32x4* sa = lds + buf * STAGE;
+    u32x4* sb = sa + BM * 8;
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int r = (tid + 256 * i) >> 3;
+      if (A_CH % 256 == 0 || r < BM) sa[r * 8 + (chunk ^ (r & 7))] = ra_reg[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) {
+      const int r = (tid + 256 * i) >> 3;
+      if (B_CH % 256 == 0 || r < BN) sb[r * 8 + (chunk ^ (r & 7))] = rb_reg[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) load_tile(kt + 1);
+    const u32x4* sa = lds + buf * STAGE;
+    const u32x4* sb = sa + BM * 8;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+      const int c = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16 + fr;
+        af[i] = __builtin_bit_cast(bf16x8, sa[r * 8 + (c ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * TN + j * 16 + fr;
+        bfr[j] = __builtin_bit_cast(bf16x8, sb[r * 8 + (c ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  // output row offsets (elements) for the BM rows of this tile, via LDS
+  int* rowoff = reinterpret_cast<int*>(lds);
+  float* red = reinterpret_cast<float*>(lds) + BM;  // [WM][BN][2]
+  for (int r = tid; r < BM; r += 256) {
+    const int m = m0 + r;
+    int off = -1;
+    if (m < M) {
+      if (p.plain) {
+        off = m * p.ldc;
+      } else {
+        const uint32_t b = fdiv((uint32_t)m, ph->fd_hw);
+        const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph->Hq * ph->Wq);
+        const uint32_t qy = fdiv(rem, ph->fd_w);
+        const uint32_t qx = rem - qy * (uint32_t)ph->Wq;
+        const int y = (int)qy * p.ostride + ph->oy_off, x = (int)qx * p.ostride + ph->ox_off;
+        off = (((int)b * p.outH + y) * p.outW + x) * p.ldc;
+      }
+    }
+    rowoff[r] = off;
+  }
+  __syncthreads();
+
+  const bool do_stats = p.stats != nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = wn * TN + j * 16 + fr;
+    const int n = n0 + nl;
+    const bool nok = n < N;
+    const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
+    float s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ml = wm * TM + i * 16 + fq * 4 + r;
+        const int off = rowoff[ml];
+        const float v = acc[i][j][r] + bv;
+        if (off >= 0 && nok) {
+          s += v;
+          s2 += v * v;
+          const float o = apply_act(v, p.act, p.leak);
+          if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
+          else reinterpret_cast<bf16*>(p.C)[off + p.cofs + n] = f2bf(o);
+        }
+      }
+    }
+    if (do_stats) {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (fq == 0) {
+        red[(wm * BN + nl) * 2 + 0] = s;
+        red[(wm * BN + nl) * 2 + 1] = s2;
+      }
+    }
+  }
+  if (do_stats) {
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += 256) {
+      const int n = n0 + nl;
+      if (n >= N) continue;
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s += red[(w * BN + nl) * 2 + 0];
+        s2 += red[(w * BN + nl) * 2 + 1];
+      }
+      float* dst = p.stats + (size_t)(blockIdx.x * p.nphases + phase) * 2 * N;
+      dst[n] = s;
+      dst[N + n] = s2;
+    }
+  }
+}
+
+}  // namespace dcg
+
+// ---------------------------------------------------------------------------- host launch
+// Tile configurations (BM, BN, WM, WN); the engine picks one per layer.
+#define DCG_IGEMM_CONFIGS(X) \
+  X(0, 128, 128, 2, 2) X(1, 128, 64, 2, 2) X(2, 64, 128, 2, 2) X(3, 64, 64, 2, 2) \
+  X(4, 32, 64, 2, 2) X(5, 64, 32, 2, 2) X(6, 32, 32, 2, 2) X(7, 128, 16, 4, 1) \
+  X(8, 64, 16, 4, 1) X(9, 256, 64, 4, 1)
+
+extern "C" int dcg_igemm_tile(int cfg, int* bm, int* bn) {
+#define X(id, BM_, BN_, WM_, WN_) if (cfg == id) { *bm = BM_; *bn = BN_; return 0; }
+  DCG_IGEMM_CONFIGS(X)
+#undef X
+  return -1;
+}
+
+extern "C" int dcg_igemm_launch(const dcg::IGemmArgs* a, int cfg, int mtiles, int ntiles, hipStream_t s) {
+  dim3 grid(mtiles, ntiles, a->nphases);
+#define X(id, BM_, BN_, WM_, WN_) \
+  if (cfg == id) { hipLaunchKernelGGL((dcg::igemm_kernel<BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, *a); \
+                   return (int)hipGetLastError(); }
+  DCG_IGEMM_CONFIGS(X)
+#undef X
+  return -1;
+}

@@ -1,0 +1,429 @@
+// Small fused kernels of the DCGAN step for gfx950:
+//   * BCE-with-logits, all 3 reference losses + both logit gradients in ONE kernel (K15/K16)
+//   * linear layers: G projection z->h0 (K1), its weight gradient (K2), D's 1-output head
+//     (GEMV) and its gradients
+//   * TF-form Adam over a flat fp32 buffer + device-side beta powers (K17, graph-capturable)
+//   * bf16 weight packing (natural + per-tap transposed / im2col-ordered copies)
+//   * Philox-4x32-10 z ~ U(-1,1) keyed by a device step counter (K19, graph-capturable)
+//   * stride-2 TF-SAME im2col for 3-channel tensors, dtype casts
+#include "kernels.h"
+
+namespace dcg {
+
+// ---------------------------------------------------------------- losses
+// logits: [2B] (real rows first). out[0..3] = d_loss_real, d_loss_fake, g_loss, d_loss;
+// dl_d[2B] = d d_loss / d logit; dl_g[B] = d g_loss / d logit_fake; prob[2B] = sigmoid.
+__global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__ logits, int B,
+                                                       float* __restrict__ out, float* __restrict__ dl_d,
+                                                       float* __restrict__ dl_g, float* __restrict__ prob) {
+  __shared__ float red[3][256];
+  float lr = 0.f, lf = 0.f, lg = 0.f;
+  const float invB = 1.f / (float)B;
+  for (int i = threadIdx.x; i < 2 * B; i += 256) {
+    const float x = logits[i];
+    const float sp = log1pf(expf(-fabsf(x)));
+    const float sg = 1.f / (1.f + expf(-x));
+    if (prob) prob[i] = sg;
+    if (i < B) {
+      lr += fmaxf(x, 0.f) - x + sp;          // target 1
+      dl_d[i] = (sg - 1.f) * invB;
+    } else {
+      lf += fmaxf(x, 0.f) + sp;              // target 0
+      lg += fmaxf(x, 0.f) - x + sp;          // target 1 (non-saturating G loss)
+      dl_d[i] = sg * invB;
+      dl_g[i - B] = (sg - 1.f) * invB;
+    }
+  }
+  red[0][threadIdx.x] = lr;
+  red[1][threadIdx.x] = lf;
+  red[2][threadIdx.x] = lg;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float a = red[0][0] * invB, b = red[1][0] * invB, c = red[2][0] * invB;
+    out[0] = a; out[1] = b; out[2] = c; out[3] = a + b;
+  }
+}
+
+// ---------------------------------------------------------------- linear: out = z @ W + b
+// z fp32 [B][K], W fp32 [K][N], out bf16 [B][N]; block = 256 columns x RB rows
+template <int RB>
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ z, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, bf16* __restrict__ out,
+                                                         int B, int K, int N) {
+  extern __shared__ float zs[];  // [RB][K]
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int r0 = blockIdx.y * RB;
+  for (int i = threadIdx.x; i < RB * K; i += 256) {
+    const int r = i / K, k = i - r * K;
+    zs[i] = (r0 + r < B) ? z[(size_t)(r0 + r) * K + k] : 0.f;
+  }
+  __syncthreads();
+  if (n >= N) return;
+  float acc[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) acc[r] = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float w = W[(size_t)k * N + n];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k] * w;
+  }
+  const float b = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+    if (r0 + r < B) out[(size_t)(r0 + r) * N + n] = (bf16)(acc[r] + b);
+}
+
+// dW[K][N] = z^T @ dh (fp32 out), db[N] = sum_b dh; block = 256 columns x KC k-rows
+template <int KC>
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ z, const bf16* __restrict__ dh,
+                                                           float* __restrict__ dW, float* __restrict__ db, int B,
+                                                           int K, int N) {
+  extern __shared__ float zs[];  // [B][KC]
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int k0 = blockIdx.y * KC;
+  for (int i = threadIdx.x; i < B * KC; i += 256) {
+    const int b = i / KC, k = i - b * KC;
+    zs[i] = (k0 + k < K) ? z[(size_t)b * K + k0 + k] : 0.f;
+  }
+  __syncthreads();
+  if (n >= N) return;
+  float acc[KC];
+  float sb = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) acc[k] = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float g = (float)dh[(size_t)b * N + n];
+    sb += g;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) acc[k] += zs[b * KC + k] * g;
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+    if (k0 + k < K) dW[(size_t)(k0 + k) * N + n] = acc[k];
+  if (db && blockIdx.y == 0) db[n] = sb;
+}
+
+// D head: logits[r] = sum_k x[r][k] * w[k] + b ; one wave per row, x bf16 [R][K], K % 512 == 0
+__global__ __launch_bounds__(256) void gemv_head_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ b, float* __restrict__ out, int R,
+                                                        int K) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wave >= R) return;
+  float s = 0.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)wave * K + k);
+    const bf16x8 xb = __builtin_bit_cast(bf16x8, v);
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + k);
+    const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + k + 4);
+    s += (float)xb[0] * w0[0] + (float)xb[1] * w0[1] + (float)xb[2] * w0[2] + (float)xb[3] * w0[3] +
+         (float)xb[4] * w1[0] + (float)xb[5] * w1[1] + (float)xb[6] * w1[2] + (float)xb[7] * w1[3];
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[wave] = s + b[0];
+}
+
+// dx[r][k] = dl[r] * w[k] (bf16), 8 per thread
+__global__ __launch_bounds__(256) void head_dgrad_kernel(const float* __restrict__ dl, const float* __restrict__ w,
+                                                         bf16* __restrict__ dx, int R, int K) {
+  const size_t nv = (size_t)R * K / 8;
+  for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
+    const size_t e = v * 8;
+    const int r = (int)(e / K), k = (int)(e - (size_t)r * K);
+    const float g = dl[r];
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)(g * w[k + i]);
+    *reinterpret_cast<u32x4*>(dx + e) = __builtin_bit_cast(u32x4, o);
+  }
+}
+
+// head weight-grad partials: part[split][K] = sum_{r in split} x[r][k] * dl[r]
+__global__ __launch_bounds__(256) void head_wgrad_kernel(const bf16* __restrict__ x, const float* __restrict__ dl,
+                                                         float* __restrict__ part, int R, int K, int rows_per_split) {
+  const int k8 = blockIdx.x * 256 + threadIdx.x;
+  const int split = blockIdx.y;
+  if (k8 * 8 >= K) return;
+  float s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = 0.f;
+  const int r0 = split * rows_per_split, r1 = min(R, r0 + rows_per_split);
+  for (int r = r0; r < r1; ++r) {
+    const float g = dl[r];
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)r * K + k8 * 8);
+    const bf16x8 xb = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += (float)xb[i] * g;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) part[(size_t)split * K + k8 * 8 + i] = s[i];
+}
+
+// db = sum dl (single block)
+__global__ void sum_vec_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// ---------------------------------------------------------------- TF Adam
+// lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from device powers (= b^t); w -= lr_t*m/(sqrt(v)+eps)
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   const float* __restrict__ powers, size_t n, float lr,
+                                                   float b1, float b2, float eps, float gscale) {
+  const float lr_t = lr * sqrtf(1.f - powers[1]) / (1.f - powers[0]);
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i] * gscale;
+    f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+    f32x4 wv = reinterpret_cast<f32x4*>(w)[i];
+    mv = b1 * mv + (1.f - b1) * gv;
+    vv = b2 * vv + (1.f - b2) * gv * gv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wv[k] -= lr_t * mv[k] / (sqrtf(vv[k]) + eps);
+    reinterpret_cast<f32x4*>(m)[i] = mv;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+    reinterpret_cast<f32x4*>(w)[i] = wv;
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float gv = g[i] * gscale;
+    m[i] = b1 * m[i] + (1.f - b1) * gv;
+    v[i] = b2 * v[i] + (1.f - b2) * gv * gv;
+    w[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps);
+  }
+}
+
+// after both Adams: beta powers *= beta (TF variable update) and the global step counter
+__global__ void step_end_kernel(float* __restrict__ pd, float* __restrict__ pg, float b1d, float b2d, float b1g,
+                                float b2g, unsigned long long* __restrict__ step) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (pd) { pd[0] *= b1d; pd[1] *= b2d; }
+    if (pg) { pg[0] *= b1g; pg[1] *= b2g; }
+    if (step) step[0] += 1ull;
+  }
+}
+
+// ---------------------------------------------------------------- weight packing
+// src fp32 [T][A][Bd] -> nat bf16 (same order, optional) and tr bf16 at t*st + b*sb + a*sa
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, int T, int A, int Bd,
+                                                   bf16* __restrict__ nat, bf16* __restrict__ tr, int st, int sb,
+                                                   int sa) {
+  const size_t n = (size_t)T * A * Bd;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float v = src[i];
+    const int b = (int)(i % Bd);
+    const size_t ta = i / Bd;
+    const int a = (int)(ta % A), t = (int)(ta / A);
+    if (nat) nat[i] = (bf16)v;
+    if (tr) tr[(size_t)t * st + (size_t)b * sb + (size_t)a * sa] = (bf16)v;
+  }
+}
+
+// ---------------------------------------------------------------- Philox z ~ U(-1, 1)
+__device__ __forceinline__ void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                             uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+  const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+  const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+  c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+}
+
+__global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__ out, size_t n, uint64_t seed,
+                                                             const unsigned long long* __restrict__ step,
+                                                             uint64_t stream_id, float lo, float hi) {
+  const size_t i4 = blockIdx.x * 256 + threadIdx.x;
+  if (i4 * 4 >= n) return;
+  const uint64_t st = step ? step[0] : 0ull;
+  uint32_t c0 = (uint32_t)i4, c1 = (uint32_t)(i4 >> 32), c2 = (uint32_t)st, c3 = (uint32_t)(st >> 32) ^ (uint32_t)stream_id;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c0, c1, c2, c3, k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const uint32_t c[4] = {c0, c1, c2, c3};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t idx = i4 * 4 + j;
+    if (idx < n) {
+      const float u = (float)(c[j] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+      out[idx] = lo + (hi - lo) * u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- im2col (stride 2, TF SAME)
+// src bf16 [B][H][W][C] -> dst bf16 [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad
+__global__ __launch_bounds__(256) void im2col_s2_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int B,
+                                                        int H, int W, int C, int Ho, int Wo, int pl_y, int pl_x,
+                                                        int Kpad) {
+  const int kv = Kpad / 8;
+  const size_t n = (size_t)B * Ho * Wo * kv;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const int v = (int)(i % kv);
+    const size_t row = i / kv;
+    const int ox = (int)(row % Wo);
+    const size_t t1 = row / Wo;
+    const int oy = (int)(t1 % Ho), b = (int)(t1 / Ho);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = v * 8 + j;
+      float val = 0.f;
+      if (k < 25 * C) {
+        const int tap = k / C, c = k - tap * C;
+        const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+        const int iy = 2 * oy + ky - pl_y, ix = 2 * ox + kx - pl_x;
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          val = (float)src[(((size_t)b * H + iy) * W + ix) * C + c];
+      }
+      o[j] = (bf16)val;
+    }
+    *reinterpret_cast<u32x4*>(dst + row * Kpad + v * 8) = __builtin_bit_cast(u32x4, o);
+  }
+}
+
+// ---------------------------------------------------------------- casts
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ s, bf16* __restrict__ d, size_t n) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (bf16)s[i];
+}
+__global__ __launch_bounds__(256) void cast_f64_bf16_kernel(const double* __restrict__ s, bf16* __restrict__ d, size_t n) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (bf16)(float)s[i];
+}
+__global__ __launch_bounds__(256) void cast_u8_bf16_kernel(const uint8_t* __restrict__ s, bf16* __restrict__ d, size_t n,
+                                                           float scale, float shift) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    d[i] = (bf16)((float)s[i] * scale + shift);
+}
+__global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const bf16* __restrict__ s, float* __restrict__ d, size_t n) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (float)s[i];
+}
+
+}  // namespace dcg
+
+using namespace dcg;
+
+static inline unsigned grid_for(size_t n, size_t per = 256) {
+  size_t b = (n + per - 1) / per;
+  if (b > 16384) b = 16384;
+  return (unsigned)(b ? b : 1);
+}
+
+extern "C" int dcg_gan_loss(const float* logits, int B, float* out, float* dl_d, float* dl_g, float* prob,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(gan_loss_kernel, dim3(1), dim3(256), 0, s, logits, B, out, dl_d, dl_g, prob);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_linear_fwd(const float* z, const float* W, const float* b, bf16* out, int B, int K, int N,
+                              hipStream_t s) {
+  constexpr int RB = 16;
+  dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
+  hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_linear_wgrad(const float* z, const bf16* dh, float* dW, float* db, int B, int K, int N,
+                                hipStream_t s) {
+  constexpr int KC = 20;
+  if ((size_t)B * KC * sizeof(float) > 65536) return -2;
+  dim3 grid((N + 255) / 256, (K + KC - 1) / KC);
+  hipLaunchKernelGGL((linear_wgrad_kernel<KC>), grid, dim3(256), B * KC * sizeof(float), s, z, dh, dW, db, B, K, N);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_gemv_head(const bf16* x, const float* w, const float* b, float* out, int R, int K, hipStream_t s) {
+  if (K % 512) return -2;
+  hipLaunchKernelGGL(gemv_head_kernel, dim3((R + 3) / 4), dim3(256), 0, s, x, w, b, out, R, K);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_head_dgrad(const float* dl, const float* w, bf16* dx, int R, int K, hipStream_t s) {
+  if (K % 8) return -2;
+  hipLaunchKernelGGL(head_dgrad_kernel, dim3(grid_for((size_t)R * K / 8)), dim3(256), 0, s, dl, w, dx, R, K);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_head_wgrad(const bf16* x, const float* dl, float* part, int R, int K, int splits,
+                              hipStream_t s) {
+  if (K % 8) return -2;
+  const int rps = (R + splits - 1) / splits;
+  dim3 grid((K / 8 + 255) / 256, splits);
+  hipLaunchKernelGGL(head_wgrad_kernel, grid, dim3(256), 0, s, x, dl, part, R, K, rps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_sum_vec(const float* v, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(sum_vec_kernel, dim3(1), dim3(256), 0, s, v, n, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_adam(float* w, const float* g, float* m, float* v, const float* powers, size_t n, float lr,
+                        float b1, float b2, float eps, float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, g, m, v, powers, n, lr, b1, b2,
+                     eps, gscale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_step_end(float* pd, float* pg, float b1d, float b2d, float b1g, float b2g,
+                            unsigned long long* step, hipStream_t s) {
+  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(64), 0, s, pd, pg, b1d, b2d, b1g, b2g, step);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_pack(const float* src, int T, int A, int Bd, bf16* nat, bf16* tr, int st, int sb, int sa,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(pack_kernel, dim3(grid_for((size_t)T * A * Bd)), dim3(256), 0, s, src, T, A, Bd, nat, tr, st,
+                     sb, sa);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_philox_uniform(float* out, size_t n, uint64_t seed, const unsigned long long* step,
+                                  uint64_t stream_id, float lo, float hi, hipStream_t s) {
+  hipLaunchKernelGGL(philox_uniform_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, out, n, seed, step,
+                     stream_id, lo, hi);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_im2col_s2(const bf16* src, bf16* dst, int B, int H, int W, int C, int Ho, int Wo, int pl_y,
+                             int pl_x, int Kpad, hipStream_t s) {
+  if (Kpad % 8) return -2;
+  hipLaunchKernelGGL(im2col_s2_kernel, dim3(grid_for((size_t)B * Ho * Wo * (Kpad / 8))), dim3(256), 0, s, src, dst,
+                     B, H, W, C, Ho, Wo, pl_y, pl_x, Kpad);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_cast_to_bf16(const void* src, int src_dtype, bf16* dst, size_t n, float scale, float shift,
+                                hipStream_t s) {
+  // src_dtype: 0 f32, 1 f64, 2 u8 (x*scale+shift)
+  if (src_dtype == 0)
+    hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const float*)src, dst, n);
+  else if (src_dtype == 1)
+    hipLaunchKernelGGL(cast_f64_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const double*)src, dst, n);
+  else if (src_dtype == 2)
+    hipLaunchKernelGGL(cast_u8_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const uint8_t*)src, dst, n, scale,
+                       shift);
+  else
+    return -2;
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_cast_bf16_f32(const bf16* src, float* dst, size_t n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n);
+  return (int)hipGetLastError();
+}

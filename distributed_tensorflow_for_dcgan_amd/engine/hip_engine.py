@@ -1,0 +1,642 @@
+"""Fused HIP training engine: the whole reference DCGAN step on hand-written gfx950 kernels.
+
+The step (``image_train.py:151-158`` semantics) is recorded ONCE into
+native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buffers, then
+replayed every step -- optionally captured into hipGraphs so a step is a handful of graph
+launches:
+
+  segment A  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
+             2B batch [real | fake] with per-half BN statistics (= the reference's two
+             D calls) -> fused 3-loss BCE -> D backward of d_loss (both halves; D grads final)
+  [DDP]      D-gradient all-reduce starts on the comm stream ...
+  segment B  ... while the g_loss chain runs back through D(fake) (pre-update D weights) into
+             G's backward (G grads final)
+  [DDP]      G-gradient all-reduce
+  segment C  TF-Adam(D), TF-Adam(G) (device beta powers, 1/W folded in), step counter,
+             bf16 re-pack of the updated conv weights for the next step's kernels
+
+Layouts: activations NHWC bf16; master weights fp32 in TF layout inside the flat
+``ParamSet`` buffers (what the checkpoint writes and DDP reduces); each conv weight also
+has bf16 copies packed for the implicit-GEMM kernels ([25][N][Kc]: natural and per-tap
+transposed, or an im2col-ordered [N][80] matrix for the 3-channel layers).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from ..models.config import DCGANConfig, same_pads
+from ..models.dcgan import DCGAN
+from ..optim.adam import TFAdam
+from ..ops import hip as H
+from ..parallel import dist as D
+
+RELU, LRELU, TANH, NONE = 1, 2, 3, 0
+
+
+def _p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _kpad(c: int) -> int:
+    return -(-25 * c // 16) * 16
+
+
+class HipEngine:
+    name = "hip"
+    dtype_name = "bf16"
+
+    def __init__(self, cfg: DCGANConfig, batch_size: int, device: torch.device, dtype: str = "bf16",
+                 seed: int = 0, lr: float = 2e-4, beta1: float = 0.5, zero_debias: bool = False, rank: int = 0,
+                 world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 8.0,
+                 **_):
+        if dtype != "bf16":
+            raise ValueError("the HIP engine computes in bf16 (fp32 master weights / statistics)")
+        if device.type != "cuda":
+            raise ValueError("HipEngine needs a GPU")
+        self.ext = H.ext()
+        self.cfg = cfg
+        self.B = int(batch_size)
+        self.device = device
+        self.rank, self.world = rank, world
+        self.seed = int(seed)
+        self.lr, self.beta1 = float(lr), float(beta1)
+        self.model = DCGAN(cfg, device=device, seed=seed, zero_debias=zero_debias)
+        if world > 1:
+            D.broadcast_tensors([self.model.g.flat, self.model.d.flat, self.model.g_bn.flat, self.model.d_bn.flat])
+        self.opt_d = TFAdam(self.model.d, lr, beta1, power_suffix="")
+        self.opt_g = TFAdam(self.model.g, lr, beta1, power_suffix="_1")
+        self.opt_d.use_hip = self.opt_g.use_hip = True
+        self.grad_d = self.model.d.like()
+        self.grad_g = self.model.g.like()
+        self._step_host = 0
+        self.step_counter = torch.zeros(1, dtype=torch.int64, device=device)  # device global step
+        self.graph_requested = bool(graph)
+        self.graph_enabled = False
+        self._graphs: List[Optional[torch.cuda.CUDAGraph]] = []
+        self.comm_stream = torch.cuda.Stream(device=device) if world > 1 else None
+        self.allreduce_dtype = allreduce_dtype
+        self.bucket_mb = bucket_mb
+        self._alloc()
+        self._build()
+        self._repack_weights_now()
+
+    # ------------------------------------------------------------------ buffers
+    def _t(self, *shape, dtype=torch.bfloat16, zero=False):
+        f = torch.zeros if zero else torch.empty
+        return f(*shape, dtype=dtype, device=self.device)
+
+    def _alloc(self):
+        cfg, B = self.cfg, self.B
+        B2 = 2 * B
+        s = cfg.output_size
+        self.gl = cfg.g_layers()
+        self.dl = cfg.d_layers()
+        t = self._t
+        self.z = t(B, cfg.z_dim, dtype=torch.float32)
+        self.sample_z = t(B, cfg.z_dim, dtype=torch.float32)
+        # ---------------- G
+        self.g_h0_pre = t(B, cfg.g_lin_out)
+        self.g_h0 = t(B, cfg.g_lin_out)
+        self.g_x = {}   # pre-BN deconv outputs
+        self.g_a = {}   # activations (post BN+ReLU)
+        for L in self.gl[:-1]:
+            self.g_x[L.name] = t(B, L.out_hw, L.out_hw, L.cout)
+            self.g_a[L.name] = t(B, L.out_hw, L.out_hw, L.cout)
+        # ---------------- D input [real | fake]
+        self.d_in = t(B2, s, s, cfg.c_dim, zero=True)
+        self.real_src = t(B, s, s, cfg.c_dim)
+        self.fake = self.d_in[B:]
+        self.d_x, self.d_a = {}, {}
+        for i, L in enumerate(self.dl):
+            if L.bn:
+                self.d_x[L.name] = t(B2, L.out_hw, L.out_hw, L.cout)
+            self.d_a[L.name] = t(B2, L.out_hw, L.out_hw, L.cout)
+        self.kp_d0 = _kpad(cfg.c_dim)
+        self.d0_col = t(B2 * self.dl[0].out_hw ** 2, self.kp_d0)
+        self.logits = t(B2, dtype=torch.float32)
+        self.prob = t(B2, dtype=torch.float32)
+        self.losses = t(4, dtype=torch.float32, zero=True)
+        self.dl_d = t(B2, dtype=torch.float32)
+        self.dl_g = t(B, dtype=torch.float32)
+        # ---------------- BN state (fwd): mean/rstd/scale/shift per layer [groups][C]
+        self.bn = {}
+        for name, C in cfg.g_bn_layers():
+            self.bn[name] = {k: t(1, C, dtype=torch.float32) for k in ("mean", "rstd", "scale", "shift")}
+        for name, C in cfg.d_bn_layers():
+            self.bn[name] = {k: t(2, C, dtype=torch.float32) for k in ("mean", "rstd", "scale", "shift")}
+        # ---------------- backward buffers
+        self.d_da = {L.name: t(B2, L.out_hw, L.out_hw, L.cout) for L in self.dl}
+        self.d_dx = {L.name: t(B2, L.out_hw, L.out_hw, L.cout) for L in self.dl}
+        self.d_head_dx = t(B2, cfg.d_lin_in)
+        self.d_head_part = t(16, cfg.d_lin_in, dtype=torch.float32)
+        self.img_grad = t(B, s, s, cfg.c_dim)
+        self.img_g = t(B, s, s, cfg.c_dim)
+        Lg = self.gl[-1]
+        self.kp_g = _kpad(cfg.c_dim)
+        self.g_last_col = t(B * Lg.in_hw ** 2, self.kp_g)
+        self.g_da = {}
+        self.g_dx = {}
+        for L in self.gl[:-1]:
+            self.g_da[L.name] = t(B, L.out_hw, L.out_hw, L.cout)
+            self.g_dx[L.name] = t(B, L.out_hw, L.out_hw, L.cout)
+        self.g_da0 = t(B, cfg.g_lin_out)
+        self.g_dx0 = t(B, cfg.g_lin_out)
+        self.coef = {name: t(2, C, 3, dtype=torch.float32) for name, C in cfg.d_bn_layers()}
+        self.coef.update({name: t(1, C, 3, dtype=torch.float32) for name, C in cfg.g_bn_layers()})
+        self.coef_g = {name: t(1, C, 3, dtype=torch.float32) for name, C in cfg.d_bn_layers()}
+        self.small_part = t(64, 16, dtype=torch.float32)
+        # ---------------- packed bf16 weights
+        self.wp = {}
+        for L in self.dl:
+            w = self.model.d[L.name + "/w"]
+            nat = t(25, L.cin, L.cout)  # HWIO natural -> dgrad [25][N=ci][Kc=co]
+            if L.cin % 8 == 0:
+                tr = t(25, L.cout, L.cin)  # fwd [25][co][ci]
+            else:
+                tr = t(L.cout, self.kp_d0, zero=True)  # im2col [co][tap*ci]
+            self.wp[L.name] = (nat, tr)
+        for L in self.gl:
+            nat = t(25, L.cout, L.cin)  # fwd [25][co][ci]
+            if L.cout % 8 == 0:
+                tr = t(25, L.cin, L.cout)  # dgrad [25][ci][co]
+            else:
+                tr = t(L.cin, self.kp_g, zero=True)  # im2col [ci][tap*co]
+            self.wp[L.name] = (nat, tr)
+
+    # ------------------------------------------------------------------ program build
+    def _stats_buf(self, key, P, C):
+        buf = self._t(P, 2, C, dtype=torch.float32)
+        self._keep.append(buf)
+        return buf
+
+    def _build(self):
+        ext = self.ext
+        self._keep: List[torch.Tensor] = []
+        self.progA = ext.Program()
+        self.progB = ext.Program()
+        self.progC = ext.Program()
+        self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
+        self._build_d_backward_dloss(self.progA)
+        self._build_gloss_and_g_backward(self.progB)
+        self._build_update(self.progC)
+        self.progPack = ext.Program()
+        self._build_pack(self.progPack)
+        self._build_pack(self.progC)
+        self.progS = None  # sampler program, built lazily
+        self.progEval = None
+
+    # ---- helpers
+    def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
+               cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None):
+        if mode == 1:
+            M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
+            phases = 4
+        else:
+            M = Bn * Hout * Wout
+            phases = 1
+        cfg = H.pick_igemm_cfg(M, N, phases, rows_per_group)
+        prog.igemm(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
+                   ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0)
+        return cfg
+
+    def _igemm_stats_tiles(self, mode, Bn, Hout, Wout, N, rows_per_group=None):
+        if mode == 1:
+            M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
+            phases = 4
+        else:
+            M = Bn * Hout * Wout
+            phases = 1
+        cfg = H.pick_igemm_cfg(M, N, phases, rows_per_group)
+        bm, _ = H.IGEMM_CFGS[cfg]
+        return -(-M // bm) * phases
+
+    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema):
+        cfgm = self.cfg
+        st = self.bn[name]
+        bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
+        P = self.model.d if name.startswith("d_") else self.model.g
+        ema_m = bnstate.mean[name] if update_ema else None
+        ema_v = bnstate.var[name] if update_ema else None
+        prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
+                         _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
+                         _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
+        prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
+                          rows // groups, act, cfgm.lrelu_leak, 0)
+
+    @staticmethod
+    def _rows_per_block(rows_per_group: int, C: int) -> int:
+        for rpb in (256, 128, 64, 32, 16, 8, 4, 2, 1):
+            if rows_per_group % rpb == 0 and rows_per_group // rpb >= 1:
+                # keep at least ~256 blocks when possible
+                if rows_per_group // rpb >= 64 or rpb == 1:
+                    return rpb
+        return 1
+
+    # ---- forward
+    def _build_forward(self, prog, update_ema: bool, z, train_z: bool):
+        cfg, B = self.cfg, self.B
+        B2 = 2 * B
+        Pg, Pd = self.model.g, self.model.d
+        if train_z:
+            prog.philox_uniform("z", _p(z), z.numel(), self.seed * 1000003 + 17 + 7919 * self.rank,
+                                _p(self.step_counter), 0, -1.0, 1.0, 0)
+        # G projection + g_bn0 + relu
+        prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
+                        B, cfg.z_dim, cfg.g_lin_out, 0)
+        C0 = cfg.g_base_ch
+        rows0 = B * cfg.g_base_hw ** 2
+        rpb = self._rows_per_block(rows0, C0)
+        part0 = self._stats_buf("g_bn0", rows0 // rpb, C0)
+        prog.colstats("g_bn0.stats", 0, _p(self.g_h0_pre), 0, 0, 0, 0, 0, 0.0, rows0, C0, rpb, rows0, _p(part0), 0)
+        self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, rows0 // rpb, update_ema)
+        a_prev = self.g_h0
+        for L in self.gl:
+            nat, tr = self.wp[L.name]
+            pad = same_pads(L.out_hw)[0]
+            if L.bn:
+                P = self._igemm_stats_tiles(1, B, L.out_hw, L.out_hw, L.cout)
+                part = self._stats_buf(L.bn, P, L.cout)
+                self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part)
+                rows = B * L.out_hw ** 2
+                self._bn_fwd(prog, L.bn, self.g_x[L.name], self.g_a[L.name], rows, L.cout, 1, RELU, part, P,
+                             update_ema)
+                a_prev = self.g_a[L.name]
+            else:  # last: + bias, tanh, written into the fake half of D's input
+                self._igemm(prog, L.name, 1, a_prev, nat, self.fake, B, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], act=TANH)
+        # D forward on [real | fake]
+        prev = self.d_in
+        for i, L in enumerate(self.dl):
+            nat, tr = self.wp[L.name]
+            pad = same_pads(L.in_hw)[0]
+            rows = B2 * L.out_hw ** 2
+            if i == 0 and L.cin % 8 != 0:
+                prog.im2col_s2("d0.im2col", _p(prev), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                               L.out_hw, pad, pad, self.kp_d0, 0)
+                self._igemm(prog, L.name, 2, self.d0_col, tr, self.d_a[L.name], B2, 1, 1, self.kp_d0, L.out_hw,
+                            L.out_hw, L.cout, 0, bias=Pd[L.name + "/biases"], act=LRELU)
+            elif not L.bn:
+                self._igemm(prog, L.name, 0, prev, tr, self.d_a[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU)
+            else:
+                rpg = B * L.out_hw ** 2
+                P = self._igemm_stats_tiles(0, B2, L.out_hw, L.out_hw, L.cout, rpg)
+                part = self._stats_buf(L.bn, P, L.cout)
+                self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg)
+                self._bn_fwd(prog, L.bn, self.d_x[L.name], self.d_a[L.name], rows, L.cout, 2, LRELU, part, P // 2,
+                             update_ema)
+            prev = self.d_a[L.name]
+        lin = cfg.d_lin_name
+        prog.gemv_head("d_head", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits), B2,
+                       cfg.d_lin_in, 0)
+        prog.gan_loss("loss", _p(self.logits), B, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob), 0)
+
+    # ---- D backward for d_loss (2B rows, both groups) -> all D gradients
+    def _build_d_backward_dloss(self, prog):
+        cfg, B = self.cfg, self.B
+        B2 = 2 * B
+        Pd, gD = self.model.d, self.grad_d
+        lin = cfg.d_lin_name
+        last = self.dl[-1]
+        prog.head_wgrad("d_head.wgrad", _p(self.d_a[last.name]), _p(self.dl_d), _p(self.d_head_part), B2,
+                        cfg.d_lin_in, 16, _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), 0)
+        prog.head_dgrad("d_head.dgrad", _p(self.dl_d), _p(Pd[lin + "/Matrix"]), _p(self.d_da[last.name]), B2,
+                        cfg.d_lin_in, 0)
+        for i in range(len(self.dl) - 1, -1, -1):
+            L = self.dl[i]
+            rows = B2 * L.out_hw ** 2
+            da, a = self.d_da[L.name], self.d_a[L.name]
+            dx = self.d_dx[L.name]
+            if L.bn:
+                self._bn_bwd(prog, L.bn, self.d_x[L.name], da, a, dx, rows, L.cout, 2, LRELU, Pd, gD,
+                             self.coef[L.bn], write_param_grads=True)
+            else:
+                prog.act_bwd(L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
+                # live bias (no BN after it): db = sum over rows of dx
+                self._colsum(prog, L.name + ".dbias", dx, rows, L.cout, gD[L.name + "/biases"])
+            # weight gradient
+            src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
+            pad = same_pads(L.in_hw)[0]
+            if i == 0 and L.cin % 8 != 0:
+                self._wgrad(prog, L.name, 2, self.d0_col, 1, 1, self.kp_d0, dx, B2 * L.out_hw ** 2, 1, 1, L.cout, 0,
+                            gD[L.name + "/w"])
+            else:
+                self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
+                            gD[L.name + "/w"])
+            # data gradient into the previous activation (not needed below layer 0)
+            if i > 0:
+                nat, _ = self.wp[L.name]
+                P_ = self.dl[i - 1]
+                self._igemm(prog, L.name + ".dgrad", 1, dx, nat, self.d_da[P_.name], B2, L.out_hw, L.out_hw, L.cout,
+                            L.in_hw, L.in_hw, L.cin, pad)
+
+    def _colsum(self, prog, name, x, rows, C, dst):
+        if C % 8 == 0:
+            rpb = self._rows_per_block(rows, C)
+            part = self._stats_buf(name, rows // rpb, C)
+            prog.colstats(name, 2, _p(x), 0, 0, 0, 0, 0, 0.0, rows, C, rpb, rows, _p(part), 0)
+            prog.sum_partials(name + ".sum", _p(part), rows // rpb, 2 * C, C, _p(dst), 0)
+        else:
+            blocks = 64
+            prog.colsum_small(name, _p(x), rows, C, _p(self.small_part), blocks, 0)
+            prog.sum_partials(name + ".sum", _p(self.small_part), blocks, C, C, _p(dst), 0)
+
+    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst):
+        K = Bn * Hd * Wd
+        taps = 1 if mode == 2 else 25
+        cfg, splits = H.pick_wgrad(Mc, Nc, K, taps)
+        slabs = self._t(splits, taps, Mc, Nc, dtype=torch.float32)
+        self._keep.append(slabs)
+        prog.wgrad(name + ".wgrad", mode, _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(slabs),
+                   _p(dst), dst.numel(), 1.0, 0)
+
+    def _bn_bwd(self, prog, name, x, dy, y, dx, rows, C, groups, act, P, grads, coef, write_param_grads,
+                stats_key=None, row_offset_groups=None):
+        st = self.bn[name]
+        mean, rstd = st["mean"], st["rstd"]
+        if row_offset_groups is not None:  # fake-half only (group 1)
+            mean = mean[row_offset_groups:row_offset_groups + 1]
+            rstd = rstd[row_offset_groups:row_offset_groups + 1]
+        rpg = rows // groups
+        rpb = self._rows_per_block(rpg, C)
+        Pn = rows // rpb
+        part = self._stats_buf(name + ".bwd", Pn, C)
+        prog.colstats(name + ".bwd_stats", 1, _p(x), _p(dy), _p(y), _p(mean), _p(rstd), act, self.cfg.lrelu_leak,
+                      rows, C, rpb, rpg, _p(part), 0)
+        dg = grads[name + "/gamma"] if write_param_grads else None
+        db = grads[name + "/beta"] if write_param_grads else None
+        prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg), _p(P[name + "/gamma"]),
+                             _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
+        prog.bn_bwd_apply(name + ".bwd_apply", _p(dy), _p(y), _p(x), _p(coef), _p(dx), rows, C, rpg, act,
+                          self.cfg.lrelu_leak, 0)
+
+    # ---- g_loss back through D(fake) (fake rows only, no D grads) and G backward
+    def _build_gloss_and_g_backward(self, prog):
+        cfg, B = self.cfg, self.B
+        Pd, Pg, gG = self.model.d, self.model.g, self.grad_g
+        lin = cfg.d_lin_name
+        last = self.dl[-1]
+        half = lambda t: t[B:]  # noqa: E731  fake half of a [2B, ...] buffer
+        prog.head_dgrad("g.d_head.dgrad", _p(self.dl_g), _p(Pd[lin + "/Matrix"]), _p(half(self.d_da[last.name])), B,
+                        cfg.d_lin_in, 0)
+        for i in range(len(self.dl) - 1, -1, -1):
+            L = self.dl[i]
+            rows = B * L.out_hw ** 2
+            da, a, dx = half(self.d_da[L.name]), half(self.d_a[L.name]), half(self.d_dx[L.name])
+            if L.bn:
+                self._bn_bwd(prog, L.bn, half(self.d_x[L.name]), da, a, dx, rows, L.cout, 1, LRELU, Pd, None,
+                             self.coef_g[L.bn], write_param_grads=False, row_offset_groups=1)
+            else:
+                prog.act_bwd("g." + L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
+            nat, _ = self.wp[L.name]
+            pad = same_pads(L.in_hw)[0]
+            if i > 0:
+                P_ = self.dl[i - 1]
+                self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, half(self.d_da[P_.name]), B, L.out_hw,
+                            L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
+            else:
+                self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw, L.out_hw,
+                            L.cout, L.in_hw, L.in_hw, L.cin, pad)
+        # ---------------- G backward
+        n = len(self.gl)
+        Lg = self.gl[-1]
+        prog.act_bwd("g_out.tanh_bwd", _p(self.img_grad), _p(self.fake), _p(self.img_g), self.img_g.numel(), TANH,
+                     0.0, 0)
+        self._colsum(prog, Lg.name + ".dbias", self.img_g, B * Lg.out_hw ** 2, Lg.cout, gG[Lg.name + "/biases"])
+        a_prev = self.g_a[self.gl[-2].name] if n > 1 else self.g_h0
+        da_prev = self.g_da[self.gl[-2].name] if n > 1 else self.g_da0
+        padL = same_pads(Lg.out_hw)[0]
+        _, trL = self.wp[Lg.name]
+        if Lg.cout % 8 != 0:
+            prog.im2col_s2("g_out.im2col", _p(self.img_g), _p(self.g_last_col), B, Lg.out_hw, Lg.out_hw, Lg.cout,
+                           Lg.in_hw, Lg.in_hw, padL, padL, self.kp_g, 0)
+            self._wgrad(prog, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
+                        0, gG[Lg.name + "/w"])
+            self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, trL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
+                        Lg.in_hw, Lg.cin, 0)
+        else:
+            self._wgrad(prog, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
+                        Lg.cin, padL, gG[Lg.name + "/w"])
+            self._igemm(prog, Lg.name + ".dgrad", 0, self.img_g, trL, da_prev, B, Lg.out_hw, Lg.out_hw, Lg.cout,
+                        Lg.in_hw, Lg.in_hw, Lg.cin, padL)
+        for j in range(n - 2, -1, -1):
+            L = self.gl[j]
+            rows = B * L.out_hw ** 2
+            x, a, da, dx = self.g_x[L.name], self.g_a[L.name], self.g_da[L.name], self.g_dx[L.name]
+            self._bn_bwd(prog, L.bn, x, da, a, dx, rows, L.cout, 1, RELU, Pg, gG, self.coef[L.bn],
+                         write_param_grads=True)
+            src = self.g_a[self.gl[j - 1].name] if j > 0 else self.g_h0
+            dsrc = self.g_da[self.gl[j - 1].name] if j > 0 else self.g_da0
+            pad = same_pads(L.out_hw)[0]
+            self._wgrad(prog, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
+                        gG[L.name + "/w"])
+            _, tr = self.wp[L.name]
+            self._igemm(prog, L.name + ".dgrad", 0, dx, tr, dsrc, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw,
+                        L.cin, pad)
+        # g_bn0 backward + projection gradients
+        C0 = cfg.g_base_ch
+        rows0 = B * cfg.g_base_hw ** 2
+        self._bn_bwd(prog, "g_bn0", self.g_h0_pre, self.g_da0, self.g_h0, self.g_dx0, rows0, C0, 1, RELU, Pg, gG,
+                     self.coef["g_bn0"], write_param_grads=True)
+        prog.linear_wgrad("g_h0_lin.wgrad", _p(self.z), _p(self.g_dx0), _p(gG["g_h0_lin/Matrix"]),
+                          _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
+
+    # ---- optimiser + repack
+    def _build_update(self, prog):
+        gs = 1.0 / self.world
+        od, og = self.opt_d, self.opt_g
+        prog.adam("adam_d", _p(self.model.d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers),
+                  self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0)
+        prog.adam("adam_g", _p(self.model.g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat), _p(og.powers),
+                  self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0)
+        prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
+                      _p(self.step_counter), 0)
+
+    def _build_pack(self, prog):
+        for L in self.dl:
+            w = self.model.d[L.name + "/w"]
+            nat, tr = self.wp[L.name]
+            ci, co = L.cin, L.cout
+            if ci % 8 == 0:
+                prog.pack(L.name + ".pack", _p(w), 25, ci, co, _p(nat), _p(tr), co * ci, ci, 1, 0)
+            else:  # tr[co][tap*ci + a]
+                prog.pack(L.name + ".pack", _p(w), 25, ci, co, _p(nat), _p(tr), ci, self.kp_d0, 1, 0)
+        for L in self.gl:
+            w = self.model.g[L.name + "/w"]
+            nat, tr = self.wp[L.name]
+            co, ci = L.cout, L.cin  # w [25][co][ci]
+            if co % 8 == 0:
+                prog.pack(L.name + ".pack", _p(w), 25, co, ci, _p(nat), _p(tr), ci * co, co, 1, 0)
+            else:
+                prog.pack(L.name + ".pack", _p(w), 25, co, ci, _p(nat), _p(tr), co, self.kp_g, 1, 0)
+
+    def _repack_weights_now(self):
+        H.run(self.progPack)
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ execution
+    def _streams(self):
+        return [torch.cuda.current_stream(self.device)]
+
+    def _run_eager(self):
+        st = self._streams()
+        H.run(self.progA, st)
+        if self.world > 1:
+            self._ar_d.launch()
+        H.run(self.progB, st)
+        if self.world > 1:
+            self._ar_g.launch()
+            self._ar_d.wait(scale_in_place=False)
+            self._ar_g.wait(scale_in_place=False)
+        H.run(self.progC, st)
+
+    def _ensure_comm(self):
+        if self.world > 1 and not hasattr(self, "_ar_d"):
+            self._ar_d = D.GradAllReducer(self.grad_d.flat, self.bucket_mb, self.allreduce_dtype)
+            self._ar_g = D.GradAllReducer(self.grad_g.flat, self.bucket_mb, self.allreduce_dtype)
+
+    def _capture(self):
+        """Capture the whole step (A+B+C) into one hipGraph (single process). Capturing does
+        not execute anything; it is attempted only after one eager step has loaded every code
+        object, and any failure falls back to eager replay of the recorded programs."""
+        if self.world > 1:
+            return False
+        try:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                cs = torch.cuda.current_stream(self.device)
+                H.run(self.progA, [cs])
+                H.run(self.progB, [cs])
+                H.run(self.progC, [cs])
+            self._graphs = [g]
+            return True
+        except Exception as e:  # pragma: no cover - depends on runtime
+            print("[hip_engine] graph capture failed, running eagerly: %s" % e)
+            self._graphs = []
+            return False
+
+    def train_step(self) -> None:
+        self._ensure_comm()
+        if (self.graph_requested and not self.graph_enabled and self.world == 1 and self._step_host >= 1
+                and not getattr(self, "_cap_tried", 0)):
+            self._cap_tried = 1
+            self.graph_enabled = self._capture()
+        if self.graph_enabled:
+            self._graphs[0].replay()
+        else:
+            self._run_eager()
+        self._step_host += 1
+
+    @property
+    def global_step(self) -> int:
+        return int(self.step_counter.item())
+
+    @global_step.setter
+    def global_step(self, v: int) -> None:
+        self.step_counter.fill_(int(v))
+
+    def set_synthetic_batch(self, real: torch.Tensor) -> None:
+        self.set_batch(real)
+
+    def set_batch(self, real: torch.Tensor) -> None:
+        """Copy a [B,H,W,C] batch (any float dtype, values already in [-1,1]) into the real half."""
+        B = self.B
+        if real.shape[0] != B:
+            raise ValueError("batch %d != engine batch %d" % (real.shape[0], B))
+        self.d_in[:B].copy_(real.to(self.device, non_blocking=True))
+
+    def last_losses(self) -> Dict[str, float]:
+        l = self.losses.tolist()
+        return {"d_loss_real": l[0], "d_loss_fake": l[1], "g_loss": l[2], "d_loss": l[3]}
+
+    def losses_tensor(self) -> torch.Tensor:
+        return self.losses
+
+    # ------------------------------------------------------------------ sampling / eval
+    def sampler(self, z: torch.Tensor) -> torch.Tensor:
+        """G with inference-mode BN (moving averages) -- distriubted_model.py:131-153."""
+        if self.progS is None:
+            self._build_sampler()
+        self.sample_z.copy_(z.to(self.device, torch.float32))
+        H.run(self.progS)
+        return self._s_out.float().clone()
+
+    def _build_sampler(self):
+        cfg, B = self.cfg, self.B
+        prog = self.ext.Program()
+        Pg = self.model.g
+        t = self._t
+        self._s_bufs = {}
+        h0p, h0 = t(B, cfg.g_lin_out), t(B, cfg.g_lin_out)
+        self._s_out = t(B, cfg.output_size, cfg.output_size, cfg.c_dim)
+        sc = {name: (t(C, dtype=torch.float32), t(C, dtype=torch.float32)) for name, C in cfg.g_bn_layers()}
+        self._s_keep = [h0p, h0, sc]
+        bnst = self.model.g_bn
+        debias = 1.0
+        prog.linear_fwd("s.lin", _p(self.sample_z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(h0p), B,
+                        cfg.z_dim, cfg.g_lin_out, 0)
+
+        def coef(name, C):
+            # zero-debias (if enabled) is applied host-side at build; BN state is read live
+            prog.bn_coef_eval("s." + name, C, _p(Pg[name + "/gamma"]), _p(Pg[name + "/beta"]), cfg.bn_eps,
+                              _p(bnst.mean[name]), _p(bnst.var[name]), debias, _p(sc[name][0]), _p(sc[name][1]), 0)
+
+        C0 = cfg.g_base_ch
+        coef("g_bn0", C0)
+        prog.bn_apply_act("s.g_bn0", _p(h0p), _p(h0), _p(sc["g_bn0"][0]), _p(sc["g_bn0"][1]),
+                          B * cfg.g_base_hw ** 2, C0, B * cfg.g_base_hw ** 2, RELU, 0.0, 0)
+        prev = h0
+        for L in self.gl:
+            nat, _ = self.wp[L.name]
+            pad = same_pads(L.out_hw)[0]
+            if L.bn:
+                xb, ab = t(B, L.out_hw, L.out_hw, L.cout), t(B, L.out_hw, L.out_hw, L.cout)
+                self._s_keep += [xb, ab]
+                self._igemm(prog, "s." + L.name, 1, prev, nat, xb, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw,
+                            L.cout, pad, bias=Pg[L.name + "/biases"])
+                coef(L.bn, L.cout)
+                rows = B * L.out_hw ** 2
+                prog.bn_apply_act("s." + L.bn, _p(xb), _p(ab), _p(sc[L.bn][0]), _p(sc[L.bn][1]), rows, L.cout, rows,
+                                  RELU, 0.0, 0)
+                prev = ab
+            else:
+                self._igemm(prog, "s." + L.name, 1, prev, nat, self._s_out, B, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], act=TANH)
+        self.progS = prog
+
+    def eval_losses(self, real: torch.Tensor, z: torch.Tensor) -> Dict[str, float]:
+        """Sample-time d_loss / g_loss (image_train.py:181-184) in train-mode BN but WITHOUT
+        mutating the moving averages (documented deviation)."""
+        if self.progEval is None:
+            prog = self.ext.Program()
+            self._ev_z = self._t(self.B, self.cfg.z_dim, dtype=torch.float32)
+            self._build_forward(prog, update_ema=False, z=self._ev_z, train_z=False)
+            self.progEval = prog
+        saved_real = self.d_in[:self.B].clone()
+        saved_losses = self.losses.clone()
+        self.set_batch(real)
+        self._ev_z.copy_(z.to(self.device, torch.float32))
+        H.run(self.progEval)
+        l = self.losses.tolist()
+        self.d_in[:self.B].copy_(saved_real)
+        self.losses.copy_(saved_losses)
+        return {"d_loss": l[3], "g_loss": l[2]}
+
+    def sync_state_for_checkpoint(self) -> None:
+        torch.cuda.synchronize(self.device)
+
+    def after_state_load(self) -> None:
+        """Call after loading weights/slots from a checkpoint: refresh packed bf16 weights."""
+        self._repack_weights_now()
+
+    def op_names(self) -> List[str]:
+        out = []
+        for p in (self.progA, self.progB, self.progC):
+            out += [p.name(i) for i in range(p.size())]
+        return out

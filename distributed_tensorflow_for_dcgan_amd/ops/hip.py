@@ -1,0 +1,260 @@
+"""Loader and thin tensor-level wrappers for the gfx950 kernel library (``_dcgan_hip``).
+
+The extension is built in-tree by ``csrc/build.py`` (``__graft_entry__.build()``). On a
+machine with a GPU the HIP path is mandatory: if the extension is missing or was built
+for another architecture, :func:`ext` raises instead of silently falling back to PyTorch.
+
+The wrappers below run ONE op through a throw-away ``Program`` on the current torch
+stream; they exist for unit tests and for the autograd modules in ``ops.functional``.
+The training engine records its whole step into persistent programs instead
+(``engine.hip_engine``).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from ..models.config import same_out, same_pads
+
+_EXT = None
+
+ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
+
+
+class HipUnavailable(RuntimeError):
+    pass
+
+
+def ext():
+    """Import the compiled extension (torch must be imported first so that the HIP runtime
+    shared by torch and the extension is the one already loaded)."""
+    global _EXT
+    if _EXT is None:
+        try:
+            _EXT = importlib.import_module("distributed_tensorflow_for_dcgan_amd._dcgan_hip")
+        except ImportError as e:  # pragma: no cover - depends on build state
+            raise HipUnavailable(
+                "native HIP extension _dcgan_hip is not built; run `python csrc/build.py` "
+                "(or __graft_entry__.build()). Original error: %s" % e) from e
+    return _EXT
+
+
+def available() -> bool:
+    try:
+        ext()
+        return torch.cuda.is_available()
+    except HipUnavailable:
+        return False
+
+
+def stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def run(prog, streams: Optional[Sequence] = None, begin: int = 0, end: int = -1) -> None:
+    if streams is None:
+        streams = [torch.cuda.current_stream()]
+    prog.run([stream_ptr(s) if not isinstance(s, int) else s for s in streams], begin, end)
+
+
+def _p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+# --------------------------------------------------------------------------- tile policy
+IGEMM_CFGS = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (32, 64), 5: (64, 32),
+              6: (32, 32), 7: (128, 16), 8: (64, 16), 9: (256, 64)}
+WGRAD_CFGS = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64), 4: (32, 64), 5: (64, 32), 6: (32, 32)}
+CU_COUNT = 256
+
+
+def pick_igemm_cfg(M: int, N: int, phases: int = 1, rows_per_group: Optional[int] = None,
+                   target_blocks: int = 2 * CU_COUNT) -> int:
+    """Largest tile that still gives >= target_blocks workgroups (fill 256 CUs twice);
+    BM must divide rows_per_group when per-group BN statistics are produced."""
+    if N <= 16:
+        order = [7, 8]
+    else:
+        order = [0, 1, 2, 3, 4, 5, 6]
+    best = None
+    for c in order:
+        bm, bn = IGEMM_CFGS[c]
+        if rows_per_group is not None and rows_per_group % bm != 0:
+            continue
+        if bn > 16 and N < bn and bn > 32 and c not in (5, 6):
+            # avoid tiles wider than N (wasted MFMA columns) unless nothing else fits
+            continue
+        blocks = -(-M // bm) * -(-N // bn) * phases
+        if best is None:
+            best = c
+        if blocks >= target_blocks:
+            return c
+        best = c
+    if best is None:
+        raise ValueError("no igemm tile fits M=%d N=%d rows_per_group=%s" % (M, N, rows_per_group))
+    return best
+
+
+def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_COUNT) -> Tuple[int, int]:
+    """(cfg, splits) for a weight-gradient GEMM of Mc x Nc per tap over K pixels."""
+    if Mc >= 128 and Nc >= 128:
+        cfg = 0
+    elif Mc < 128 and Nc >= 128:
+        cfg = 1 if Mc > 32 else 4
+    elif Mc >= 128 and Nc < 128:
+        cfg = 2 if Nc > 32 else 5
+    elif Mc > 32 and Nc > 32:
+        cfg = 3
+    elif Nc > 32:
+        cfg = 4
+    elif Mc > 32:
+        cfg = 5
+    else:
+        cfg = 6
+    bm, bn = WGRAD_CFGS[cfg]
+    tiles = -(-Mc // bm) * -(-Nc // bn) * taps
+    kt = -(-K // 64)
+    splits = max(1, min(-(-target_blocks // tiles), max(1, kt // 4)))
+    return cfg, splits
+
+
+# --------------------------------------------------------------------------- one-shot wrappers
+def _check_bf16(*ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous() or not t.is_cuda):
+            raise ValueError("expected contiguous cuda bf16 tensor, got %s %s" % (t.dtype, t.device))
+
+
+def pack_conv_weight(w: torch.Tensor, kind: str, use: str) -> torch.Tensor:
+    """bf16 B-operand layout [25][N][Kc] for the igemm kernel.
+
+    conv weight HWIO [5,5,ci,co]: use='fwd' -> [25][co][ci] (transposed), 'dgrad' -> natural.
+    deconv weight [5,5,co,ci]:    use='fwd' -> natural,              'dgrad' -> [25][ci][co]."""
+    w = w.reshape(25, w.shape[2], w.shape[3])
+    transpose = (kind == "conv" and use == "fwd") or (kind == "deconv" and use == "dgrad")
+    if transpose:
+        w = w.transpose(1, 2)
+    return w.contiguous().to(torch.bfloat16)
+
+
+def pack_im2col_weight(w: torch.Tensor, kind: str, kpad: int) -> torch.Tensor:
+    """[N][kpad] bf16 for a 3-channel layer run as a plain GEMM over im2col rows.
+    conv (D L0) HWIO [5,5,3,co] -> Bt[co][tap*3+ci]; deconv dgrad (G last) [5,5,3,ci]:
+    Bt[ci][tap*3+co]."""
+    A = w.shape[2]
+    t = w.reshape(25 * A, w.shape[3]).t()  # [N][25*A], k = tap*A + a
+    out = torch.zeros(t.shape[0], kpad, dtype=torch.bfloat16, device=w.device)
+    out[:, :25 * A] = t.to(torch.bfloat16)
+    return out
+
+
+def conv2d_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
+                act: Optional[str] = None, leak: float = 0.2, stats: bool = False, out_f32: bool = False,
+                cfg: Optional[int] = None):
+    """TF-SAME stride-2 5x5 conv on the HIP igemm kernel. x bf16 NHWC [B,H,W,Ci] (Ci % 8 == 0),
+    w_packed bf16 [25][co][ci]. Returns y (and per-tile stats partials [P,2,co] if stats)."""
+    _check_bf16(x, w_packed)
+    B, H, W, Ci = x.shape
+    Ho, Wo = same_out(H), same_out(W)
+    py, px = same_pads(H)[0], same_pads(W)[0]
+    M = B * Ho * Wo
+    cfg = pick_igemm_cfg(M, cout) if cfg is None else cfg
+    bm, bn = IGEMM_CFGS[cfg]
+    y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    mt = -(-M // bm)
+    st = torch.empty(mt, 2, cout, device=x.device, dtype=torch.float32) if stats else None
+    prog = ext().Program()
+    prog.igemm("conv", 0, _p(x), _p(w_packed), _p(y), B, H, W, Ci, Ho, Wo, cout, py, px, cfg, int(out_f32), cout, 0,
+               _p(bias), ACT[act], leak, _p(st), 0)
+    run(prog)
+    return (y, st) if stats else y
+
+
+def conv2d_transpose_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, out_hw: Tuple[int, int],
+                          bias: Optional[torch.Tensor] = None, act: Optional[str] = None, leak: float = 0.2,
+                          stats: bool = False, out_f32: bool = False, cfg: Optional[int] = None):
+    """TF-SAME stride-2 5x5 conv_transpose via 4 sub-pixel phases. x bf16 [B,Hi,Wi,Ci],
+    w_packed bf16 [25][co][ci]."""
+    _check_bf16(x, w_packed)
+    B, Hi, Wi, Ci = x.shape
+    Ho, Wo = out_hw
+    py, px = same_pads(Ho)[0], same_pads(Wo)[0]
+    Mphase = B * (-(-Ho // 2)) * (-(-Wo // 2))
+    cfg = pick_igemm_cfg(Mphase, cout, phases=4) if cfg is None else cfg
+    bm, bn = IGEMM_CFGS[cfg]
+    y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    prog = ext().Program()
+    st = None
+    if stats:
+        mt = -(-Mphase // bm)
+        st = torch.empty(mt * 4, 2, cout, device=x.device, dtype=torch.float32)
+    prog.igemm("deconv", 1, _p(x), _p(w_packed), _p(y), B, Hi, Wi, Ci, Ho, Wo, cout, py, px, cfg, int(out_f32), cout,
+               0, _p(bias), ACT[act], leak, _p(st), 0)
+    run(prog)
+    return (y, st) if stats else y
+
+
+def gemm_plain(a: torch.Tensor, bt: torch.Tensor, out_f32: bool = False, bias=None, act=None,
+               cfg: Optional[int] = None) -> torch.Tensor:
+    """C[M][N] = A[M][K] . Bt[N][K] (bf16, K % 8 == 0)."""
+    _check_bf16(a, bt)
+    M, K = a.shape
+    N = bt.shape[0]
+    cfg = pick_igemm_cfg(M, N) if cfg is None else cfg
+    c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    prog = ext().Program()
+    prog.igemm("gemm", 2, _p(a), _p(bt), _p(c), M, 1, 1, K, 1, 1, N, 0, 0, cfg, int(out_f32), N, 0, _p(bias),
+               ACT[act], 0.2, 0, 0)
+    run(prog)
+    return c
+
+
+def conv_wgrad(g_src: torch.Tensor, dm: torch.Tensor, pad: int, mode: int = 0, cfg=None, splits=None) -> torch.Tensor:
+    """out[25][Mc][Nc] = sum_k G[b,2y+ky-pad,2x+kx-pad,m] * Dm[b,y,x,n] (fp32).
+    mode 2: g_src is an im2col matrix [K][Mc] and the result is [Mc][Nc]."""
+    _check_bf16(g_src, dm)
+    if mode == 2:
+        K, Mc = g_src.shape
+        Nc = dm.shape[-1]
+        Bn, Hd, Wd = K, 1, 1
+        Hg = Wg = 1
+        taps = 1
+    else:
+        Bn, Hg, Wg, Mc = g_src.shape
+        _, Hd, Wd, Nc = dm.shape
+        taps = 25
+        K = Bn * Hd * Wd
+    c, s = pick_wgrad(Mc, Nc, K, taps)
+    cfg = c if cfg is None else cfg
+    splits = s if splits is None else splits
+    slabs = torch.empty(splits, taps, Mc, Nc, device=dm.device, dtype=torch.float32)
+    out = torch.empty(taps, Mc, Nc, device=dm.device, dtype=torch.float32)
+    prog = ext().Program()
+    prog.wgrad("wgrad", mode, _p(g_src), Hg, Wg, Mc, _p(dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(slabs), _p(out),
+               out.numel(), 1.0, 0)
+    run(prog)
+    return out if mode != 2 else out[0]
+
+
+def im2col_s2(x: torch.Tensor, kpad: int) -> torch.Tensor:
+    _check_bf16(x)
+    B, H, W, C = x.shape
+    Ho, Wo = same_out(H), same_out(W)
+    out = torch.empty(B * Ho * Wo, kpad, device=x.device, dtype=torch.bfloat16)
+    prog = ext().Program()
+    prog.im2col_s2("im2col", _p(x), _p(out), B, H, W, C, Ho, Wo, same_pads(H)[0], same_pads(W)[0], kpad, 0)
+    run(prog)
+    return out
+
+
+def adam_(w: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, powers: torch.Tensor, lr: float,
+          beta1: float, beta2: float, eps: float, gscale: float = 1.0, advance_powers: bool = True) -> None:
+    prog = ext().Program()
+    prog.adam("adam", _p(w), _p(g), _p(m), _p(v), _p(powers), w.numel(), lr, beta1, beta2, eps, gscale, 0)
+    if advance_powers:
+        prog.step_end("powers", _p(powers), 0, beta1, beta2, 0.0, 0.0, 0, 0)
+    run(prog)

@@ -1,0 +1,305 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (MI355X only).
+
+Inputs are rounded to bf16 first, so the reference sees exactly the kernel's operands; the
+remaining differences are fp32 accumulation order and the bf16 rounding of outputs.
+Asymmetric data everywhere (guide: symmetric operands hide transposes).
+"""
+import math
+
+import pytest
+import torch
+
+from distributed_tensorflow_for_dcgan_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def H():
+    from distributed_tensorflow_for_dcgan_amd.ops import hip
+    return hip
+
+
+def bf(t):
+    return t.to(torch.bfloat16).contiguous()
+
+
+def close(out, ref, rel=1.5e-2, name=""):
+    out = out.float()
+    ref = ref.float()
+    scale = ref.abs().max().item() + 1e-6
+    err = (out - ref).abs().max().item()
+    assert err <= rel * scale, "%s: max err %.3e vs scale %.3e" % (name, err, scale)
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * 2 - 1).mul(scale).to(dev)
+
+
+@pytest.mark.parametrize("B,Hs,Ci,Co", [(4, 16, 64, 128), (2, 8, 128, 256), (3, 7, 64, 64), (2, 32, 64, 128)])
+def test_conv2d_same_fwd(B, Hs, Ci, Co):
+    h = H()
+    x = bf(rnd(B, Hs, Hs, Ci, seed=1))
+    w = rnd(5, 5, Ci, Co, scale=0.05, seed=2)
+    wp = h.pack_conv_weight(w, "conv", "fwd")
+    bias = rnd(Co, scale=0.1, seed=3)
+    y = h.conv2d_same(x, wp, Co, bias=bias, out_f32=True)
+    ref = R.conv2d_same(x.float(), wp.float().reshape(25, Co, Ci).transpose(1, 2).reshape(5, 5, Ci, Co), bias)
+    close(y, ref, 2e-3, "conv fwd")
+
+
+def test_conv2d_same_act_stats_bf16_all_tiles():
+    h = H()
+    B, Hs, Ci, Co = 4, 16, 64, 128
+    x = bf(rnd(B, Hs, Hs, Ci, seed=4))
+    w = rnd(5, 5, Ci, Co, scale=0.05, seed=5)
+    wp = h.pack_conv_weight(w, "conv", "fwd")
+    wref = wp.float().reshape(25, Co, Ci).transpose(1, 2).reshape(5, 5, Ci, Co)
+    ref_pre = R.conv2d_same(x.float(), wref)
+    for cfg in h.IGEMM_CFGS:
+        if h.IGEMM_CFGS[cfg][1] == 16:
+            continue
+        y, st = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg)
+        close(y, R.lrelu(ref_pre), 1.5e-2, "conv lrelu cfg%d" % cfg)
+        s = st.sum(0)
+        close(s[0], ref_pre.reshape(-1, Co).sum(0), 2e-3, "stats sum cfg%d" % cfg)
+        close(s[1], ref_pre.reshape(-1, Co).pow(2).sum(0), 2e-3, "stats sumsq cfg%d" % cfg)
+
+
+@pytest.mark.parametrize("B,Hi,Ho,Ci,Co", [(4, 4, 8, 128, 64), (2, 8, 16, 64, 128), (2, 4, 7, 64, 64),
+                                          (2, 16, 32, 128, 64), (2, 32, 64, 64, 3)])
+def test_conv2d_transpose_same(B, Hi, Ho, Ci, Co):
+    h = H()
+    x = bf(rnd(B, Hi, Hi, Ci, seed=6))
+    w = rnd(5, 5, Co, Ci, scale=0.05, seed=7)
+    wp = h.pack_conv_weight(w, "deconv", "fwd")
+    bias = rnd(Co, scale=0.1, seed=8)
+    y, st = h.conv2d_transpose_same(x, wp, Co, (Ho, Ho), bias=bias, out_f32=True, stats=True)
+    ref = R.conv2d_transpose_same(x.float(), wp.float().reshape(5, 5, Co, Ci), (Ho, Ho), bias)
+    close(y, ref, 2e-3, "deconv")
+    close(st.sum(0)[0], ref.reshape(-1, Co).sum(0), 3e-3, "deconv stats")
+
+
+def test_dgrad_is_adjoint():
+    """D dgrad = deconv with the natural HWIO weight; G dgrad = conv with the transposed one."""
+    h = H()
+    B, Hs, Ci, Co = 2, 16, 64, 128
+    x = rnd(B, Hs, Hs, Ci, seed=9).requires_grad_(True)
+    w = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=10)).float()
+    dy = bf(rnd(B, 8, 8, Co, seed=11))
+    y = R.conv2d_same(x, w)
+    (gx,) = torch.autograd.grad(y, x, dy.float())
+    out = h.conv2d_transpose_same(dy, h.pack_conv_weight(w, "conv", "dgrad"), Ci, (Hs, Hs), out_f32=True)
+    close(out, gx, 2e-3, "conv dgrad")
+    # G deconv dgrad
+    xd = rnd(B, 8, 8, Co, seed=12).requires_grad_(True)
+    wd = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=13)).float()  # [5,5,out=Ci,in=Co]
+    yd = R.conv2d_transpose_same(xd, wd, (Hs, Hs))
+    dyd = bf(rnd(B, Hs, Hs, Ci, seed=14))
+    (gxd,) = torch.autograd.grad(yd, xd, dyd.float())
+    outd = h.conv2d_same(dyd, h.pack_conv_weight(wd, "deconv", "dgrad"), Co, out_f32=True)
+    close(outd, gxd, 2e-3, "deconv dgrad")
+
+
+def test_im2col_and_plain_gemm_3ch():
+    h = H()
+    B, Hs, C, Co = 4, 64, 3, 64
+    x = bf(rnd(B, Hs, Hs, C, seed=15))
+    col = h.im2col_s2(x, 80)
+    w = bf(rnd(5, 5, C, Co, scale=0.05, seed=16)).float()
+    bt = h.pack_im2col_weight(w, "conv", 80)
+    y = h.gemm_plain(col, bt, out_f32=True)
+    ref = R.conv2d_same(x.float(), w).reshape(-1, Co)
+    close(y, ref, 2e-3, "im2col conv")
+
+
+def test_wgrad_conv_and_deconv():
+    h = H()
+    B, Hs, Ci, Co = 4, 16, 64, 128
+    x = bf(rnd(B, Hs, Hs, Ci, seed=17))
+    w = rnd(5, 5, Ci, Co, scale=0.05, seed=18).requires_grad_(True)
+    dy = bf(rnd(B, 8, 8, Co, seed=19))
+    y = R.conv2d_same(x.float(), w)
+    (gw,) = torch.autograd.grad(y, w, dy.float())
+    out = h.conv_wgrad(x, dy, pad=1)
+    close(out.reshape(5, 5, Ci, Co), gw, 2e-3, "conv wgrad")
+    for cfg in h.WGRAD_CFGS:
+        out = h.conv_wgrad(x, dy, pad=1, cfg=cfg, splits=3)
+        close(out.reshape(5, 5, Ci, Co), gw, 2e-3, "conv wgrad cfg%d" % cfg)
+    # deconv: Y = deconv(X), W [5,5,co,ci]; G-operand = dY (gathered), Dm = X
+    Xd = bf(rnd(B, 8, 8, Ci, seed=20))
+    wd = rnd(5, 5, Co, Ci, scale=0.05, seed=21).requires_grad_(True)
+    yd = R.conv2d_transpose_same(Xd.float(), wd, (Hs, Hs))
+    dyd = bf(rnd(B, Hs, Hs, Co, seed=22))
+    (gwd,) = torch.autograd.grad(yd, wd, dyd.float())
+    outd = h.conv_wgrad(dyd, Xd, pad=1)
+    close(outd.reshape(5, 5, Co, Ci), gwd, 2e-3, "deconv wgrad")
+
+
+def test_wgrad_plain_im2col():
+    h = H()
+    B, Hs, C, Co = 4, 32, 3, 64
+    x = bf(rnd(B, Hs, Hs, C, seed=23))
+    w = rnd(5, 5, C, Co, scale=0.05, seed=24).requires_grad_(True)
+    dy = bf(rnd(B, Hs // 2, Hs // 2, Co, seed=25))
+    (gw,) = torch.autograd.grad(R.conv2d_same(x.float(), w), w, dy.float())
+    col = h.im2col_s2(x, 80)
+    out = h.conv_wgrad(col, dy.reshape(-1, Co), pad=0, mode=2)
+    close(out[:75].reshape(5, 5, C, Co), gw, 2e-3, "plain wgrad")
+
+
+def _prog():
+    return H().ext().Program()
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def test_bn_forward_backward_groups():
+    """colstats -> finalize (+EMA) -> apply(act) and the backward chain vs autograd (2 groups)."""
+    h = H()
+    groups, Bg, Hs, C = 2, 4, 8, 128
+    R_ = groups * Bg * Hs * Hs
+    x = bf(rnd(groups * Bg, Hs, Hs, C, scale=2.0, seed=26) + 0.3)
+    gamma = (1 + 0.1 * rnd(C, seed=27)).contiguous()
+    beta = (0.1 * rnd(C, seed=28)).contiguous()
+    rows_pb = 64
+    P = R_ // rows_pb
+    part = torch.empty(P, 2, C, device=dev)
+    mean = torch.empty(groups, C, device=dev)
+    rstd = torch.empty_like(mean)
+    scale = torch.empty_like(mean)
+    shift = torch.empty_like(mean)
+    ema_m = torch.zeros(groups, C, device=dev)
+    ema_v = torch.zeros(groups, C, device=dev)
+    y = torch.empty_like(x)
+    pr = _prog()
+    pr.colstats("st", 0, _p(x), 0, 0, 0, 0, 0, 0.2, R_, C, rows_pb, R_ // groups, _p(part), 0)
+    pr.bn_finalize("fin", _p(part), P // groups, groups, C, float(R_ // groups), _p(gamma), _p(beta), 1e-5,
+                   _p(mean), _p(rstd), _p(scale), _p(shift), _p(ema_m), _p(ema_v), 0.9, 0)
+    pr.bn_apply_act("apply", _p(x), _p(y), _p(scale), _p(shift), R_, C, R_ // groups, 2, 0.2, 0)
+    h.run(pr)
+    xr = x.float().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    m_ref, v_ref = R.moments(xr, groups)
+    yr = R.lrelu(R.batch_norm(xr, m_ref, v_ref, br, gr, 1e-5, groups=groups))
+    close(mean, m_ref, 1e-4, "mean")
+    close(1.0 / rstd ** 2 - 1e-5, v_ref, 1e-3, "var")
+    close(ema_m, 0.1 * m_ref, 1e-4, "ema mean")
+    close(y, yr, 1.5e-2, "bn apply")
+    # backward
+    dy = bf(rnd(groups * Bg, Hs, Hs, C, seed=29))
+    gx, gg, gb = torch.autograd.grad(yr, [xr, gr, br], dy.float())
+    part2 = torch.empty(P, 2, C, device=dev)
+    coef = torch.empty(groups, C, 3, device=dev)
+    dgam = torch.empty(C, device=dev)
+    dbet = torch.empty(C, device=dev)
+    dx = torch.empty_like(x)
+    pr = _prog()
+    pr.colstats("bst", 1, _p(x), _p(dy), _p(y), _p(mean), _p(rstd), 2, 0.2, R_, C, rows_pb, R_ // groups,
+                _p(part2), 0)
+    pr.bn_bwd_finalize("bfin", _p(part2), P // groups, groups, C, float(R_ // groups), _p(gamma), _p(mean),
+                       _p(rstd), _p(dgam), _p(dbet), _p(coef), 0)
+    pr.bn_bwd_apply("bapp", _p(dy), _p(y), _p(x), _p(coef), _p(dx), R_, C, R_ // groups, 2, 0.2, 0)
+    h.run(pr)
+    close(dgam, gg, 2e-2, "dgamma")
+    close(dbet, gb, 2e-2, "dbeta")
+    close(dx, gx, 3e-2, "dx")
+
+
+def test_adam_matches_tf_formula():
+    h = H()
+    n = 10000 + 3
+    w = rnd(n, seed=30)
+    g = rnd(n, scale=1e-2, seed=31)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    powers = torch.tensor([0.5, 0.999], device=dev)
+    wr, mr, vr = w.clone().cpu(), m.clone().cpu(), v.clone().cpu()
+    b1p, b2p = 0.5, 0.999
+    for _ in range(3):
+        h.adam_(w, g, m, v, powers, 2e-4, 0.5, 0.999, 1e-8)
+        R.tf_adam_update(wr, g.cpu(), mr, vr, b1p, b2p, 2e-4, 0.5)
+        b1p *= 0.5
+        b2p *= 0.999
+    assert torch.allclose(w.cpu(), wr, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(powers.cpu(), torch.tensor([b1p, b2p]), rtol=1e-6)
+
+
+def test_gan_loss_kernel():
+    h = H()
+    B = 37
+    logits = rnd(2 * B, scale=4.0, seed=32)
+    out = torch.empty(4, device=dev)
+    dld = torch.empty(2 * B, device=dev)
+    dlg = torch.empty(B, device=dev)
+    prob = torch.empty(2 * B, device=dev)
+    pr = _prog()
+    pr.gan_loss("loss", _p(logits), B, _p(out), _p(dld), _p(dlg), _p(prob), 0)
+    h.run(pr)
+    lr = logits[:B].clone().requires_grad_(True)
+    lf = logits[B:].clone().requires_grad_(True)
+    dr, df, gl, dl = R.gan_losses(lr, lf)
+    close(out, torch.stack([dr, df, gl, dl]), 1e-5, "losses")
+    gdr, gdf = torch.autograd.grad(dl, [lr, lf], retain_graph=True)
+    (ggf,) = torch.autograd.grad(gl, [lf])
+    close(dld, torch.cat([gdr, gdf]), 1e-5, "dl_d")
+    close(dlg, ggf, 1e-5, "dl_g")
+
+
+def test_linear_and_head():
+    h = H()
+    B, K, N = 33, 100, 8192
+    z = rnd(B, K, seed=33)
+    W = rnd(K, N, scale=0.02, seed=34)
+    b = rnd(N, scale=0.1, seed=35)
+    out = torch.empty(B, N, device=dev, dtype=torch.bfloat16)
+    dh = bf(rnd(B, N, seed=36))
+    dW = torch.empty(K, N, device=dev)
+    db = torch.empty(N, device=dev)
+    pr = _prog()
+    pr.linear_fwd("lin", _p(z), _p(W), _p(b), _p(out), B, K, N, 0)
+    pr.linear_wgrad("linw", _p(z), _p(dh), _p(dW), _p(db), B, K, N, 0)
+    h.run(pr)
+    close(out, z @ W + b, 1e-2, "linear fwd")
+    close(dW, z.t() @ dh.float(), 1e-3, "linear wgrad")
+    close(db, dh.float().sum(0), 1e-3, "linear bias grad")
+    # D head
+    R_, Kh = 2 * B, 8192
+    x = bf(rnd(R_, Kh, seed=37))
+    w = rnd(Kh, scale=0.02, seed=38)
+    hb = rnd(1, seed=39)
+    logit = torch.empty(R_, device=dev)
+    dl = rnd(R_, seed=40)
+    dx = torch.empty(R_, Kh, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(8, Kh, device=dev)
+    dw = torch.empty(Kh, device=dev)
+    dbh = torch.empty(1, device=dev)
+    pr = _prog()
+    pr.gemv_head("head", _p(x), _p(w), _p(hb), _p(logit), R_, Kh, 0)
+    pr.head_dgrad("hd", _p(dl), _p(w), _p(dx), R_, Kh, 0)
+    pr.head_wgrad("hw", _p(x), _p(dl), _p(part), R_, Kh, 8, _p(dw), _p(dbh), 0)
+    h.run(pr)
+    close(logit, x.float() @ w + hb, 1e-4, "head fwd")
+    close(dx, dl[:, None] * w[None, :], 1e-2, "head dgrad")
+    close(dw, x.float().t() @ dl, 1e-4, "head wgrad")
+    close(dbh, dl.sum().reshape(1), 1e-5, "head bias")
+
+
+def test_philox_uniform_range_and_determinism():
+    h = H()
+    n = 128 * 100
+    out1 = torch.empty(n, device=dev)
+    out2 = torch.empty(n, device=dev)
+    step = torch.zeros(1, dtype=torch.int64, device=dev)
+    pr = _prog()
+    pr.philox_uniform("z", _p(out1), n, 1234, _p(step), 0, -1.0, 1.0, 0)
+    pr.philox_uniform("z", _p(out2), n, 1234, _p(step), 0, -1.0, 1.0, 0)
+    h.run(pr)
+    assert torch.equal(out1, out2)
+    assert out1.min() >= -1 and out1.max() < 1
+    assert abs(out1.mean().item()) < 0.03 and abs(out1.std().item() - 1 / math.sqrt(3)) < 0.02
