@@ -94,21 +94,51 @@ __global__ __launch_bounds__(256) void colstats_kernel(int mode, const bf16* __r
   }
 }
 
+// ---------------------------------------------------------------- partial-row reduction
+// Sum rows [p0, p1) of part (row stride `stride` floats) for 32 channels c0..c0+31, column
+// offsets off0 / off1 (two quantities per row). 256 threads = 32 channels x 8 row lanes; fixed
+// order -> deterministic. Result valid in lane 0 (threadIdx.x < 32).
+template <typename T>
+__device__ __forceinline__ void reduce_rows2(const float* __restrict__ part, int p0, int p1, size_t stride, int c,
+                                             bool cok, int off1, T& s1, T& s2) {
+  __shared__ T red[2][8][33];
+  const int ch = threadIdx.x & 31, lane = threadIdx.x >> 5;
+  T a = 0, b = 0;
+  if (cok)
+    for (int p = p0 + lane; p < p1; p += 8) {
+      a += (T)part[(size_t)p * stride + c];
+      if (off1 >= 0) b += (T)part[(size_t)p * stride + off1 + c];
+    }
+  red[0][lane][ch] = a;
+  red[1][lane][ch] = b;
+  __syncthreads();
+  if (lane == 0) {
+    a = 0; b = 0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) { a += red[0][l][ch]; b += red[1][l][ch]; }
+  }
+  __syncthreads();
+  s1 = a;
+  s2 = b;
+}
+
 // ---------------------------------------------------------------- BN forward finalize
 // part: [P][2][C], partials of group g are [g*ppg, (g+1)*ppg). count = rows per group.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int ppg, int groups, int C, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                   float* __restrict__ scale_out, float* __restrict__ shift_out,
-                                   float* __restrict__ ema_mean, float* __restrict__ ema_var, float decay) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= groups * C) return;
-  const int g = idx / C, c = idx - g * C;
-  double s = 0.0, s2 = 0.0;
-  for (int p = g * ppg; p < (g + 1) * ppg; ++p) {
-    s += (double)part[(size_t)p * 2 * C + c];
-    s2 += (double)part[(size_t)p * 2 * C + C + c];
-  }
+// grid (ceil(C/32), groups), block 256.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int ppg, int groups, int C,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          float* __restrict__ scale_out, float* __restrict__ shift_out,
+                                                          float* __restrict__ ema_mean, float* __restrict__ ema_var,
+                                                          float decay) {
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool cok = c < C;
+  double s, s2;
+  reduce_rows2<double>(part, g * ppg, (g + 1) * ppg, (size_t)2 * C, c, cok, C, s, s2);
+  if ((threadIdx.x >> 5) != 0 || !cok) return;
+  const int idx = g * C + c;
   const double m = s / count;
   double v = s2 / count - m * m;
   if (v < 0.0) v = 0.0;
@@ -160,32 +190,36 @@ __global__ __launch_bounds__(256) void bn_apply_act_kernel(const bf16* __restric
 
 // ---------------------------------------------------------------- BN backward finalize
 // part: [P][2][C] (sum g, sum g*xhat). Writes dgamma/dbeta (sum over groups) when non-null and
-// the per-(group, channel) affine coefficients of dx = A*g + Bc*x + D.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int ppg, int groups, int C, float count,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// the per-(group, channel) affine coefficients of dx = A*g + Bc*x + D. grid ceil(C/32), block 256.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int ppg, int groups,
+                                                              int C, float count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ coef) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool cok = c < C;
+  const bool lead = (threadIdx.x >> 5) == 0 && cok;
   float dg = 0.f, db = 0.f;
   for (int g = 0; g < groups; ++g) {
-    float s1 = 0.f, s2 = 0.f;
-    for (int p = g * ppg; p < (g + 1) * ppg; ++p) {
-      s1 += part[(size_t)p * 2 * C + c];
-      s2 += part[(size_t)p * 2 * C + C + c];
+    float s1, s2;
+    reduce_rows2<float>(part, g * ppg, (g + 1) * ppg, (size_t)2 * C, c, cok, C, s1, s2);
+    if (lead) {
+      dg += s2;
+      db += s1;
+      const float r = rstd[g * C + c], mu = mean[g * C + c];
+      const float a = gamma[c] * r;
+      const float c2 = -a * s2 / count;  // multiplies xhat
+      const float b = -a * s1 / count;
+      coef[(g * C + c) * 3 + 0] = a;
+      coef[(g * C + c) * 3 + 1] = c2 * r;            // * x
+      coef[(g * C + c) * 3 + 2] = b - c2 * mu * r;   // constant
     }
-    dg += s2;
-    db += s1;
-    const float r = rstd[g * C + c], mu = mean[g * C + c];
-    const float a = gamma[c] * r;
-    const float c2 = -a * s2 / count;  // multiplies xhat
-    const float b = -a * s1 / count;
-    coef[(g * C + c) * 3 + 0] = a;
-    coef[(g * C + c) * 3 + 1] = c2 * r;             // * x
-    coef[(g * C + c) * 3 + 2] = b - c2 * mu * r;    // constant
   }
-  if (dgamma) dgamma[c] = dg;
-  if (dbeta) dbeta[c] = db;
+  if (lead) {
+    if (dgamma) dgamma[c] = dg;
+    if (dbeta) dbeta[c] = db;
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
@@ -219,13 +253,13 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ d
     dx[i] = (bf16)((float)dy[i] * act_grad_from_out((float)y[i], act, leak));
 }
 
-// sum over partial rows -> dst[C]
-__global__ void sum_partials_kernel(const float* __restrict__ part, int P, int stride, int C, float* __restrict__ dst) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * stride + c];
-  dst[c] = s;
+// sum over partial rows -> dst[C]; grid ceil(C/32), block 256
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part, int P, int stride, int C,
+                                                           float* __restrict__ dst) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  float s, unused;
+  reduce_rows2<float>(part, 0, P, (size_t)stride, c, c < C, -1, s, unused);
+  if ((threadIdx.x >> 5) == 0 && c < C) dst[c] = s;
 }
 
 // column sums for a small channel count (C <= 16), e.g. dbias of a 3-channel image gradient
@@ -271,8 +305,7 @@ extern "C" int dcg_colstats(int mode, const bf16* x, const bf16* dy, const bf16*
 extern "C" int dcg_bn_finalize(const float* part, int ppg, int groups, int C, double count, const float* gamma,
                                const float* beta, float eps, float* mean, float* rstd, float* scale, float* shift,
                                float* ema_mean, float* ema_var, float decay, hipStream_t s) {
-  const int n = groups * C;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, ppg, groups, C, count, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32, groups), dim3(256), 0, s, part, ppg, groups, C, count, gamma,
                      beta, eps, mean, rstd, scale, shift, ema_mean, ema_var, decay);
   return (int)hipGetLastError();
 }
@@ -295,7 +328,7 @@ extern "C" int dcg_bn_apply_act(const bf16* x, bf16* y, const float* scale, cons
 extern "C" int dcg_bn_bwd_finalize(const float* part, int ppg, int groups, int C, float count, const float* gamma,
                                    const float* mean, const float* rstd, float* dgamma, float* dbeta, float* coef,
                                    hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, ppg, groups, C, count,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, s, part, ppg, groups, C, count,
                      gamma, mean, rstd, dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }
@@ -314,7 +347,7 @@ extern "C" int dcg_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t n, in
 }
 
 extern "C" int dcg_sum_partials(const float* part, int P, int stride, int C, float* dst, hipStream_t s) {
-  hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, stride, C, dst);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 31) / 32), dim3(256), 0, s, part, P, stride, C, dst);
   return (int)hipGetLastError();
 }
 

@@ -207,8 +207,11 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
         const int off = rowoff[ml];
         const float v = acc[i][j][r] + bv;
         if (off >= 0 && nok) {
-          s += v;
-          s2 += v * v;
+          // statistics of exactly the stored (bf16-rounded) tensor, so BN forward/backward
+          // see one consistent x
+          const float vs = p.out_f32 ? v : (float)f2bf(v);
+          s += vs;
+          s2 += vs * vs;
           const float o = apply_act(v, p.act, p.leak);
           if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
           else reinterpret_cast<bf16*>(p.C)[off + p.cofs + n] = f2bf(o);

@@ -175,19 +175,34 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     }
 }
 
-// sum of `splits` fp32 slabs of `n` elements -> dst (optionally scaled); float4 vectorised
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ src, int splits,
-                                                            size_t n, float* __restrict__ dst, float scale) {
+// sum of `splits` fp32 slabs of `n` elements -> dst (scaled). Block = (256/L) float4 columns x L
+// split lanes; each lane sums every L-th slab, then the L partial sums are combined in LDS in a
+// fixed order (deterministic). Handles the few-elements / many-slabs shape of small wgrads.
+template <int L>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* src, int splits, size_t n,
+                                                            float* dst, float scale) {
+  constexpr int COLS = 256 / L;
+  __shared__ f32x4 red[L][COLS];
+  const int col = threadIdx.x % COLS, lane = threadIdx.x / COLS;
   const size_t n4 = n / 4;
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-    f32x4 s = reinterpret_cast<const f32x4*>(src)[i];
-    for (int k = 1; k < splits; ++k) s += reinterpret_cast<const f32x4*>(src + (size_t)k * n)[i];
-    reinterpret_cast<f32x4*>(dst)[i] = s * scale;
+  const size_t i = (size_t)blockIdx.x * COLS + col;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4)
+    for (int k = lane; k < splits; k += L) s += reinterpret_cast<const f32x4*>(src + (size_t)k * n)[i];
+  red[lane][col] = s;
+  __syncthreads();
+  if (lane == 0 && i < n4) {
+    f32x4 t = red[0][col];
+#pragma unroll
+    for (int l = 1; l < L; ++l) t += red[l][col];
+    reinterpret_cast<f32x4*>(dst)[i] = t * scale;
   }
-  for (size_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += src[(size_t)k * n + i];
-    dst[i] = s * scale;
+  // scalar tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (int)(n - n4 * 4)) {
+    const size_t j = n4 * 4 + threadIdx.x;
+    float t = 0.f;
+    for (int k = 0; k < splits; ++k) t += src[(size_t)k * n + j];
+    dst[j] = t * scale;
   }
 }
 
@@ -217,9 +232,16 @@ extern "C" int dcg_wgrad_launch(const dcg::WGradArgs* a, int cfg, int splits, hi
 }
 
 extern "C" int dcg_splitk_reduce(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s) {
-  size_t blocks = (n / 4 + 255) / 256;
-  if (blocks < 1) blocks = 1;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(dcg::splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, splits, n, dst, scale);
+  const size_t n4 = n / 4;
+  if (splits >= 64) {
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  } else if (splits >= 8) {
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  } else {
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  }
   return (int)hipGetLastError();
 }

@@ -228,11 +228,11 @@ class HipEngine:
 
     @staticmethod
     def _rows_per_block(rows_per_group: int, C: int) -> int:
+        """Rows per column-reduction block: a divisor of rows_per_group (blocks never straddle
+        a BN group), as large as possible while keeping >= 256 blocks per group (fill the CUs)."""
         for rpb in (256, 128, 64, 32, 16, 8, 4, 2, 1):
-            if rows_per_group % rpb == 0 and rows_per_group // rpb >= 1:
-                # keep at least ~256 blocks when possible
-                if rows_per_group // rpb >= 64 or rpb == 1:
-                    return rpb
+            if rows_per_group % rpb == 0 and (rows_per_group // rpb >= 256 or rpb == 1):
+                return rpb
         return 1
 
     # ---- forward
@@ -284,10 +284,21 @@ class HipEngine:
                             L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU)
             else:
                 rpg = B * L.out_hw ** 2
-                P = self._igemm_stats_tiles(0, B2, L.out_hw, L.out_hw, L.cout, rpg)
-                part = self._stats_buf(L.bn, P, L.cout)
-                self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                            L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg)
+                if H.pick_igemm_cfg(rows, L.cout, 1, rpg) is not None:
+                    # BN partial statistics straight from the conv epilogue (tiles never straddle
+                    # the real/fake boundary)
+                    P = self._igemm_stats_tiles(0, B2, L.out_hw, L.out_hw, L.cout, rpg)
+                    part = self._stats_buf(L.bn, P, L.cout)
+                    self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                                L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg)
+                else:  # odd sizes: no tile divides the group -> separate group-aligned stats pass
+                    self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                                L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"])
+                    rpb = self._rows_per_block(rpg, L.cout)
+                    P = rows // rpb
+                    part = self._stats_buf(L.bn, P, L.cout)
+                    prog.colstats(L.bn + ".stats", 0, _p(self.d_x[L.name]), 0, 0, 0, 0, 0, 0.0, rows, L.cout, rpb,
+                                  rpg, _p(part), 0)
                 self._bn_fwd(prog, L.bn, self.d_x[L.name], self.d_a[L.name], rows, L.cout, 2, LRELU, part, P // 2,
                              update_ema)
             prev = self.d_a[L.name]

@@ -230,6 +230,8 @@ class DCGAN:
             record["g_h0"] = h
         for L in cfg.g_layers():
             h = R.conv2d_transpose_same(h, P[L.name + "/w"], (L.out_hw, L.out_hw), P[L.name + "/biases"])
+            if record is not None:
+                record[L.name + "/pre"] = h
             if L.bn:
                 h = self._bn(h, L.bn, P, self.g_bn, train, update_ema, groups=1, slots=(0,))
                 h = torch.relu(h)
@@ -252,8 +254,12 @@ class DCGAN:
         cfg = self.cfg
         P = P if P is not None else self.d.tensors
         h = x
+        if record is not None:
+            record["d_in"] = h
         for L in cfg.d_layers():
             h = R.conv2d_same(h, P[L.name + "/w"], P[L.name + "/biases"])
+            if record is not None:
+                record[L.name + "/pre"] = h
             if L.bn:
                 h = self._bn(h, L.bn, P, self.d_bn, train, update_ema, groups=groups, slots=slots)
             h = R.lrelu(h, cfg.lrelu_leak)
