@@ -62,7 +62,31 @@ class ReferenceEngine:
 
     def train_step(self) -> None:
         z = self.sample_z(self._real.shape[0])
+        self._last_z = z
         self._losses = self.step_impl.step(self._real, z)
+
+    def activations(self) -> "Dict[str, torch.Tensor]":
+        """Re-run the last step's forward (pre-update weights are gone; uses current ones,
+        no EMA update) and return the summary tensors."""
+        from collections import OrderedDict
+        rec: Dict[str, torch.Tensor] = {}
+        B = self._real.shape[0]
+        with torch.no_grad():
+            out = self.step_impl.forward_losses(self._real, self._last_z, update_ema=False, record=rec)
+        a = OrderedDict()
+        a["z"] = self._last_z
+        a["d"] = torch.sigmoid(out["logits_real"])
+        a["d_"] = torch.sigmoid(out["logits_fake"])
+        a["G"] = out["fake"]
+        a["g_h0_relu"] = rec["g_h0"]
+        gl = self.cfg.g_layers()
+        for L in gl[:-1]:
+            a[L.name + "_relu"] = rec[L.name]
+        a[gl[-1].name] = rec[gl[-1].name]
+        for L in self.cfg.d_layers():
+            a[L.name] = rec[L.name][:B]
+        a[self.cfg.d_lin_name] = out["logits_real"]
+        return a
 
     def last_losses(self) -> Dict[str, float]:
         return dict(self._losses)
@@ -79,6 +103,13 @@ class ReferenceEngine:
 
     def sync_state_for_checkpoint(self) -> None:
         pass
+
+    def sync_bn_state(self) -> None:
+        """Average the BN moving averages over ranks (collective; every rank must call it).
+        Each rank tracks its own local-batch statistics; the reference's shared PS copy saw
+        every worker's updates, which the mean over ranks approximates."""
+        D.all_reduce_mean_(self.model.g_bn.flat)
+        D.all_reduce_mean_(self.model.d_bn.flat)
 
 
 def build_engine(cfg: DCGANConfig, batch_size: int, device: torch.device, engine: str = "auto",

@@ -569,6 +569,24 @@ class HipEngine:
     def losses_tensor(self) -> torch.Tensor:
         return self.losses
 
+    def activations(self) -> "Dict[str, torch.Tensor]":
+        """Views of the last step's tensors for summaries (no extra compute)."""
+        from collections import OrderedDict
+        B = self.B
+        a = OrderedDict()
+        a["z"] = self.z
+        a["d"] = self.prob[:B]
+        a["d_"] = self.prob[B:]
+        a["G"] = self.fake
+        a["g_h0_relu"] = self.g_h0
+        for L in self.gl[:-1]:
+            a[L.name + "_relu"] = self.g_a[L.name]
+        a[self.gl[-1].name] = self.fake
+        for L in self.dl:
+            a[L.name] = self.d_a[L.name][:B]
+        a[self.cfg.d_lin_name] = self.logits[:B]
+        return a
+
     # ------------------------------------------------------------------ sampling / eval
     def sampler(self, z: torch.Tensor) -> torch.Tensor:
         """G with inference-mode BN (moving averages) -- distriubted_model.py:131-153."""
@@ -641,6 +659,11 @@ class HipEngine:
 
     def sync_state_for_checkpoint(self) -> None:
         torch.cuda.synchronize(self.device)
+
+    def sync_bn_state(self) -> None:
+        """Average BN moving averages over ranks (collective; see ReferenceEngine)."""
+        D.all_reduce_mean_(self.model.g_bn.flat)
+        D.all_reduce_mean_(self.model.d_bn.flat)
 
     def after_state_load(self) -> None:
         """Call after loading weights/slots from a checkpoint: refresh packed bf16 weights."""

@@ -90,6 +90,16 @@ def all_reduce_mean_(t: torch.Tensor) -> None:
     t.mul_(1.0 / dist.get_world_size())
 
 
+def any_rank(flag: bool, device: torch.device) -> bool:
+    """Collective OR of a per-rank boolean (used to share the chief's save decision)."""
+    if not is_initialized():
+        return bool(flag)
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(int(t.item()))
+
+
 def average_scalars(values: Sequence[float], device: torch.device) -> List[float]:
     """Mean of a few host scalars over ranks (logging steps only)."""
     if not is_initialized():

@@ -1,0 +1,190 @@
+"""``image_train.py``-compatible training driver (reference ``image_train.py:51-249``).
+
+Loop per step: next batch (native loader, already on the device) -> engine step (G fwd,
+D(real)+D(fake), 3 losses, backward, gradient all-reduce over RCCL when W > 1, two TF-Adam
+updates) -> the reference's log line -> chief-only TensorBoard summaries every
+``--save_summaries_secs`` -> chief-only sample grid when ``global_step % 100 == 1`` -> chief-only
+checkpoint every ``--save_model_secs``; auto-resume from the newest checkpoint on start.
+
+Deliberate differences: synchronous data parallelism instead of the
+asynchronous parameter server (``--job_name=ps`` exits with a notice), every flag is honoured,
+epochs count W*B images per global step, the sample-time losses do not mutate the BN moving
+averages, samples go to ``--sample_dir``, optimiser state is checkpointed.
+"""
+from __future__ import annotations
+
+import math
+import os
+import pprint
+import sys
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ckpt.checkpoint import CheckpointManager
+from ..data.pipeline import make_source
+from ..engine.factory import build_engine
+from ..models.config import config_from_flags
+from ..obs import images as IM
+from ..obs import summaries as SUM
+from ..obs.events import SummaryWriter
+from ..parallel import dist as D
+from ..utils.flags import Flags, cluster_from_flags
+
+STEP_LINE = "Epoch: [%2d] step: [%2d] time: %4.4f, d_loss: %.8f, g_loss: %.8f"
+SYNC_EVERY = 10  # steps between collective checks of the chief's time-based save decision
+
+
+def _device(flags: Flags, local_rank: int) -> torch.device:
+    want = flags.device
+    if want == "cpu" or (want == "auto" and not torch.cuda.is_available()):
+        return torch.device("cpu")
+    return torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+
+
+def run(flags: Flags, out=None) -> int:
+    out = sys.stdout if out is None else out
+    pprint.pprint(flags.as_dict(), stream=out)
+    if flags.job_name == "ps":
+        print("--job_name=ps: this framework trains with synchronous data parallelism over RCCL; "
+              "there is no parameter server to run. Launch one worker per GPU instead "
+              "(e.g. torchrun --nproc-per-node N image_train.py ...).", file=out)
+        return 0
+    if flags.job_name not in ("", "worker"):
+        raise SystemExit("unknown --job_name=%r (expected 'worker' or 'ps')" % flags.job_name)
+    os.makedirs(flags.checkpoint_dir, exist_ok=True)
+    os.makedirs(flags.sample_dir, exist_ok=True)
+
+    cl = cluster_from_flags(flags)
+    rank, world = cl["rank"], cl["world_size"]
+    device = _device(flags, cl["local_rank"])
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    D.init_distributed(world, rank, device, cl["master_addr"], cl["master_port"])
+    chief = rank == 0
+    cfg = config_from_flags(flags)
+    B = int(flags.batch_size)
+    shape = (cfg.output_size, cfg.output_size, cfg.c_dim)
+    if flags.verbose and chief:
+        print("device %s rank %d/%d engine %s" % (device, rank, world, flags.engine), file=out)
+
+    engine = build_engine(cfg, B, device, engine=flags.engine, dtype=flags.dtype, seed=int(flags.seed), rank=rank,
+                          world=world, graph=bool(flags.graph), allreduce_dtype=flags.allreduce_dtype,
+                          lr=float(flags.learning_rate), beta1=float(flags.beta1),
+                          zero_debias=bool(flags.bn_zero_debias), bucket_mb=float(flags.bucket_mb))
+    ckpt = CheckpointManager(flags.checkpoint_dir, keep=int(flags.keep_checkpoints),
+                             save_secs=float(flags.save_model_secs))
+    info = ckpt.restore_latest(engine)
+    if chief:
+        print(" [*] Reading checkpoints...", file=out)
+        print("load success! (%s, global_step %d)" % (info["path"], info["global_step"]) if info
+              else "load failed!!", file=out)
+        if info and not (info.get("adam_d") and info.get("adam_g")):
+            print("note: checkpoint has no optimiser state (reference-style); Adam restarts at t=0", file=out)
+
+    source = make_source(flags, B, shape, device, rank=rank, world=world)
+    sample_source = None
+    if chief and not flags.synthetic and os.path.isdir(flags.sample_image_dir):
+        sample_source = make_source(flags, B, shape, device, rank=0, world=1, data_dir=flags.sample_image_dir,
+                                    seed_offset=99, shuffle_buffer=min(int(flags.shuffle_buffer), 4 * B))
+    gen = torch.Generator().manual_seed(int(flags.seed) + 4242)
+    sample_z = (torch.rand(B, cfg.z_dim, generator=gen) * 2 - 1).to(device)  # fixed (image_train.py:77)
+
+    n_ex = source.num_examples
+    if flags.train_size != math.inf:
+        n_ex = min(n_ex, int(flags.train_size))
+    step_per_epoch = max(1, -(-n_ex // (B * world)))
+    max_steps = int(flags.max_steps)
+    if flags.epoch and int(flags.epoch) > 0:
+        max_steps = min(max_steps, int(flags.epoch) * step_per_epoch)
+
+    writer = SummaryWriter(flags.checkpoint_dir) if (chief and flags.summaries) else None
+    prof_range = None
+    if flags.profile_steps:
+        a, b = flags.profile_steps.split(":")
+        prof_range = (int(a), int(b))
+    prof = None
+    fault_at = int(os.environ.get("DCGAN_FAULT_AT_STEP", "-1"))
+
+    step = int(engine.global_step)
+    start_time = time.time()
+    next_summary = start_time + float(flags.save_summaries_secs)
+    last_rate_t, last_rate_step = start_time, step
+    try:
+        while step < max_steps:
+            if prof_range and step == prof_range[0] and prof is None:
+                prof = torch.profiler.profile(record_shapes=False, with_stack=False)
+                prof.__enter__()
+            engine.set_batch(source.next())
+            engine.train_step()
+            step += 1
+            if prof is not None and step >= prof_range[1]:
+                prof.__exit__(None, None, None)
+                if chief:
+                    prof.export_chrome_trace(os.path.join(flags.checkpoint_dir, "trace_rank%d.json" % rank))
+                prof = None
+            now = time.time()
+            summary_due = chief and writer is not None and now >= next_summary
+            if step % max(1, int(flags.log_every)) == 0 or summary_due or step == max_steps:
+                L = engine.last_losses()
+                ips = B * world * (step - last_rate_step) / max(1e-9, now - last_rate_t) if step > last_rate_step else 0.0
+                print(STEP_LINE % (step // step_per_epoch, step % step_per_epoch, now - start_time,
+                                   L["d_loss"], L["g_loss"]) + ", images/sec: %.1f" % ips, file=out, flush=True)
+                if summary_due:
+                    print("Running Summary operation on the chief.", file=out)
+                    rate = (step - last_rate_step) / max(1e-9, now - last_rate_t)
+                    vals = SUM.collect(engine, L, steps_per_sec=rate, loader_stats=source.stats())
+                    writer.add_summary_values(vals, step)
+                    writer.flush()
+                    print("Finished running Summary operation.", file=out)
+                    period = float(flags.save_summaries_secs)
+                    next_summary = next_summary + period if period > 0 else now
+                    while period > 0 and next_summary < now:
+                        next_summary += period
+                last_rate_t, last_rate_step = now, step
+            sample_now = int(flags.sample_every) > 0 and step % int(flags.sample_every) == 1
+            # the chief's time-based save decision is shared every SYNC_EVERY steps so that all
+            # ranks take part in the BN moving-average averaging that precedes a save
+            save_now = False
+            if step % SYNC_EVERY == 0 or step == max_steps:
+                due = chief and ckpt.save_secs > 0 and time.time() - ckpt.last_save >= ckpt.save_secs
+                save_now = D.any_rank(due, device) if world > 1 else due
+            if world > 1 and (sample_now or save_now):
+                engine.sync_bn_state()
+            if chief and sample_now:
+                _sample(engine, flags, sample_source, source, sample_z, step, step_per_epoch, out)
+            if chief and save_now:
+                ckpt.save(engine)
+            if fault_at >= 0 and step == fault_at:
+                print("DCGAN_FAULT_AT_STEP=%d: simulated failure" % fault_at, file=out, flush=True)
+                out.flush()
+                os._exit(3)
+        if world > 1:
+            engine.sync_bn_state()
+        if chief:
+            path = ckpt.save(engine)
+            print("saved %s" % path, file=out)
+    finally:
+        source.close()
+        if sample_source is not None:
+            sample_source.close()
+        if writer is not None:
+            writer.close()
+        D.barrier()
+        D.shutdown()
+    return 0
+
+
+def _sample(engine, flags, sample_source, source, sample_z, step, step_per_epoch, out) -> None:
+    """Chief sampling side path (image_train.py:179-192): EMA-BN sampler grid + sample losses."""
+    batch = (sample_source or source).next()
+    samples = engine.sampler(sample_z)
+    losses = engine.eval_losses(batch, sample_z)
+    n = samples.shape[0]
+    grid = (8, 8) if n == 64 else IM.grid_size(n)
+    path = os.path.join(flags.sample_dir, "train_{:02d}_{:04d}.png".format(step // step_per_epoch,
+                                                                          step % step_per_epoch))
+    IM.save_images(samples.detach().float().cpu().numpy(), grid, path)
+    print("[Sample] d_loss: %.8f, g_loss: %.8f" % (losses["d_loss"], losses["g_loss"]), file=out, flush=True)

@@ -53,7 +53,7 @@ EXTRA_FLAGS: List[Tuple[str, str, Any, str]] = [
     ("z_dim", "int", 100, "latent dimension"),
     ("depth", "int", 0, "number of stride-2 stages (0 = auto from output_size)"),
     ("max_channels", "int", 0, "cap on per-layer channels (0 = no cap)"),
-    ("save_model_secs", "int", 600, "chief checkpoint interval in seconds (reference Supervisor default 600)"),
+    ("save_model_secs", "float", 600.0,"chief checkpoint interval in seconds (reference Supervisor default 600)"),
     ("keep_checkpoints", "int", 5, "number of checkpoints to keep (TF Saver default 5)"),
     ("sample_every", "int", 100, "sample when global_step %% sample_every == 1 (reference: 100)"),
     ("engine", "str", "auto", "auto | hip | reference : which training step implementation"),

@@ -1,0 +1,148 @@
+"""TFRecord / tf.train.Example I/O (Python + native C++), loader semantics, sharding."""
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_tensorflow_for_dcgan_amd.data import native, pipeline as PL, tfrecord as TR
+from distributed_tensorflow_for_dcgan_amd.utils import wire
+
+
+def test_crc32c_vectors():
+    assert wire.crc32c_py(b"123456789") == 0xE3069283
+    assert native.crc32c(b"123456789") == 0xE3069283
+    data = os.urandom(10007)
+    assert native.crc32c(data) == wire.crc32c_py(data)
+    assert wire.unmask_crc(wire.mask_crc(0xDEADBEEF)) == 0xDEADBEEF
+
+
+def test_example_roundtrip_and_native_parse():
+    img = np.random.RandomState(0).uniform(-1, 1, (4, 4, 3))
+    ex = TR.encode_image_example(img, "float64")
+    d = wire.decode_example(ex)
+    assert set(d) == {"image_raw"} and len(d["image_raw"]) == 4 * 4 * 3 * 8
+    assert native.ext().example_feature(ex, "image_raw") == d["image_raw"]
+    assert native.ext().example_feature(ex, "nope") is None
+    back = TR.decode_image_example(ex, (4, 4, 3))
+    assert np.allclose(back, img.astype(np.float32))
+    multi = wire.encode_example({"a": b"xyz", "f": [1.5, 2.5], "i": [3, 400]})
+    dd = wire.decode_example(multi)
+    assert dd["a"] == b"xyz" and dd["f"] == [1.5, 2.5] and dd["i"] == [3, 400]
+
+
+def test_tfrecord_python_native_interop(tmp_path):
+    imgs = np.random.RandomState(1).uniform(-1, 1, (7, 8, 8, 3))
+    p = str(tmp_path / "a.tfrecords")
+    assert TR.write_image_records(p, imgs) == 7
+    py = list(TR.read_records(p))
+    nat = native.ext().read_records(p, True)
+    assert py == list(nat) and len(py) == 7
+    assert native.ext().count_records(p) == 7
+    p2 = str(tmp_path / "b.tfrecords")
+    native.ext().write_records(p2, py)
+    assert open(p, "rb").read() == open(p2, "rb").read()
+
+
+def test_corruption_detected(tmp_path):
+    p = str(tmp_path / "c.tfrecords")
+    TR.write_image_records(p, np.zeros((2, 4, 4, 3)))
+    raw = bytearray(open(p, "rb").read())
+    raw[20] ^= 0xFF
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(IOError):
+        list(TR.read_records(p))
+    with pytest.raises(RuntimeError):
+        native.ext().read_records(p, True)
+
+
+def _make_dataset(d, n_files=4, per_file=10, hw=8, c=3, dtype="float64"):
+    os.makedirs(d, exist_ok=True)
+    k = 0
+    for f in range(n_files):
+        imgs = np.zeros((per_file, hw, hw, c))
+        for i in range(per_file):
+            imgs[i] = (k % 200) / 100.0 - 1.0  # constant image encodes its id
+            k += 1
+        if dtype == "uint8":
+            imgs = ((imgs + 1) * 127.5).round().astype(np.uint8)
+        TR.write_image_records(os.path.join(d, "part-%d" % f), imgs, dtype)
+    return n_files * per_file
+
+
+def test_native_loader_covers_every_example_once_per_epoch(tmp_path):
+    d = str(tmp_path / "train")
+    n = _make_dataset(d)
+    files = TR.list_record_files(d)
+    L = native.ext().Loader(files, "image_raw", 8, 8, 3, 8, 16, 8, 1, 123, "f32", "auto", False, True,
+                            1 / 127.5, -1.0)
+    buf = torch.empty(8, 8, 8, 3)
+    ids = []
+    while True:
+        got = L.next_batch(buf.data_ptr())
+        ids += [round((float(buf[i, 0, 0, 0]) + 1) * 100) for i in range(got)]
+        if got < 8:
+            break
+    assert sorted(ids) == list(range(n))
+    assert ids != sorted(ids)  # shuffled
+    s = L.stats()
+    assert s["records"] == n
+
+
+def test_native_loader_bf16_and_uint8(tmp_path):
+    d = str(tmp_path / "u8")
+    _make_dataset(d, n_files=1, per_file=6, dtype="uint8")
+    L = native.ext().Loader(TR.list_record_files(d), "image_raw", 8, 8, 3, 6, 6, 0, 2, 1, "bf16", "auto", False,
+                            True, 1 / 127.5, -1.0)
+    buf = torch.empty(6, 8, 8, 3, dtype=torch.bfloat16)
+    assert L.next_batch(buf.data_ptr()) == 6
+    vals = sorted(set(round(float(v) * 100) for v in buf[:, 0, 0, 0]))
+    assert vals == [-100, -99, -98, -97, -96, -95]
+
+
+def test_shuffle_buffer_min_after_dequeue(tmp_path):
+    """RandomShuffleQueue semantics: the first batch is drawn from >= min_after_dequeue pooled."""
+    d = str(tmp_path / "s")
+    _make_dataset(d, n_files=1, per_file=100)
+    L = native.ext().Loader(TR.list_record_files(d), "image_raw", 8, 8, 3, 4, 60, 50, 1, 7, "f32", "auto", True,
+                            True, 1 / 127.5, -1.0)
+    buf = torch.empty(4, 8, 8, 3)
+    L.next_batch(buf.data_ptr())
+    assert L.stats()["records"] >= 54
+    L.stop()
+
+
+def test_sharding():
+    files = ["f%d" % i for i in range(10)]
+    parts = [PL.shard_files(files, r, 4, True)[0] for r in range(4)]
+    assert sorted(sum(parts, [])) == sorted(files)
+    assert all(set(a).isdisjoint(b) for i, a in enumerate(parts) for b in parts[i + 1:])
+    few, sharded = PL.shard_files(files[:2], 1, 4, True)
+    assert few == files[:2] and not sharded
+
+
+def test_tfrecord_source_end_to_end(tmp_path):
+    d = str(tmp_path / "train")
+    _make_dataset(d, n_files=2, per_file=20)
+    src = PL.TFRecordSource(d, 8, (8, 8, 3), "cpu", shuffle_buffer=10, threads=2, seed=3)
+    seen = []
+    for _ in range(10):
+        x = src.next()
+        assert x.shape == (8, 8, 8, 3) and x.dtype == torch.float32
+        seen += [round((float(v) + 1) * 100) for v in x[:, 0, 0, 0]]
+    assert set(seen) <= set(range(40)) and len(set(seen)) > 20
+    assert src.num_examples == 40
+    src.close()
+
+
+def test_image_folder_source(tmp_path):
+    from PIL import Image
+    d = tmp_path / "imgs"
+    d.mkdir()
+    for i in range(5):
+        Image.fromarray(np.full((20, 30, 3), i * 40, np.uint8)).save(str(d / ("%d.png" % i)))
+    src = PL.ImageFolderSource(str(d), 4, (8, 8, 3), "cpu", is_crop=True, image_size=16)
+    x = src.next()
+    assert x.shape == (4, 8, 8, 3) and float(x.min()) >= -1 and float(x.max()) <= 1
+    src.close()

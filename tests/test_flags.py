@@ -1,0 +1,69 @@
+"""CLI flag parity with the reference's tf.app.flags (image_train.py:10-40)."""
+import math
+
+import pytest
+
+from distributed_tensorflow_for_dcgan_amd.utils import flags as F
+
+REF_DEFAULTS = {
+    "epoch": 25, "learning_rate": 0.0002, "beta1": 0.5, "train_size": math.inf, "batch_size": 64,
+    "image_size": 108, "output_size": 64, "c_dim": 3, "dataset": "celebA", "checkpoint_dir": "checkpoint",
+    "sample_dir": "samples", "is_train": False, "is_crop": False, "visualize": False, "data_dir": "train",
+    "sample_image_dir": "sample_data", "ps_hosts": "", "worker_hosts": "", "job_name": "", "task_index": 0,
+    "log_device_placement": True, "save_summaries_secs": 10,
+}
+
+
+def test_all_reference_flags_with_defaults():
+    fl = F.parse_flags([])
+    assert len(F.REFERENCE_FLAGS) == 22
+    for k, v in REF_DEFAULTS.items():
+        assert getattr(fl, k) == v, k
+    assert set(REF_DEFAULTS) <= set(fl.as_dict())
+    assert fl.__getattr__("__flags")["batch_size"] == 64
+
+
+def test_flag_syntax_variants():
+    fl = F.parse_flags(["--batch_size=128", "--learning_rate", "0.001", "--is_crop", "--nolog_device_placement",
+                        "--is_train=false", "--train_size=inf", "--dataset", "mnist"])
+    assert fl.batch_size == 128 and fl.learning_rate == 0.001
+    assert fl.is_crop is True and fl.log_device_placement is False and fl.is_train is False
+    assert fl.train_size == math.inf and fl.dataset == "mnist"
+    fl = F.parse_flags(["--is_train=1", "--visualize", "true"])
+    assert fl.is_train is True and fl.visualize is True
+
+
+def test_unknown_flag_rejected():
+    with pytest.raises(SystemExit):
+        F.parse_flags(["--no_such_flag=1"])
+
+
+def test_cluster_mapping(monkeypatch):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    fl = F.parse_flags(["--job_name=worker", "--task_index=1", "--worker_hosts=127.0.0.1:2222,127.0.0.1:2223",
+                        "--ps_hosts=127.0.0.1:2221"])
+    c = F.cluster_from_flags(fl)
+    assert c["world_size"] == 2 and c["rank"] == 1 and c["master_port"] == 2222
+    monkeypatch.setenv("RANK", "3")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    c = F.cluster_from_flags(fl)
+    assert (c["rank"], c["world_size"], c["source"]) == (3, 8, "env")
+    monkeypatch.delenv("RANK")
+    monkeypatch.delenv("WORLD_SIZE")
+    with pytest.raises(ValueError):
+        F.cluster_from_flags(F.parse_flags(["--task_index=5", "--worker_hosts=a:1,b:2"]))
+
+
+def test_ps_role_exits_cleanly(tmp_path, capsys):
+    from distributed_tensorflow_for_dcgan_amd.train.trainer import run
+    fl = F.parse_flags(["--job_name=ps", "--checkpoint_dir=%s" % (tmp_path / "c")])
+    assert run(fl) == 0
+    assert "no parameter server" in capsys.readouterr().out
+
+
+def test_bad_job_name():
+    from distributed_tensorflow_for_dcgan_amd.train.trainer import run
+    with pytest.raises(SystemExit):
+        run(F.parse_flags(["--job_name=chief"]))
