@@ -340,7 +340,7 @@ extern "C" int dcg_linear_fwd(const float* z, const float* W, const float* b, bf
 
 extern "C" int dcg_linear_wgrad(const float* z, const bf16* dh, float* dW, float* db, int B, int K, int N,
                                 hipStream_t s) {
-  constexpr int KC = 20;
+  constexpr int KC = 4;  // 4 k-rows per block: (N/256) x (K/4) = 800 blocks for the 64x64 model
   if ((size_t)B * KC * sizeof(float) > 65536) return -2;
   dim3 grid((N + 255) / 256, (K + KC - 1) / KC);
   hipLaunchKernelGGL((linear_wgrad_kernel<KC>), grid, dim3(256), B * KC * sizeof(float), s, z, dh, dW, db, B, K, N);
