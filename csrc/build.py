@@ -67,7 +67,8 @@ def build_hip(verbose: bool = False, jobs: int = 8) -> str:
         inc = []
         for i in _py_includes():
             inc += ["-I", i]
-        jobs_list.append([HIPCC, "-O2", "-fPIC", "-std=c++17", "-I", CSRC] + inc + ["-c", binding, "-o", bo])
+        jobs_list.append([HIPCC, "-O2", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC] + inc +
+                         ["-c", binding, "-o", bo])
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for out in ex.map(_run, jobs_list):
             if verbose and out.strip():

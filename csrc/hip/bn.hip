@@ -1,16 +1,18 @@
 // BatchNorm (TF batch_norm_with_global_normalization semantics) and
 // activation kernels for gfx950, NHWC bf16 activations, fp32 statistics.
 //
-// Forward:  conv epilogue (igemm) or bn_stats -> per-tile partial sum / sum^2
+// Forward:  conv epilogue (igemm) or colstats -> per-tile partial sum / sum^2
 //           -> bn_finalize (fp64 combine, biased variance, EMA update of the moving averages,
 //              scale = gamma*rsqrt(var+eps), shift = beta - mean*scale)
 //           -> bn_apply_act (y = act(x*scale + shift), 8 x bf16 per thread)
-// Backward: bn_bwd_reduce (partials of sum g and sum g*xhat, g = dy*act'(y))
+// Backward: colstats mode 1 (partials of sum g and sum g*xhat, g = dy*act'(y))
 //           -> bn_bwd_finalize (d gamma, d beta into the flat fp32 gradient; per-group coefs)
-//           -> bn_bwd_apply (dx = a*g + c*x + d, bf16)
+//           -> bn_bwd_apply (dx = A*g + Bx*x + Cc, bf16)
 // Every reduction is two-stage with fixed order -> bitwise deterministic, no float atomics.
 // "groups" split the rows into equal contiguous parts with independent statistics, which is
 // how D(real) and D(fake) run as one 2B batch with the reference's per-call BN statistics.
+// Elementwise kernels: 16-byte vector loads/stores, 32-bit index math with precomputed
+// magic-number division, per-channel coefficients as float4 loads.
 #include "kernels.h"
 
 namespace dcg {
@@ -27,6 +29,13 @@ __device__ __forceinline__ void store8(bf16* p, const float* f) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) b[i] = (bf16)f[i];
   *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, b);
+}
+
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
 }
 
 // ---------------------------------------------------------------- column partial sums
@@ -51,8 +60,8 @@ __global__ __launch_bounds__(256) void colstats_kernel(int mode, const bf16* __r
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = 0.f; s2[i] = 0.f; mu[i] = 0.f; rs[i] = 0.f; }
   if (mode == 1) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { mu[i] = mean[g * C + cv * 8 + i]; rs[i] = rstd[g * C + cv * 8 + i]; }
+    load8f(mean + g * C + cv * 8, mu);
+    load8f(rstd + g * C + cv * 8, rs);
   }
   if (rl < lanes) {
     for (int r = r0 + rl; r < r1; r += lanes) {
@@ -95,36 +104,46 @@ __global__ __launch_bounds__(256) void colstats_kernel(int mode, const bf16* __r
 }
 
 // ---------------------------------------------------------------- partial-row reduction
-// Sum rows [p0, p1) of part (row stride `stride` floats) for 32 channels c0..c0+31, column
-// offsets off0 / off1 (two quantities per row). 256 threads = 32 channels x 8 row lanes; fixed
-// order -> deterministic. Result valid in lane 0 (threadIdx.x < 32).
+// Sum rows [p0, p1) of part (row stride `stride` floats) for the 16 channels of this block,
+// two quantities per row (column offsets 0 and off1). 256 threads = 16 channels x 16 row lanes,
+// each lane with 4 independent accumulators (latency hiding), fixed combine order ->
+// deterministic. Result valid in lane 0 (threadIdx.x < 16).
 template <typename T>
 __device__ __forceinline__ void reduce_rows2(const float* __restrict__ part, int p0, int p1, size_t stride, int c,
                                              bool cok, int off1, T& s1, T& s2) {
-  __shared__ T red[2][8][33];
-  const int ch = threadIdx.x & 31, lane = threadIdx.x >> 5;
-  T a = 0, b = 0;
-  if (cok)
-    for (int p = p0 + lane; p < p1; p += 8) {
-      a += (T)part[(size_t)p * stride + c];
-      if (off1 >= 0) b += (T)part[(size_t)p * stride + off1 + c];
-    }
-  red[0][lane][ch] = a;
-  red[1][lane][ch] = b;
-  __syncthreads();
-  if (lane == 0) {
-    a = 0; b = 0;
+  __shared__ T red[2][16][17];
+  const int ch = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  T a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  if (cok) {
+    int p = p0 + lane;
+    for (; p + 48 < p1; p += 64) {
 #pragma unroll
-    for (int l = 0; l < 8; ++l) { a += red[0][l][ch]; b += red[1][l][ch]; }
+      for (int u = 0; u < 4; ++u) {
+        a[u] += (T)part[(size_t)(p + 16 * u) * stride + c];
+        if (off1 >= 0) b[u] += (T)part[(size_t)(p + 16 * u) * stride + off1 + c];
+      }
+    }
+    for (; p < p1; p += 16) {
+      a[0] += (T)part[(size_t)p * stride + c];
+      if (off1 >= 0) b[0] += (T)part[(size_t)p * stride + off1 + c];
+    }
+  }
+  red[0][lane][ch] = (a[0] + a[1]) + (a[2] + a[3]);
+  red[1][lane][ch] = (b[0] + b[1]) + (b[2] + b[3]);
+  __syncthreads();
+  T x = 0, y = 0;
+  if (lane == 0) {
+#pragma unroll
+    for (int l = 0; l < 16; ++l) { x += red[0][l][ch]; y += red[1][l][ch]; }
   }
   __syncthreads();
-  s1 = a;
-  s2 = b;
+  s1 = x;
+  s2 = y;
 }
 
 // ---------------------------------------------------------------- BN forward finalize
 // part: [P][2][C], partials of group g are [g*ppg, (g+1)*ppg). count = rows per group.
-// grid (ceil(C/32), groups), block 256.
+// grid (ceil(C/16), groups), block 256.
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int ppg, int groups, int C,
                                                           double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps,
@@ -133,11 +152,11 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ ema_mean, float* __restrict__ ema_var,
                                                           float decay) {
   const int g = blockIdx.y;
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C;
   double s, s2;
   reduce_rows2<double>(part, g * ppg, (g + 1) * ppg, (size_t)2 * C, c, cok, C, s, s2);
-  if ((threadIdx.x >> 5) != 0 || !cok) return;
+  if ((threadIdx.x >> 4) != 0 || !cok) return;
   const int idx = g * C + c;
   const double m = s / count;
   double v = s2 / count - m * m;
@@ -170,36 +189,38 @@ __global__ void bn_coef_eval_kernel(int C, const float* __restrict__ gamma, cons
 }
 
 // ---------------------------------------------------------------- BN apply + activation
+// nv = R*C/8 vectors; vector v: row = v / C8, channel base = (v % C8) * 8, group = row / rpg
 __global__ __launch_bounds__(256) void bn_apply_act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                            const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, int R, int C,
-                                                           int rows_per_group, int act, float leak) {
-  const size_t nv = (size_t)R * C / 8;
-  for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
-    const size_t e = v * 8;
-    const int r = (int)(e / C), c = (int)(e - (size_t)r * C);
-    const int g = r / rows_per_group;
-    float xv[8];
-    load8(x + e, xv);
+                                                           const float* __restrict__ shift, uint32_t nv, int C,
+                                                           FastDiv fd_c8, FastDiv fd_rpg, int act, float leak) {
+  for (uint32_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += gridDim.x * 256) {
+    const uint32_t r = fdiv(v, fd_c8);
+    const int c = (int)(v - r * fd_c8.d) * 8;
+    const int g = (int)fdiv(r, fd_rpg);
+    float xv[8], sc[8], sh[8];
+    load8(x + (size_t)v * 8, xv);
+    load8f(scale + g * C + c, sc);
+    load8f(shift + g * C + c, sh);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      xv[i] = apply_act(xv[i] * scale[g * C + c + i] + shift[g * C + c + i], act, leak);
-    store8(y + e, xv);
+    for (int i = 0; i < 8; ++i) xv[i] = apply_act(xv[i] * sc[i] + sh[i], act, leak);
+    store8(y + (size_t)v * 8, xv);
   }
 }
 
 // ---------------------------------------------------------------- BN backward finalize
 // part: [P][2][C] (sum g, sum g*xhat). Writes dgamma/dbeta (sum over groups) when non-null and
-// the per-(group, channel) affine coefficients of dx = A*g + Bc*x + D. grid ceil(C/32), block 256.
+// per-(group, channel) coefficients of dx = A*g + Bx*x + Cc, layout coef[g][3][C].
+// grid ceil(C/16), block 256.
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int ppg, int groups,
                                                               int C, float count, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ rstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ coef) {
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C;
-  const bool lead = (threadIdx.x >> 5) == 0 && cok;
+  const bool lead = (threadIdx.x >> 4) == 0 && cok;
   float dg = 0.f, db = 0.f;
   for (int g = 0; g < groups; ++g) {
     float s1, s2;
@@ -211,9 +232,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
       const float a = gamma[c] * r;
       const float c2 = -a * s2 / count;  // multiplies xhat
       const float b = -a * s1 / count;
-      coef[(g * C + c) * 3 + 0] = a;
-      coef[(g * C + c) * 3 + 1] = c2 * r;            // * x
-      coef[(g * C + c) * 3 + 2] = b - c2 * mu * r;   // constant
+      coef[(g * 3 + 0) * C + c] = a;
+      coef[(g * 3 + 1) * C + c] = c2 * r;            // * x
+      coef[(g * 3 + 2) * C + c] = b - c2 * mu * r;   // constant
     }
   }
   if (lead) {
@@ -225,41 +246,49 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
                                                            const bf16* __restrict__ x,
                                                            const float* __restrict__ coef, bf16* __restrict__ dx,
-                                                           int R, int C, int rows_per_group, int act, float leak) {
-  const size_t nv = (size_t)R * C / 8;
-  for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
-    const size_t e = v * 8;
-    const int r = (int)(e / C), c = (int)(e - (size_t)r * C);
-    const int g = r / rows_per_group;
-    float dv[8], yv[8], xv[8];
-    load8(dy + e, dv);
-    load8(y + e, yv);
-    load8(x + e, xv);
+                                                           uint32_t nv, int C, FastDiv fd_c8, FastDiv fd_rpg, int act,
+                                                           float leak) {
+  for (uint32_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += gridDim.x * 256) {
+    const uint32_t r = fdiv(v, fd_c8);
+    const int c = (int)(v - r * fd_c8.d) * 8;
+    const int g = (int)fdiv(r, fd_rpg);
+    float dv[8], yv[8], xv[8], ca[8], cb[8], cc[8];
+    load8(dy + (size_t)v * 8, dv);
+    load8(y + (size_t)v * 8, yv);
+    load8(x + (size_t)v * 8, xv);
+    load8f(coef + (g * 3 + 0) * C + c, ca);
+    load8f(coef + (g * 3 + 1) * C + c, cb);
+    load8f(coef + (g * 3 + 2) * C + c, cc);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float* cf = coef + (g * C + c + i) * 3;
-      const float gv = dv[i] * act_grad_from_out(yv[i], act, leak);
-      dv[i] = cf[0] * gv + cf[1] * xv[i] + cf[2];
-    }
-    store8(dx + e, dv);
+    for (int i = 0; i < 8; ++i) dv[i] = ca[i] * (dv[i] * act_grad_from_out(yv[i], act, leak)) + cb[i] * xv[i] + cc[i];
+    store8(dx + (size_t)v * 8, dv);
   }
 }
 
 // ---------------------------------------------------------------- activation backward (no BN)
-// dx = dy * act'(y); n elements (any count), scalar tail
+// dx = dy * act'(y); 8 per thread + scalar tail
 __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
                                                       bf16* __restrict__ dx, size_t n, int act, float leak) {
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+  const size_t nv = n / 8;
+  for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
+    float dv[8], yv[8];
+    load8(dy + v * 8, dv);
+    load8(y + v * 8, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dv[i] *= act_grad_from_out(yv[i], act, leak);
+    store8(dx + v * 8, dv);
+  }
+  for (size_t i = nv * 8 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
     dx[i] = (bf16)((float)dy[i] * act_grad_from_out((float)y[i], act, leak));
 }
 
-// sum over partial rows -> dst[C]; grid ceil(C/32), block 256
+// sum over partial rows -> dst[C]; grid ceil(C/16), block 256
 __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part, int P, int stride, int C,
                                                            float* __restrict__ dst) {
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   float s, unused;
   reduce_rows2<float>(part, 0, P, (size_t)stride, c, c < C, -1, s, unused);
-  if ((threadIdx.x >> 5) == 0 && c < C) dst[c] = s;
+  if ((threadIdx.x >> 4) == 0 && c < C) dst[c] = s;
 }
 
 // column sums for a small channel count (C <= 16), e.g. dbias of a 3-channel image gradient
@@ -305,8 +334,8 @@ extern "C" int dcg_colstats(int mode, const bf16* x, const bf16* dy, const bf16*
 extern "C" int dcg_bn_finalize(const float* part, int ppg, int groups, int C, double count, const float* gamma,
                                const float* beta, float eps, float* mean, float* rstd, float* scale, float* shift,
                                float* ema_mean, float* ema_var, float decay, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32, groups), dim3(256), 0, s, part, ppg, groups, C, count, gamma,
-                     beta, eps, mean, rstd, scale, shift, ema_mean, ema_var, decay);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16, groups), dim3(256), 0, s, part, ppg, groups, C, count,
+                     gamma, beta, eps, mean, rstd, scale, shift, ema_mean, ema_var, decay);
   return (int)hipGetLastError();
 }
 
@@ -320,15 +349,17 @@ extern "C" int dcg_bn_coef_eval(int C, const float* gamma, const float* beta, fl
 extern "C" int dcg_bn_apply_act(const bf16* x, bf16* y, const float* scale, const float* shift, int R, int C,
                                 int rows_per_group, int act, float leak, hipStream_t s) {
   if (C % 8) return -2;
-  hipLaunchKernelGGL(bn_apply_act_kernel, dim3(ew_blocks((size_t)R * C / 8)), dim3(256), 0, s, x, y, scale, shift,
-                     R, C, rows_per_group, act, leak);
+  const size_t nv = (size_t)R * C / 8;
+  if (nv >= 0x80000000ull) return -3;
+  hipLaunchKernelGGL(bn_apply_act_kernel, dim3(ew_blocks(nv)), dim3(256), 0, s, x, y, scale, shift, (uint32_t)nv, C,
+                     fastdiv_make(C / 8), fastdiv_make(rows_per_group), act, leak);
   return (int)hipGetLastError();
 }
 
 extern "C" int dcg_bn_bwd_finalize(const float* part, int ppg, int groups, int C, float count, const float* gamma,
                                    const float* mean, const float* rstd, float* dgamma, float* dbeta, float* coef,
                                    hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, s, part, ppg, groups, C, count,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, ppg, groups, C, count,
                      gamma, mean, rstd, dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }
@@ -336,18 +367,20 @@ extern "C" int dcg_bn_bwd_finalize(const float* part, int ppg, int groups, int C
 extern "C" int dcg_bn_bwd_apply(const bf16* dy, const bf16* y, const bf16* x, const float* coef, bf16* dx, int R,
                                 int C, int rows_per_group, int act, float leak, hipStream_t s) {
   if (C % 8) return -2;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks((size_t)R * C / 8)), dim3(256), 0, s, dy, y, x, coef, dx,
-                     R, C, rows_per_group, act, leak);
+  const size_t nv = (size_t)R * C / 8;
+  if (nv >= 0x80000000ull) return -3;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nv)), dim3(256), 0, s, dy, y, x, coef, dx, (uint32_t)nv, C,
+                     fastdiv_make(C / 8), fastdiv_make(rows_per_group), act, leak);
   return (int)hipGetLastError();
 }
 
 extern "C" int dcg_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t n, int act, float leak, hipStream_t s) {
-  hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, dy, y, dx, n, act, leak);
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_blocks(n / 8 + 1)), dim3(256), 0, s, dy, y, dx, n, act, leak);
   return (int)hipGetLastError();
 }
 
 extern "C" int dcg_sum_partials(const float* part, int P, int stride, int C, float* dst, hipStream_t s) {
-  hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 31) / 32), dim3(256), 0, s, part, P, stride, C, dst);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, P, stride, C, dst);
   return (int)hipGetLastError();
 }
 

@@ -55,6 +55,14 @@ __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t o
 
 constexpr uint32_t OOB = 0x80000000u;  // any offset past the descriptor size
 
+// 16-byte LDS-DMA: buffer_load_dwordx4 ... lds. The wave's 64 lanes write 1 KiB contiguously at
+// `lds` (wave-uniform) + 16 * lane; the global offset is per lane (out of range -> zeros).
+__device__ __forceinline__ void buf_load16_lds(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+#endif
+}
+
 // Unsigned division by a runtime-invariant divisor (round-up multiply method, exact for all
 // 32-bit n). Host computes {mul, shift} with fastdiv_make().
 struct FastDiv {

@@ -11,22 +11,27 @@
 // Weights are pre-packed bf16 [25][N][Kc] (k contiguous per output channel), so both operands
 // are "K-contiguous rows" and every fragment is one 16-byte ds_read_b128.
 //
-// Block = 256 threads (4 waves, WM x WN wave grid), tile BM x BN x 64. Register-staged double
-// buffer: the next K-tile's global loads are issued before the current tile's MFMAs and written
-// to the other LDS buffer after them (one barrier per K-tile). LDS rows are 128 B with a
-// chunk ^= (row & 7) XOR swizzle (conflict-free ds_read_b128 for the 16x16x32 A/B maps).
-// A-operand gathers use buffer loads whose out-of-range offset returns zeros, which implements
-// the conv zero padding with no branches.
+// Block = 256 threads (4 waves, WM x WN wave grid), tile BM x BN x 64, two LDS stages, one
+// barrier per K-tile. Two staging variants (template STAGING):
+//   0: register staging -- next tile's 16-byte global loads issued before the current tile's
+//      MFMAs, written to the other LDS stage after them (ds_write_b128).
+//   1: LDS-DMA staging -- `buffer_load_dwordx4 ... lds` writes each 1 KiB wave piece (8 rows x
+//      128 B) straight into LDS: no VGPR staging, no ds_write. The LDS image is lane-linear, so
+//      the XOR swizzle is applied to the per-lane SOURCE chunk (rule: linear dest + swizzled
+//      source + the same XOR on the read).
+// LDS rows are 128 B with a chunk ^= (row & 7) swizzle: conflict-free ds_read_b128 for the
+// 16x16x32 A/B fragment maps. A-operand gathers use buffer loads whose out-of-range offset
+// returns zeros, which implements the conv zero padding with no branches.
 //
-// Fused epilogue: + bias, per-channel BN partial statistics (sum, sum of squares over the
-// tile's rows, written per (M-tile, phase) for a deterministic finalize), activation
-// (relu / lrelu / tanh), bf16 or fp32 store with the phase's pixel scatter, optional channel
-// offset (writes into a slice of a wider tensor).
+// Fused epilogue: + bias, per-channel BN partial statistics (sum, sum^2 of the stored bf16
+// value over the tile's rows, per (M-tile, phase) for a deterministic finalize), activation
+// (relu / lrelu / tanh), pixel scatter of the phase, output staged through LDS and written as
+// 16-byte row segments (bf16, N % 8 == 0) or element-wise (fp32 / narrow N).
 #include "kernels.h"
 
 namespace dcg {
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int STAGING>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -34,6 +39,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr int A_CH = BM * 8, B_CH = BN * 8;
   constexpr int A_PT = (A_CH + 255) / 256, B_PT = (B_CH + 255) / 256;
   constexpr int STAGE = (BM + BN) * 8;  // 16-byte units per stage
+  constexpr int NPA = BM / 8, NPB = BN / 8;  // 1 KiB LDS-DMA pieces per stage
+  constexpr int PPW_A = (NPA + 3) / 4, PPW_B = (NPB + 3) / 4;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(FM >= 1 && FN >= 1, "tile");
   __shared__ __attribute__((aligned(16))) u32x4 lds[2 * STAGE];
@@ -60,13 +67,18 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, p.b_bytes);
 
-  // ---- per-thread A rows (fixed for the whole K loop)
-  int a_bh[A_PT], a_iy[A_PT], a_ix[A_PT];
-  bool a_ok[A_PT];
-  const int chunk = tid & 7;
+  // ---- the A rows this thread loads (fixed for the whole K loop)
+  constexpr int AR = STAGING ? PPW_A : A_PT;
+  int a_bh[AR], a_iy[AR], a_ix[AR], a_row[AR];
+  bool a_ok[AR];
+  // register staging: row = (tid + 256 i) / 8, chunk = tid & 7
+  // LDS-DMA: piece q = wave + 4 i, row = 8 q + lane / 8, LDS slot = lane & 7,
+  //          global chunk = slot ^ (row & 7) = (lane & 7) ^ (lane >> 3)
+  const int chunk = STAGING ? ((lane & 7) ^ (lane >> 3)) : (tid & 7);
 #pragma unroll
-  for (int i = 0; i < A_PT; ++i) {
-    const int r = (tid + 256 * i) >> 3;
+  for (int i = 0; i < AR; ++i) {
+    const int r = STAGING ? (8 * (wave + 4 * i) + (lane >> 3)) : ((tid + 256 * i) >> 3);
+    a_row[i] = r;
     const int m = m0 + r;
     a_ok[i] = (r < BM) && (m < M);
     if (p.plain) {
@@ -82,49 +94,73 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     }
   }
 
-  u32x4 ra_reg[A_PT], rb_reg[B_PT];
+  auto a_offset = [&](int i, int dy, int dx, int cc, bool kval) -> uint32_t {
+    uint32_t off = OOB;
+    if (p.plain) {
+      if (a_ok[i] && kval) off = (uint32_t)(a_bh[i] * Kc + cc) * 2u;
+    } else {
+      const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
+      if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+        off = (uint32_t)(((a_bh[i] + iy) * p.W + ix) * Kc + cc) * 2u;
+    }
+    return off;
+  };
 
-  auto load_tile = [&](int kt) {
+  u32x4 ra_reg[STAGING ? 1 : A_PT], rb_reg[STAGING ? 1 : B_PT];
+
+  auto load_tile = [&](int kt, int buf) {
     const int ti = kt / kt_per_tap;
     const int c0 = (kt - ti * kt_per_tap) * BK;
     const int cc = c0 + chunk * 8;
     const bool kval = cc < Kc;
     int dy = 0, dx = 0, wt = 0;
     if (!p.plain) { dy = ph->dy[ti]; dx = ph->dx[ti]; wt = ph->wtap[ti]; }
+    if constexpr (STAGING) {
+      u32x4* sa = lds + buf * STAGE;
+      u32x4* sb = sa + BM * 8;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) {
-      uint32_t off = OOB;
-      if (p.plain) {
-        if (a_ok[i] && kval) off = (uint32_t)(a_bh[i] * Kc + cc) * 2u;
-      } else {
-        const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
-        if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
-          off = (uint32_t)(((a_bh[i] + iy) * p.W + ix) * Kc + cc) * 2u;
+      for (int i = 0; i < PPW_A; ++i) {
+        const int q = wave + 4 * i;
+        if (NPA % 4 == 0 || q < NPA)
+          buf_load16_lds(ra, sa + q * 64, a_offset(i, dy, dx, cc, kval));
       }
-      ra_reg[i] = buf_load16(ra, off);
-    }
 #pragma unroll
-    for (int i = 0; i < B_PT; ++i) {
-      const int r = (tid + 256 * i) >> 3;
-      const int n = n0 + r;
-      uint32_t off = OOB;
-      if (r < BN && n < N && kval) off = (uint32_t)((wt * N + n) * Kc + cc) * 2u;
-      rb_reg[i] = buf_load16(rb, off);
+      for (int i = 0; i < PPW_B; ++i) {
+        const int q = wave + 4 * i;
+        if (NPB % 4 == 0 || q < NPB) {
+          const int n = n0 + 8 * q + (lane >> 3);
+          const uint32_t off = (n < N && kval) ? (uint32_t)((wt * N + n) * Kc + cc) * 2u : OOB;
+          buf_load16_lds(rb, sb + q * 64, off);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PT; ++i) ra_reg[i] = buf_load16(ra, a_offset(i, dy, dx, cc, kval));
+#pragma unroll
+      for (int i = 0; i < B_PT; ++i) {
+        const int r = (tid + 256 * i) >> 3;
+        const int n = n0 + r;
+        uint32_t off = OOB;
+        if (r < BN && n < N && kval) off = (uint32_t)((wt * N + n) * Kc + cc) * 2u;
+        rb_reg[i] = buf_load16(rb, off);
+      }
     }
   };
 
-  auto store_tile = [&](int buf) {
-    u32x4* sa = lds + buf * STAGE;
-    u32x4* sb = sa + BM * 8;
+  auto store_tile = [&](int buf) {  // register staging only
+    if constexpr (!STAGING) {
+      u32x4* sa = lds + buf * STAGE;
+      u32x4* sb = sa + BM * 8;
 #pragma unroll
-    for (int i = 0; i < A_PT; ++i) {
-      const int r = (tid + 256 * i) >> 3;
-      if (A_CH % 256 == 0 || r < BM) sa[r * 8 + (chunk ^ (r & 7))] = ra_reg[i];
-    }
+      for (int i = 0; i < A_PT; ++i) {
+        const int r = (tid + 256 * i) >> 3;
+        if (A_CH % 256 == 0 || r < BM) sa[r * 8 + (chunk ^ (r & 7))] = ra_reg[i];
+      }
 #pragma unroll
-    for (int i = 0; i < B_PT; ++i) {
-      const int r = (tid + 256 * i) >> 3;
-      if (B_CH % 256 == 0 || r < BN) sb[r * 8 + (chunk ^ (r & 7))] = rb_reg[i];
+      for (int i = 0; i < B_PT; ++i) {
+        const int r = (tid + 256 * i) >> 3;
+        if (B_CH % 256 == 0 || r < BN) sb[r * 8 + (chunk ^ (r & 7))] = rb_reg[i];
+      }
     }
   };
 
@@ -134,14 +170,15 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  load_tile(0);
+  load_tile(0, 0);
   store_tile(0);
+  if constexpr (STAGING) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < KT) load_tile(kt + 1);
+    if (kt + 1 < KT) load_tile(kt + 1, buf ^ 1);
     const u32x4* sa = lds + buf * STAGE;
     const u32x4* sb = sa + BM * 8;
 #pragma unroll
@@ -165,13 +202,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < KT) store_tile(buf ^ 1);
+    if constexpr (STAGING) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ------------------------------------------------------------------ epilogue
-  // output row offsets (elements) for the BM rows of this tile, via LDS
+  // LDS reuse: rowoff[BM] ints | red[WM][BN][2] floats | C tile [BM][BN + 8] bf16
   int* rowoff = reinterpret_cast<int*>(lds);
-  float* red = reinterpret_cast<float*>(lds) + BM;  // [WM][BN][2]
+  float* red = reinterpret_cast<float*>(lds) + BM;
+  constexpr int CPAD = BN + 8;
+  bf16* ctile = reinterpret_cast<bf16*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
+  static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= 2 * STAGE * 16, "epilogue LDS");
   for (int r = tid; r < BM; r += 256) {
     const int m = m0 + r;
     int off = -1;
@@ -192,6 +233,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   __syncthreads();
 
   const bool do_stats = p.stats != nullptr;
+  // vector store path: bf16 output, whole 8-channel groups, aligned destination
+  const bool vec = !p.out_f32 && (BN % 8 == 0) && (N % 8 == 0) && (p.ldc % 8 == 0) && (p.cofs % 8 == 0);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int nl = wn * TN + j * 16 + fr;
@@ -206,13 +249,18 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
         const int ml = wm * TM + i * 16 + fq * 4 + r;
         const int off = rowoff[ml];
         const float v = acc[i][j][r] + bv;
+        const bf16 vb = f2bf(v);
         if (off >= 0 && nok) {
           // statistics of exactly the stored (bf16-rounded) tensor, so BN forward/backward
           // see one consistent x
-          const float vs = p.out_f32 ? v : (float)f2bf(v);
+          const float vs = p.out_f32 ? v : (float)vb;
           s += vs;
           s2 += vs * vs;
-          const float o = apply_act(v, p.act, p.leak);
+        }
+        const float o = apply_act(v, p.act, p.leak);
+        if (vec) {
+          ctile[ml * CPAD + nl] = f2bf(o);
+        } else if (off >= 0 && nok) {
           if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
           else reinterpret_cast<bf16*>(p.C)[off + p.cofs + n] = f2bf(o);
         }
@@ -229,8 +277,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       }
     }
   }
+  if (do_stats || vec) __syncthreads();
+  if (vec) {
+    constexpr int CPR = BN / 8;  // 16-byte chunks per row
+    bf16* C = reinterpret_cast<bf16*>(p.C);
+    for (int q = tid; q < BM * CPR; q += 256) {
+      const int r = q / CPR, c = q - r * CPR;
+      const int off = rowoff[r];
+      const int n = n0 + 8 * c;
+      if (off >= 0 && n < N)
+        *reinterpret_cast<u32x4*>(C + off + p.cofs + n) = *reinterpret_cast<const u32x4*>(ctile + r * CPAD + 8 * c);
+    }
+  }
   if (do_stats) {
-    __syncthreads();
     for (int nl = tid; nl < BN; nl += 256) {
       const int n = n0 + nl;
       if (n >= N) continue;
@@ -250,14 +309,16 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
 }  // namespace dcg
 
 // ---------------------------------------------------------------------------- host launch
-// Tile configurations (BM, BN, WM, WN); the engine picks one per layer.
+// Tile configurations (BM, BN, WM, WN); the engine picks one per layer. cfg + 100 selects the
+// LDS-DMA staging variant of the same tile.
 #define DCG_IGEMM_CONFIGS(X) \
   X(0, 128, 128, 2, 2) X(1, 128, 64, 2, 2) X(2, 64, 128, 2, 2) X(3, 64, 64, 2, 2) \
   X(4, 32, 64, 2, 2) X(5, 64, 32, 2, 2) X(6, 32, 32, 2, 2) X(7, 128, 16, 4, 1) \
   X(8, 64, 16, 4, 1) X(9, 256, 64, 4, 1)
 
 extern "C" int dcg_igemm_tile(int cfg, int* bm, int* bn) {
-#define X(id, BM_, BN_, WM_, WN_) if (cfg == id) { *bm = BM_; *bn = BN_; return 0; }
+  const int c = cfg % 100;
+#define X(id, BM_, BN_, WM_, WN_) if (c == id) { *bm = BM_; *bn = BN_; return 0; }
   DCG_IGEMM_CONFIGS(X)
 #undef X
   return -1;
@@ -265,9 +326,14 @@ extern "C" int dcg_igemm_tile(int cfg, int* bm, int* bn) {
 
 extern "C" int dcg_igemm_launch(const dcg::IGemmArgs* a, int cfg, int mtiles, int ntiles, hipStream_t s) {
   dim3 grid(mtiles, ntiles, a->nphases);
-#define X(id, BM_, BN_, WM_, WN_) \
-  if (cfg == id) { hipLaunchKernelGGL((dcg::igemm_kernel<BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, *a); \
-                   return (int)hipGetLastError(); }
+  const int c = cfg % 100;
+  const bool glds = cfg >= 100;
+#define X(id, BM_, BN_, WM_, WN_)                                                                    \
+  if (c == id) {                                                                                    \
+    if (glds) hipLaunchKernelGGL((dcg::igemm_kernel<BM_, BN_, WM_, WN_, 1>), grid, dim3(256), 0, s, *a); \
+    else hipLaunchKernelGGL((dcg::igemm_kernel<BM_, BN_, WM_, WN_, 0>), grid, dim3(256), 0, s, *a);      \
+    return (int)hipGetLastError();                                                                  \
+  }
   DCG_IGEMM_CONFIGS(X)
 #undef X
   return -1;

@@ -218,17 +218,17 @@ __global__ void step_end_kernel(float* __restrict__ pd, float* __restrict__ pg, 
 
 // ---------------------------------------------------------------- weight packing
 // src fp32 [T][A][Bd] -> nat bf16 (same order, optional) and tr bf16 at t*st + b*sb + a*sa
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, int T, int A, int Bd,
-                                                   bf16* __restrict__ nat, bf16* __restrict__ tr, int st, int sb,
-                                                   int sa) {
-  const size_t n = (size_t)T * A * Bd;
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, uint32_t n, FastDiv fd_b,
+                                                   FastDiv fd_a, bf16* __restrict__ nat, bf16* __restrict__ tr,
+                                                   int st, int sb, int sa) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const float v = src[i];
-    const int b = (int)(i % Bd);
-    const size_t ta = i / Bd;
-    const int a = (int)(ta % A), t = (int)(ta / A);
+    const uint32_t ta = fdiv(i, fd_b);
+    const uint32_t b = i - ta * fd_b.d;
+    const uint32_t t = fdiv(ta, fd_a);
+    const uint32_t a = ta - t * fd_a.d;
     if (nat) nat[i] = (bf16)v;
-    if (tr) tr[(size_t)t * st + (size_t)b * sb + (size_t)a * sa] = (bf16)v;
+    if (tr) tr[t * st + b * sb + a * sa] = (bf16)v;
   }
 }
 
@@ -388,8 +388,10 @@ extern "C" int dcg_step_end(float* pd, float* pg, float b1d, float b2d, float b1
 
 extern "C" int dcg_pack(const float* src, int T, int A, int Bd, bf16* nat, bf16* tr, int st, int sb, int sa,
                         hipStream_t s) {
-  hipLaunchKernelGGL(pack_kernel, dim3(grid_for((size_t)T * A * Bd)), dim3(256), 0, s, src, T, A, Bd, nat, tr, st,
-                     sb, sa);
+  const size_t n = (size_t)T * A * Bd;
+  if (n >= 0x80000000ull) return -3;
+  hipLaunchKernelGGL(pack_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, (uint32_t)n, fastdiv_make(Bd),
+                     fastdiv_make(A), nat, tr, st, sb, sa);
   return (int)hipGetLastError();
 }
 

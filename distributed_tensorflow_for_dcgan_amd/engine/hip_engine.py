@@ -191,26 +191,20 @@ class HipEngine:
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
                cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None):
-        if mode == 1:
-            M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
-            phases = 4
-        else:
-            M = Bn * Hout * Wout
-            phases = 1
-        cfg = H.pick_igemm_cfg(M, N, phases, rows_per_group)
+        cfg = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group)
         prog.igemm(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
                    ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0)
         return cfg
 
-    def _igemm_stats_tiles(self, mode, Bn, Hout, Wout, N, rows_per_group=None):
+    def _igemm_stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None):
         if mode == 1:
             M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
             phases = 4
         else:
             M = Bn * Hout * Wout
             phases = 1
-        cfg = H.pick_igemm_cfg(M, N, phases, rows_per_group)
-        bm, _ = H.IGEMM_CFGS[cfg]
+        cfg = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group)
+        bm, _ = H.IGEMM_CFGS[cfg % 100]
         return -(-M // bm) * phases
 
     def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema):
@@ -257,7 +251,7 @@ class HipEngine:
             nat, tr = self.wp[L.name]
             pad = same_pads(L.out_hw)[0]
             if L.bn:
-                P = self._igemm_stats_tiles(1, B, L.out_hw, L.out_hw, L.cout)
+                P = self._igemm_stats_tiles(1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout)
                 part = self._stats_buf(L.bn, P, L.cout)
                 self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
                             L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part)
@@ -287,7 +281,7 @@ class HipEngine:
                 if H.pick_igemm_cfg(rows, L.cout, 1, rpg) is not None:
                     # BN partial statistics straight from the conv epilogue (tiles never straddle
                     # the real/fake boundary)
-                    P = self._igemm_stats_tiles(0, B2, L.out_hw, L.out_hw, L.cout, rpg)
+                    P = self._igemm_stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg)
                     part = self._stats_buf(L.bn, P, L.cout)
                     self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                 L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg)

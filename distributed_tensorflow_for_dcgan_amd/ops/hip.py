@@ -97,6 +97,39 @@ def pick_igemm_cfg(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
     return best  # None when no tile divides rows_per_group (caller computes stats separately)
 
 
+_TUNED = None
+TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "igemm_tuned.json")
+
+
+def tuned_table() -> dict:
+    """Per-layer tile choices measured on MI355X by ``benchmarks/bench_kernels.py --write``
+    (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> cfg; cfg >= 100 selects LDS-DMA staging)."""
+    global _TUNED
+    if _TUNED is None:
+        _TUNED = {}
+        if os.environ.get("DCGAN_NO_TUNED") != "1" and os.path.exists(TUNED_PATH):
+            import json
+            with open(TUNED_PATH) as f:
+                _TUNED = {k: int(v) for k, v in json.load(f).items()}
+    return _TUNED
+
+
+def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wout: int, N: int,
+                  rows_per_group: Optional[int] = None) -> Optional[int]:
+    """Tile for one implicit-GEMM launch: the tuned entry when present and legal for the
+    BN-statistics grouping, else the occupancy heuristic of :func:`pick_igemm_cfg`."""
+    if mode == 1:
+        M, phases = Bn * (-(-Hout // 2)) * (-(-Wout // 2)), 4
+    else:
+        M, phases = Bn * Hout * Wout, 1
+    cfg = tuned_table().get("%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N))
+    if cfg is not None and cfg % 100 in IGEMM_CFGS:
+        bm, _ = IGEMM_CFGS[cfg % 100]
+        if rows_per_group is None or rows_per_group % bm == 0:
+            return cfg
+    return pick_igemm_cfg(M, N, phases, rows_per_group)
+
+
 def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_COUNT) -> Tuple[int, int]:
     """(cfg, splits) for a weight-gradient GEMM of Mc x Nc per tap over K pixels."""
     if Mc >= 128 and Nc >= 128:
@@ -161,7 +194,7 @@ def conv2d_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, bias: Option
     py, px = same_pads(H)[0], same_pads(W)[0]
     M = B * Ho * Wo
     cfg = pick_igemm_cfg(M, cout) if cfg is None else cfg
-    bm, bn = IGEMM_CFGS[cfg]
+    bm, bn = IGEMM_CFGS[cfg % 100]
     y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     mt = -(-M // bm)
     st = torch.empty(mt, 2, cout, device=x.device, dtype=torch.float32) if stats else None
@@ -183,7 +216,7 @@ def conv2d_transpose_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, ou
     py, px = same_pads(Ho)[0], same_pads(Wo)[0]
     Mphase = B * (-(-Ho // 2)) * (-(-Wo // 2))
     cfg = pick_igemm_cfg(Mphase, cout, phases=4) if cfg is None else cfg
-    bm, bn = IGEMM_CFGS[cfg]
+    bm, bn = IGEMM_CFGS[cfg % 100]
     y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     prog = ext().Program()
     st = None

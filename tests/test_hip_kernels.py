@@ -58,8 +58,8 @@ def test_conv2d_same_act_stats_bf16_all_tiles():
     wp = h.pack_conv_weight(w, "conv", "fwd")
     wref = wp.float().reshape(25, Co, Ci).transpose(1, 2).reshape(5, 5, Ci, Co)
     ref_pre = R.conv2d_same(x.float(), wref)
-    for cfg in h.IGEMM_CFGS:
-        if h.IGEMM_CFGS[cfg][1] == 16:
+    for cfg in list(h.IGEMM_CFGS) + [c + 100 for c in h.IGEMM_CFGS]:  # both staging variants
+        if h.IGEMM_CFGS[cfg % 100][1] == 16:
             continue
         y, st = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg)
         close(y, R.lrelu(ref_pre), 1.5e-2, "conv lrelu cfg%d" % cfg)
