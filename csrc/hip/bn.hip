@@ -113,9 +113,21 @@ __device__ __forceinline__ void reduce_rows2(const float* __restrict__ part, int
                                              bool cok, int off1, T& s1, T& s2) {
   __shared__ T red[2][16][17];
   const int ch = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  // 8 independent loads per operand in flight per thread: the partial arrays are small and
+  // freshly written by other CUs, so this loop is latency-bound, not bandwidth-bound
   T a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
   if (cok) {
     int p = p0 + lane;
+    for (; p + 112 < p1; p += 128) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        va[u] = part[(size_t)(p + 16 * u) * stride + c];
+        vb[u] = off1 >= 0 ? part[(size_t)(p + 16 * u) * stride + off1 + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a[u & 3] += (T)va[u]; b[u & 3] += (T)vb[u]; }
+    }
     for (; p + 48 < p1; p += 64) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {

@@ -67,7 +67,18 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
   float acc[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) acc[r] = 0.f;
-  for (int k = 0; k < K; ++k) {
+  // 8 independent W loads in flight per thread (the loop is latency-, not FLOP-bound)
+  int k = 0;
+  for (; k + 8 <= K; k += 8) {
+    float w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = W[(size_t)(k + u) * N + n];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k + u] * w[u];
+  }
+  for (; k < K; ++k) {
     const float w = W[(size_t)k * N + n];
 #pragma unroll
     for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k] * w;
@@ -332,7 +343,7 @@ extern "C" int dcg_gan_loss(const float* logits, int B, float* out, float* dl_d,
 
 extern "C" int dcg_linear_fwd(const float* z, const float* W, const float* b, bf16* out, int B, int K, int N,
                               hipStream_t s) {
-  constexpr int RB = 16;
+  constexpr int RB = 8;  // (N/256) x (B/8) = 512 blocks for the 64x64 model at B=128
   dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
   hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N);
   return (int)hipGetLastError();

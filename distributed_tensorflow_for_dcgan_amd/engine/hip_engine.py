@@ -51,7 +51,7 @@ class HipEngine:
     def __init__(self, cfg: DCGANConfig, batch_size: int, device: torch.device, dtype: str = "bf16",
                  seed: int = 0, lr: float = 2e-4, beta1: float = 0.5, zero_debias: bool = False, rank: int = 0,
                  world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 8.0,
-                 **_):
+                 rank_seeded_z: bool = True, **_):
         if dtype != "bf16":
             raise ValueError("the HIP engine computes in bf16 (fp32 master weights / statistics)")
         if device.type != "cuda":
@@ -62,6 +62,7 @@ class HipEngine:
         self.device = device
         self.rank, self.world = rank, world
         self.seed = int(seed)
+        self.rank_seeded_z = bool(rank_seeded_z)  # False only in equivalence tests
         self.lr, self.beta1 = float(lr), float(beta1)
         self.model = DCGAN(cfg, device=device, seed=seed, zero_debias=zero_debias)
         if world > 1:
@@ -181,10 +182,11 @@ class HipEngine:
         self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
         self._build_d_backward_dloss(self.progA)
         self._build_gloss_and_g_backward(self.progB)
-        self._build_update(self.progC)
+        self._build_update(self.progC, "d")
+        self._c_split = self.progC.size()
+        self._build_update(self.progC, "g")
         self.progPack = ext.Program()
         self._build_pack(self.progPack)
-        self._build_pack(self.progC)
         self.progS = None  # sampler program, built lazily
         self.progEval = None
 
@@ -235,7 +237,7 @@ class HipEngine:
         B2 = 2 * B
         Pg, Pd = self.model.g, self.model.d
         if train_z:
-            prog.philox_uniform("z", _p(z), z.numel(), self.seed * 1000003 + 17 + 7919 * self.rank,
+            prog.philox_uniform("z", _p(z), z.numel(), self.seed * 1000003 + 17 + 7919 * self.rank * int(self.rank_seeded_z),
                                 _p(self.step_counter), 0, -1.0, 1.0, 0)
         # G projection + g_bn0 + relu
         prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
@@ -452,18 +454,24 @@ class HipEngine:
                           _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
 
     # ---- optimiser + repack
-    def _build_update(self, prog):
+    def _build_update(self, prog, which="dg"):
+        """TF-Adam for D and/or G. The D half (adam_d + D repack) comes first so that under
+        DDP it overlaps with the G-gradient all-reduce still in flight."""
         gs = 1.0 / self.world
         od, og = self.opt_d, self.opt_g
-        prog.adam("adam_d", _p(self.model.d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers),
-                  self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0)
-        prog.adam("adam_g", _p(self.model.g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat), _p(og.powers),
-                  self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0)
-        prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
-                      _p(self.step_counter), 0)
+        if "d" in which:
+            prog.adam("adam_d", _p(self.model.d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
+                      _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0)
+            self._build_pack(prog, "d")
+        if "g" in which:
+            prog.adam("adam_g", _p(self.model.g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
+                      _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0)
+            prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
+                          _p(self.step_counter), 0)
+            self._build_pack(prog, "g")
 
-    def _build_pack(self, prog):
-        for L in self.dl:
+    def _build_pack(self, prog, which="dg"):
+        for L in (self.dl if "d" in which else []):
             w = self.model.d[L.name + "/w"]
             nat, tr = self.wp[L.name]
             ci, co = L.cin, L.cout
@@ -471,7 +479,7 @@ class HipEngine:
                 prog.pack(L.name + ".pack", _p(w), 25, ci, co, _p(nat), _p(tr), co * ci, ci, 1, 0)
             else:  # tr[co][tap*ci + a]
                 prog.pack(L.name + ".pack", _p(w), 25, ci, co, _p(nat), _p(tr), ci, self.kp_d0, 1, 0)
-        for L in self.gl:
+        for L in (self.gl if "g" in which else []):
             w = self.model.g[L.name + "/w"]
             nat, tr = self.wp[L.name]
             co, ci = L.cout, L.cin  # w [25][co][ci]
@@ -488,17 +496,35 @@ class HipEngine:
     def _streams(self):
         return [torch.cuda.current_stream(self.device)]
 
-    def _run_eager(self):
+    def _segments(self):
+        """The step as (program, begin, end) segments. Single process: one segment. DDP: the
+        collectives sit between segments -- D-grad all-reduce overlaps G backward (B), the
+        G-grad all-reduce overlaps D's Adam + repack (C[:split])."""
+        if self.world == 1:
+            return [[(self.progA, 0, -1), (self.progB, 0, -1), (self.progC, 0, -1)]]
+        return [[(self.progA, 0, -1)], [(self.progB, 0, -1)], [(self.progC, 0, self._c_split)],
+                [(self.progC, self._c_split, -1)]]
+
+    def _run_segment(self, i, st):
+        if self.graph_enabled:
+            self._graphs[i].replay()
+        else:
+            for prog, b, e in self._segments()[i]:
+                H.run(prog, st, b, e)
+
+    def _run_step(self):
         st = self._streams()
-        H.run(self.progA, st)
-        if self.world > 1:
-            self._ar_d.launch()
-        H.run(self.progB, st)
-        if self.world > 1:
-            self._ar_g.launch()
-            self._ar_d.wait(scale_in_place=False)
-            self._ar_g.wait(scale_in_place=False)
-        H.run(self.progC, st)
+        if self.world == 1:
+            self._run_segment(0, st)
+            return
+        self._run_segment(0, st)          # fwd + D backward -> grad_d final
+        self._ar_d.launch()
+        self._run_segment(1, st)          # G backward (overlaps the D all-reduce)
+        self._ar_g.launch()
+        self._ar_d.wait(scale_in_place=False)
+        self._run_segment(2, st)          # Adam D + repack D (overlaps the G all-reduce)
+        self._ar_g.wait(scale_in_place=False)
+        self._run_segment(3, st)          # Adam G, step counter, repack G
 
     def _ensure_comm(self):
         if self.world > 1 and not hasattr(self, "_ar_d"):
@@ -506,20 +532,21 @@ class HipEngine:
             self._ar_g = D.GradAllReducer(self.grad_g.flat, self.bucket_mb, self.allreduce_dtype)
 
     def _capture(self):
-        """Capture the whole step (A+B+C) into one hipGraph (single process). Capturing does
-        not execute anything; it is attempted only after one eager step has loaded every code
-        object, and any failure falls back to eager replay of the recorded programs."""
-        if self.world > 1:
-            return False
+        """Capture each step segment into its own hipGraph (collectives stay outside, issued
+        between replays on the comm stream). Capturing does not execute anything; it is
+        attempted only after one eager step has loaded every code object, and any failure
+        falls back to eager replay of the recorded programs."""
         try:
             torch.cuda.synchronize(self.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                cs = torch.cuda.current_stream(self.device)
-                H.run(self.progA, [cs])
-                H.run(self.progB, [cs])
-                H.run(self.progC, [cs])
-            self._graphs = [g]
+            graphs = []
+            for seg in self._segments():
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    cs = torch.cuda.current_stream(self.device)
+                    for prog, b, e in seg:
+                        H.run(prog, [cs], b, e)
+                graphs.append(g)
+            self._graphs = graphs
             return True
         except Exception as e:  # pragma: no cover - depends on runtime
             print("[hip_engine] graph capture failed, running eagerly: %s" % e)
@@ -528,14 +555,11 @@ class HipEngine:
 
     def train_step(self) -> None:
         self._ensure_comm()
-        if (self.graph_requested and not self.graph_enabled and self.world == 1 and self._step_host >= 1
+        if (self.graph_requested and not self.graph_enabled and self._step_host >= 1
                 and not getattr(self, "_cap_tried", 0)):
             self._cap_tried = 1
             self.graph_enabled = self._capture()
-        if self.graph_enabled:
-            self._graphs[0].replay()
-        else:
-            self._run_eager()
+        self._run_step()
         self._step_host += 1
 
     @property

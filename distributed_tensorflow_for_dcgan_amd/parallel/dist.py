@@ -47,6 +47,9 @@ def init_distributed(world: int, rank_: int, device: torch.device, master_addr: 
     os.environ.setdefault("MASTER_ADDR", master_addr or "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(master_port or 29500))
     backend = "nccl" if device.type == "cuda" else "gloo"
+    # gloo over GPU tensors lets several ranks share ONE GPU (RCCL refuses that): used by the
+    # 1-GPU DDP-equivalence test of the HIP engine. Production multi-GPU runs use RCCL.
+    backend = os.environ.get("DCGAN_DIST_BACKEND", backend)
     kwargs = dict(backend=backend, world_size=world, rank=rank_,
                   timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":

@@ -1,0 +1,79 @@
+"""DDP path of the HIP engine on ONE GPU: two ranks share the card over the gloo backend
+(RCCL refuses two ranks per GPU; the collective calls, streams, segmented hipGraphs and the
+1/W gradient scale folded into Adam are the same code the RCCL run uses).
+
+With identical data and rank-independent z on both ranks, the averaged gradient equals the
+local one exactly (x + x = 2x, times 1/2 is exact in fp32), so W=2 must reproduce the
+single-process engine BIT FOR BIT after several steps -- with graphs and without."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B = 16
+STEPS = 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _make(world, rank, graph):
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+    cfg = DCGANConfig(output_size=64, c_dim=3)
+    dev = torch.device("cuda", 0)
+    eng = HipEngine(cfg, B, dev, seed=3, rank=rank, world=world, graph=graph, rank_seeded_z=False)
+    real = torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1
+    eng.set_batch(real.to(dev))
+    return eng
+
+
+def _run(eng):
+    for _ in range(STEPS):
+        eng.train_step()
+    torch.cuda.synchronize()
+    return eng.model.d.flat.cpu(), eng.model.g.flat.cpu(), eng.global_step
+
+
+def _worker(rank, world, port, graph, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DCGAN_DIST_BACKEND"] = "gloo"
+    torch.cuda.set_device(0)
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    D.init_distributed(world, rank, torch.device("cuda", 0))
+    eng = _make(world, rank, graph)
+    d, g, step = _run(eng)
+    torch.save({"d": d, "g": g, "step": step, "graph": eng.graph_enabled}, os.path.join(out_dir, "r%d.pt" % rank))
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0, "rank exited with %s" % p.exitcode
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert r0["graph"] == graph
+    assert torch.equal(r0["d"], r1["d"]) and torch.equal(r0["g"], r1["g"])
+    assert r0["step"] == STEPS
+    eng = _make(1, 0, graph)
+    d, g, _ = _run(eng)
+    assert torch.equal(r0["d"], d), (r0["d"] - d).abs().max()
+    assert torch.equal(r0["g"], g), (r0["g"] - g).abs().max()
