@@ -2,10 +2,11 @@
 """Per-layer kernel benchmark / autotuner for the implicit-GEMM conv kernel (MI355X).
 
 For every conv-shaped GEMM of the DCGAN training step (D forward on 2B, D dgrads, G forward,
-G dgrads, at per-GPU batch B) time every tile configuration and both staging variants
-(register staging vs LDS-DMA) in ONE process, interleaved (guide §5.4 rule 24), and report
-TF/s. ``--write`` stores the fastest config per shape in ops/igemm_tuned.json, which the
-engine's tile policy consults first.
+G dgrads, at per-GPU batch B) time every tile configuration -- igemm.hip (both staging
+variants) and igemm3.hip (every tile, 2/3 LDS stages, split-K 1..8) with the weight layout
+the engine reads for that GEMM -- in ONE process, interleaved (guide §5.4 rule 24), and
+report TF/s. ``--write`` stores the fastest "cfg:splits" per shape in ops/igemm_tuned.json,
+which the engine's tile policy consults first.
 
     python benchmarks/bench_kernels.py --batch 128 [--write] [--reps 20]
 """
@@ -23,25 +24,59 @@ from distributed_tensorflow_for_dcgan_amd.ops import hip as H  # noqa: E402
 
 
 def shapes(cfg: DCGANConfig, B: int):
-    """(name, mode, Bn, Hin, Win, Kc, Hout, Wout, N, pad, flops)"""
+    """(name, mode, Bn, Hin, Win, Kc, Hout, Wout, N, pad, bkn, kb_valid). bkn = weight layout the
+    engine reads: the TF layout itself, which is [tap][K][N] for D forward / G dgrad and
+    [tap][N][K] for D dgrad / G forward."""
     out = []
     for i, L in enumerate(cfg.d_layers()):
         pad = same_pads(L.in_hw)[0]
         if L.cin % 8 == 0:
-            out.append(("D%d.fwd" % i, 0, 2 * B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad))
+            out.append(("D%d.fwd" % i, 0, 2 * B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad, 1, -1))
         else:
-            out.append(("D%d.fwd(im2col)" % i, 2, 2 * B, 1, 1, -(-25 * L.cin // 16) * 16, L.out_hw, L.out_hw, L.cout, 0))
+            out.append(("D%d.fwd(im2col)" % i, 2, 2 * B, 1, 1, -(-25 * L.cin // 16) * 16, L.out_hw, L.out_hw, L.cout,
+                        0, 1, 25 * L.cin))
         if i > 0:
-            out.append(("D%d.dgrad2B" % i, 1, 2 * B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad))
-        out.append(("D%d.dgradB" % i, 1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad))
+            out.append(("D%d.dgrad2B" % i, 1, 2 * B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, 0, -1))
+        out.append(("D%d.dgradB" % i, 1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, 0, -1))
     for L in cfg.g_layers():
         pad = same_pads(L.out_hw)[0]
-        out.append(("G.%s.fwd" % L.name, 1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad))
+        out.append(("G.%s.fwd" % L.name, 1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad, 0, -1))
         if L.cout % 8 == 0:
-            out.append(("G.%s.dgrad" % L.name, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad))
+            out.append(("G.%s.dgrad" % L.name, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, 1, -1))
         else:
             out.append(("G.%s.dgrad(im2col)" % L.name, 2, B, 1, 1, -(-25 * L.cout // 16) * 16, L.in_hw, L.in_hw,
-                        L.cin, 0))
+                        L.cin, 0, 1, 25 * L.cout))
+    return out
+
+
+def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
+    """[(cfg, splits)] worth timing for one GEMM."""
+    out = []
+    if not bkn:  # igemm.hip reads k-contiguous weights only
+        for c, (bm, bn) in H.IGEMM_CFGS.items():
+            if (N <= 16) != (bn == 16):
+                continue
+            if bn > 32 and N < bn:
+                continue
+            out += [(c, 1), (c + 100, 1)]
+    if N % 8 or N <= 16:
+        return out
+    phases = 4 if mode == 1 else 1
+    M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
+    kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
+    for c in range(200, 216):
+        if c % 10 not in H.IGEMM3_TILES:
+            continue
+        bm, bn = H.IGEMM3_TILES[c % 10]
+        if bn > N:
+            continue
+        tiles = -(-M // bm) * -(-N // bn) * phases
+        for sp in (1, 2, 3, 4, 6, 8):
+            if sp > 1 and (kt // sp < 2 or tiles * sp > 4096):
+                continue
+            if sp > 1 and tiles >= 1024:
+                continue
+            out.append((c, sp))
     return out
 
 
@@ -65,32 +100,26 @@ def main():
     ext = H.ext()
     dev = torch.device("cuda", 0)
     table = {}
-    for (name, mode, Bn, Hin, Win, Kc, Hout, Wout, N, pad) in shapes(cfg, a.batch):
+    for (name, mode, Bn, Hin, Win, Kc, Hout, Wout, N, pad, bkn, kb) in shapes(cfg, a.batch):
         if a.only and a.only not in name:
             continue
         if mode == 2:
             A = torch.randn(Bn * Hout * Wout, Kc, device=dev).to(torch.bfloat16)
-            Bw = torch.randn(N, Kc, device=dev).to(torch.bfloat16)
+            Bw = torch.randn(max(N, 8) * Kc, device=dev).to(torch.bfloat16)
         else:
             A = torch.randn(Bn, Hin, Win, Kc, device=dev).to(torch.bfloat16)
             Bw = (0.05 * torch.randn(25, N, Kc, device=dev)).to(torch.bfloat16)
         C = torch.empty(Bn * Hout * Wout * N, device=dev, dtype=torch.bfloat16)
         stats = torch.empty(1 << 22, device=dev)
         fl = flops(mode, Bn, Hin, Win, Kc, Hout, Wout, N)
-        cands = []
-        for c, (bm, bn) in H.IGEMM_CFGS.items():
-            if (N <= 16) != (bn == 16):
-                continue
-            if bn > 32 and N < bn:
-                continue
-            for st in (0, 100):
-                cands.append(c + st)
+        cands = candidates(mode, Bn, Hout, Wout, Kc, N, bkn)
         progs = {}
-        for c in cands:
+        for (c, sp) in cands:
             p = ext.Program()
-            p.igemm(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad,
-                    c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0)
-            progs[c] = p
+            p.igemm_ex(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad,
+                       pad, c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn if c >= 200 else 0,
+                       kb if c >= 200 else -1, sp)
+            progs[(c, sp)] = p
         times = {c: [] for c in cands}
         s = torch.cuda.current_stream()
         for c in cands:  # warm
@@ -111,11 +140,12 @@ def main():
             res.append((med, c))
         res.sort()
         best = res[0]
-        print("%-22s M/ph=%7d N=%4d K=%5d  best cfg %3d %-10s %7.1f us %6.0f TF/s | " %
-              (name, Bn * Hout * Wout // (4 if mode == 1 else 1), N, Kc * (25 if mode == 0 else 1), best[1],
-               H.IGEMM_CFGS[best[1] % 100], best[0], fl / best[0] / 1e6) +
-              " ".join("%d:%.0f" % (c, t) for t, c in res[:6]), flush=True)
-        table["%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N)] = best[1]
+        bc, bsp = best[1]
+        print("%-22s M/ph=%7d N=%4d K=%5d  best %3d:%d %-10s %7.1f us %6.0f TF/s | " %
+              (name, Bn * Hout * Wout // (4 if mode == 1 else 1), N, Kc * (25 if mode == 0 else 1), bc, bsp,
+               H.tile_of(bc), best[0], fl / best[0] / 1e6) +
+              " ".join("%d:%d:%.0f" % (c[0], c[1], t) for t, c in res[:6]), flush=True)
+        table["%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N)] = "%d:%d" % (bc, bsp)
     if a.write:
         path = os.path.join(os.path.dirname(H.__file__), "igemm_tuned.json")
         old = {}

@@ -92,8 +92,25 @@ class Program {
   int igemm(std::string name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win, int Kc,
             int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
             uintptr_t bias, int act, float leak, uintptr_t stats, int stream) {
-    int bm = 0, bn = 0;
-    if (dcg_igemm_tile(cfg, &bm, &bn)) throw std::runtime_error("bad igemm cfg");
+    return igemm_ex(name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad_y, pad_x, cfg, out_f32, ldc, cofs, bias,
+                    act, leak, stats, stream, 0, -1, 1);
+  }
+
+  // cfg < 200: igemm.hip tiles (Bw k-contiguous only, no split-K); cfg 200..219: igemm3.hip
+  // (bkn = 1 reads Bw as [tap][Kc][N]; kb_valid = number of real B k-rows; splits = split-K).
+  int igemm_ex(std::string name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win, int Kc,
+               int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
+               uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits) {
+    int bm = 0, bn = 0, ns = 0;
+    const bool v3 = cfg >= 200;
+    if (v3 ? dcg_igemm3_tile(cfg, &bm, &bn, &ns) : dcg_igemm_tile(cfg, &bm, &bn))
+      throw std::runtime_error("bad igemm cfg " + std::to_string(cfg));
+    if (!v3 && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
+    if (splits < 1) throw std::runtime_error("splits must be >= 1");
+    if (Kc % 8) throw std::runtime_error("igemm needs Kc % 8 == 0 (16-byte A rows)");
+    if (bkn && N % 8) throw std::runtime_error("igemm bkn needs N % 8 == 0");
+    if (kb_valid < 0) kb_valid = Kc;
+    if (kb_valid > Kc) throw std::runtime_error("kb_valid > Kc");
     std::vector<IGemmPhase> ph;
     IGemmArgs a{};
     a.A = P<const bf16>(A); a.Bn = Bn; a.H = Hin; a.W = Win; a.Kc = Kc;
@@ -138,7 +155,7 @@ class Program {
       p.Hq = 1; p.Wq = 1; p.M = Bn * Hout * Wout; p.ntaps = 1;
       p.fd_hw = fastdiv_make(1); p.fd_w = fastdiv_make(1);
       ph.push_back(p);
-      a_elems = (size_t)p.M * Kc; b_elems = (size_t)N * Kc;
+      a_elems = (size_t)p.M * Kc; b_elems = bkn ? (size_t)kb_valid * N : (size_t)N * Kc;
     } else {
       throw std::runtime_error("bad igemm mode");
     }
@@ -157,9 +174,26 @@ class Program {
     a.ph = reinterpret_cast<const IGemmPhase*>(dph);
     last_mtiles_ = mtiles;
     last_nphases_ = a.nphases;
-    return add(name, stream, [a, cfg, mtiles, ntiles](hipStream_t s) {
-      return dcg_igemm_launch(&a, cfg, mtiles, ntiles, s);
-    });
+    a.kb_valid = kb_valid;
+    a.splits = splits;
+    if (!v3)
+      return add(name, stream, [a, cfg, mtiles, ntiles](hipStream_t s) {
+        return dcg_igemm_launch(&a, cfg, mtiles, ntiles, s);
+      });
+    const size_t tiles = (size_t)mtiles * ntiles * a.nphases;
+    if (splits > 1) {  // per-op workspace + zeroed arrival counters (reset by the kernel itself)
+      void* ws = nullptr;
+      void* ctr = nullptr;
+      HIPCHECK(hipMalloc(&ws, tiles * splits * (size_t)bm * bn * sizeof(float)));
+      HIPCHECK(hipMalloc(&ctr, tiles * sizeof(unsigned)));
+      HIPCHECK(hipMemset(ctr, 0, tiles * sizeof(unsigned)));
+      dev_allocs_.push_back(ws);
+      dev_allocs_.push_back(ctr);
+      a.ws = reinterpret_cast<float*>(ws);
+      a.counters = reinterpret_cast<unsigned*>(ctr);
+    }
+    const unsigned blocks = (unsigned)(tiles * splits);
+    return add(name, stream, [a, cfg, bkn, blocks](hipStream_t s) { return dcg_igemm3_launch(&a, cfg, bkn, blocks, s); });
   }
   int last_mtiles() const { return last_mtiles_; }
   int last_nphases() const { return last_nphases_; }
@@ -305,9 +339,14 @@ class Program {
   }
   int adam(std::string name, uintptr_t w, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers, size_t n, float lr,
            float b1, float b2, float eps, float gscale, int stream) {
+    return adam_bf(name, w, 0, g, m, v, powers, n, lr, b1, b2, eps, gscale, stream);
+  }
+  // + bf16 mirror of the updated weights (same flat layout)
+  int adam_bf(std::string name, uintptr_t w, uintptr_t wbf, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers,
+              size_t n, float lr, float b1, float b2, float eps, float gscale, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_adam(P<float>(w), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers), n, lr, b1,
-                      b2, eps, gscale, s);
+      return dcg_adam(P<float>(w), P<bf16>(wbf), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers),
+                      n, lr, b1, b2, eps, gscale, s);
     });
   }
   int step_end(std::string name, uintptr_t pd, uintptr_t pg, float b1d, float b2d, float b1g, float b2g,
@@ -361,6 +400,11 @@ class Program {
 };
 
 static py::tuple igemm_tile(int cfg) {
+  if (cfg >= 200) {
+    int bm, bn, ns;
+    if (dcg_igemm3_tile(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad cfg");
+    return py::make_tuple(bm, bn);
+  }
   int bm = 0, bn = 0;
   if (dcg_igemm_tile(cfg, &bm, &bn)) throw std::runtime_error("bad cfg");
   return py::make_tuple(bm, bn);
@@ -396,6 +440,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("memset", &Program::memset)
       .def("copy", &Program::copy)
       .def("igemm", &Program::igemm)
+      .def("igemm_ex", &Program::igemm_ex)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)
@@ -415,6 +460,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("head_dgrad", &Program::head_dgrad)
       .def("head_wgrad", &Program::head_wgrad)
       .def("adam", &Program::adam)
+      .def("adam_bf", &Program::adam_bf)
       .def("step_end", &Program::step_end)
       .def("pack", &Program::pack)
       .def("philox_uniform", &Program::philox_uniform)

@@ -1,0 +1,446 @@
+// Implicit-GEMM convolution, version 3: big wave tiles + deep LDS-DMA pipeline + in-kernel
+// deterministic split-K + either weight layout. Same conv/deconv/plain semantics and fused
+// epilogue as igemm.hip (read that header first); what changes is how the K loop is fed.
+//
+// Why: a 16x16x32 bf16 MFMA takes 16 cycles/SIMD and a ds_read_b128 costs 4 LDS cycles/CU
+// (256 B/clk). With 4 waves of TMxTN wave tiles, LDS time / MFMA time = 16 (TM + TN) / (TM TN):
+// 1.0 for 32x32 wave tiles (igemm.hip's 64x64 blocks -> LDS-bound), 0.5 for 64x64. So the
+// main tiles here are 128x128 (2x2 waves), 256x64 (4x1) and 64x256 (1x4), all 64x64 per wave.
+// Those tiles give too few workgroups for the small-M layers (4x4 / 8x8 outputs), so K is
+// split over workgroups: every split writes its fp32 accumulators to a workspace slab with
+// `sc1` stores, one lane bumps a per-tile counter (agent atomic), and the workgroup whose add
+// comes last sums the slabs IN SPLIT ORDER (deterministic; `sc1` loads bypass the stale L1),
+// resets the counter for the next launch / graph replay and runs the fused epilogue.
+//
+// Pipeline: NS LDS stages, LDS-DMA (buffer_load_dwordx4 ... lds) for both operands, tile
+// kt + NS - 1 issued right after the single per-tile barrier, `s_waitcnt vmcnt(LPT * (NS-2))`
+// keeps the younger tiles in flight while tile kt is consumed.
+//
+// Weight layouts (BKN template flag):
+//   BKN = 0: Bw[tap][N][Kc] (k contiguous) -> fragments via ds_read_b128, like igemm.hip;
+//   BKN = 1: Bw[tap][Kc][N] (n contiguous) -> the LDS tile is k-major and fragments are read
+//            with the gfx950 transposing read ds_read_b64_tr_b16 (as in wgrad.hip).
+// With both layouts available, every GEMM of the step reads the ONE bf16 mirror of the TF
+// weight layout (HWIO conv / [kh,kw,out,in] deconv) that Adam writes: no repack kernels.
+//
+// Workgroup -> tile mapping is XCD-aware: workgroups are dispatched round-robin over the 8
+// XCDs, so workgroup b works on tile (b % 8) * (T / 8) + b / 8, which gives every XCD a
+// contiguous run of tiles (neighbouring output pixels share input rows in that XCD's L2).
+#include "kernels.h"
+
+namespace dcg {
+
+template <int S>
+__device__ __forceinline__ int kn_swz(int r) {  // 8-byte-chunk XOR of k-major row r (stride S bytes)
+  if constexpr (S >= 256) return 4 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else if constexpr (S == 128) return 4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+  else return 4 * ((r >> 3) & 1);
+}
+
+// 16-byte stores / loads with the `sc1` cache policy (aux bit 16 on gfx94x/gfx950): stores
+// write through and drop the line from this XCD's L2, loads bypass L1 -- the cross-workgroup
+// hand-off of the split-K slabs. Builtins (not inline asm) so the compiler keeps tracking the
+// waitcnts and the store-data hazards.
+constexpr int CPOL_SC1 = 16;
+
+__device__ __forceinline__ void store16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, CPOL_SC1);
+}
+
+__device__ __forceinline__ f32x4 load16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CPOL_SC1));
+}
+
+template <int N_>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int BKN, int NS>
+__global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NPA = A_BYTES / 1024, NPB = B_BYTES / 1024;  // 1 KiB DMA pieces per stage
+  constexpr int PPW_A = NPA / 4, PPW_B = NPB / 4;             // per wave
+  constexpr int LPT = PPW_A + PPW_B;                          // DMA instructions per wave per tile
+  constexpr int SB = BN * 2;                                  // k-major B row stride (bytes)
+  constexpr int B_ROWS_PER_PIECE = BKN ? 1024 / SB : 8;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(NPA % 4 == 0 && NPB % 4 == 0, "every wave issues the same DMA count");
+  static_assert(FM >= 1 && FN >= 1, "tile");
+  static_assert(!BKN || (SB <= 1024 && 1024 % SB == 0), "k-major B rows");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // ---- tile decode (XCD-aware): t -> (phase, mt, nt, split), split fastest
+  const int S = p.splits;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int total = p.mtiles * ntn * p.nphases * S;
+  int t = blockIdx.x;
+  if ((total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);
+  const int split = t % S;
+  int r_ = t / S;
+  const int nt = r_ % ntn;
+  r_ /= ntn;
+  const int mt = r_ % p.mtiles;
+  const int phase = r_ / p.mtiles;
+  const int tile_id = (phase * p.mtiles + mt) * ntn + nt;
+
+  const IGemmPhase* ph = p.ph + phase;
+  const int M = ph->M;
+  const int m0 = mt * BM, n0 = nt * BN;
+  if (m0 >= M) {  // phase with fewer rows (odd output sizes): its stats slot must still be defined
+    if (p.stats && split == 0) {
+      float* dst = p.stats + (size_t)(mt * p.nphases + phase) * 2 * p.N;
+      for (int nl = tid; nl < BN; nl += 256)
+        if (n0 + nl < p.N) { dst[n0 + nl] = 0.f; dst[p.N + n0 + nl] = 0.f; }
+    }
+    return;
+  }
+  const int Kc = p.Kc, N = p.N;
+  const int ntaps = p.plain ? 1 : ph->ntaps;
+  const int kt_per_tap = (Kc + BK - 1) / BK;
+  const int KT = ntaps * kt_per_tap;
+  const int kps = (KT + S - 1) / S;  // per phase: deconv phases have 9 / 6 / 6 / 4 taps
+  const int kt0 = split * kps;
+  const int kt1 = min(KT, kt0 + kps);
+  const int nk = max(0, kt1 - kt0);
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, p.b_bytes);
+
+  // ---- A rows of this lane: piece q = wave + 4 i, row = 8 q + lane / 8, slot = lane & 7,
+  //      global 16-byte chunk = slot ^ (row & 7)
+  const int a_chunk = (lane & 7) ^ (lane >> 3);
+  int a_base[PPW_A], a_iy[PPW_A], a_ix[PPW_A];
+  bool a_ok[PPW_A];
+#pragma unroll
+  for (int i = 0; i < PPW_A; ++i) {
+    const int r = 8 * (wave + 4 * i) + (lane >> 3);
+    const int m = m0 + r;
+    a_ok[i] = m < M;
+    if (p.plain) {
+      a_base[i] = m * Kc; a_iy[i] = 0; a_ix[i] = 0;
+    } else {
+      const uint32_t b = fdiv((uint32_t)m, ph->fd_hw);
+      const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph->Hq * ph->Wq);
+      const uint32_t qy = fdiv(rem, ph->fd_w);
+      const uint32_t qx = rem - qy * (uint32_t)ph->Wq;
+      a_iy[i] = (int)qy * p.sstride + ph->iy0_off;
+      a_ix[i] = (int)qx * p.sstride + ph->ix0_off;
+      a_base[i] = (((int)b * p.H + a_iy[i]) * p.W + a_ix[i]) * Kc;
+    }
+  }
+  // ---- B: BKN=0 rows n (8 per piece, chunk like A); BKN=1 rows k (1024/SB per piece, the
+  //      16-byte slot of lane L holds global chunk slot ^ (swizzle(row) / 2))
+
+  // issue cursor: (tap index, channel offset) of the next tile to load
+  int cur_ti = kt0 / kt_per_tap;
+  int cur_c0 = (kt0 - cur_ti * kt_per_tap) * BK;
+
+  auto issue = [&](int slot) {
+    char* sa = lds + slot * STAGE;
+    char* sb = sa + A_BYTES;
+    int dy = 0, dx = 0, wt = 0;
+    if (!p.plain) { dy = ph->dy[cur_ti]; dx = ph->dx[cur_ti]; wt = ph->wtap[cur_ti]; }
+    const int cc = cur_c0 + a_chunk * 8;
+    const bool kval = cc < Kc;
+    const int tap_delta = (dy * p.W + dx) * Kc;
+#pragma unroll
+    for (int i = 0; i < PPW_A; ++i) {
+      uint32_t off = OOB;
+      if (p.plain) {
+        if (a_ok[i] && kval) off = (uint32_t)(a_base[i] + cc) * 2u;
+      } else {
+        const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
+        if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+          off = (uint32_t)(a_base[i] + tap_delta + cc) * 2u;
+      }
+      buf_load16_lds(ra, sa + (wave + 4 * i) * 1024, off);
+    }
+#pragma unroll
+    for (int i = 0; i < PPW_B; ++i) {
+      const int q = wave + 4 * i;
+      uint32_t off = OOB;
+      if constexpr (BKN) {
+        const int rr = q * B_ROWS_PER_PIECE + lane / (SB / 16);
+        const int k = cur_c0 + rr;
+        const int n = n0 + ((lane % (SB / 16)) ^ (kn_swz<SB>(rr) >> 1)) * 8;
+        if (k < p.kb_valid && n < N) off = (uint32_t)((wt * Kc + k) * N + n) * 2u;
+      } else {
+        const int n = n0 + 8 * q + (lane >> 3);
+        const int c = cur_c0 + a_chunk * 8;
+        if (n < N && c < Kc && c < p.kb_valid) off = (uint32_t)((wt * N + n) * Kc + c) * 2u;
+      }
+      buf_load16_lds(rb, sb + q * 1024, off);
+    }
+    cur_c0 += BK;
+    if (cur_c0 >= Kc) { cur_c0 = 0; ++cur_ti; }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s);
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed for this wave; younger tiles (up to NS-2 of them) may stay in flight
+    if constexpr (NS >= 3) {
+      if (kt + 1 < nk) wait_vmcnt<LPT * (NS - 2)>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    // every wave's tile kt landed; every wave is done with slot (kt-1) % NS. A bare s_barrier:
+    // __syncthreads() would add the workgroup release, i.e. a vmcnt(0) that also waits for the
+    // younger DMA tiles and flattens the pipeline (LDS reads of the previous tile have all
+    // returned: their values fed the MFMAs already).
+    asm volatile("s_barrier" ::: "memory");
+    if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS);
+    const char* sa = lds + (kt % NS) * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+      const int c = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+      if constexpr (BKN) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = ks * 32 + 8 * g4 + 4 * h + q4;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int c8 = (wn * TN + j * 16) / 4 + p4;
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                LDS_PTR(s16x4, sb + r * SB + ((c8 ^ kn_swz<SB>(r)) * 8)));
+            const bf16x4 vb = __builtin_bit_cast(bf16x4, v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = vb[e];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * TN + j * 16 + fr;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ------------------------------------------------------------------ split-K hand-off
+  if (S > 1) {
+    // flag word in the (now idle) dynamic LDS: a static __shared__ would shift the 16-byte
+    // alignment of the dynamic base the ds_read_b128 / tr reads rely on
+    int& last_flag = *reinterpret_cast<int*>(lds);
+    // this tile's S slabs [S][BM*BN] fp32; lane layout = accumulator-register order, so each
+    // (i, j) fragment is one fully coalesced 4 KiB block per workgroup
+    const __amdgpu_buffer_rsrc_t rw =
+        make_rsrc(p.ws + (size_t)tile_id * S * (BM * BN), (uint32_t)(S * BM * BN * 4));
+    const uint32_t own_base = (uint32_t)split * (BM * BN * 4);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) store16_sc1(rw, own_base + (uint32_t)(((i * FN + j) * 256 + tid) * 16), acc[i][j]);
+    wait_vmcnt<0>();
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(p.counters + tile_id, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = (old == (unsigned)(S - 1));
+      if (last_flag) __hip_atomic_store(p.counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    // deterministic: sum slabs in split order, independent of which split arrived last
+    f32x4 tot[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) tot[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      if (s == split) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) tot[i][j] += acc[i][j];
+      } else {
+        const uint32_t base = (uint32_t)s * (BM * BN * 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            tot[i][j] += load16_sc1(rw, base + (uint32_t)(((i * FN + j) * 256 + tid) * 16));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = tot[i][j];
+  }
+
+  // ------------------------------------------------------------------ epilogue (as igemm.hip)
+  __syncthreads();
+  int* rowoff = reinterpret_cast<int*>(lds);
+  float* red = reinterpret_cast<float*>(lds) + BM;
+  constexpr int CPAD = BN + 8;
+  bf16* ctile = reinterpret_cast<bf16*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
+  static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= NS * STAGE, "epilogue LDS");
+  for (int r = tid; r < BM; r += 256) {
+    const int m = m0 + r;
+    int off = -1;
+    if (m < M) {
+      if (p.plain) {
+        off = m * p.ldc;
+      } else {
+        const uint32_t b = fdiv((uint32_t)m, ph->fd_hw);
+        const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph->Hq * ph->Wq);
+        const uint32_t qy = fdiv(rem, ph->fd_w);
+        const uint32_t qx = rem - qy * (uint32_t)ph->Wq;
+        const int y = (int)qy * p.ostride + ph->oy_off, x = (int)qx * p.ostride + ph->ox_off;
+        off = (((int)b * p.outH + y) * p.outW + x) * p.ldc;
+      }
+    }
+    rowoff[r] = off;
+  }
+  __syncthreads();
+
+  const bool do_stats = p.stats != nullptr;
+  const bool vec = !p.out_f32 && (N % 8 == 0) && (p.ldc % 8 == 0) && (p.cofs % 8 == 0);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = wn * TN + j * 16 + fr;
+    const int n = n0 + nl;
+    const bool nok = n < N;
+    const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
+    float s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ml = wm * TM + i * 16 + fq * 4 + r;
+        const int off = rowoff[ml];
+        const float v = acc[i][j][r] + bv;
+        const bf16 vb = f2bf(v);
+        if (off >= 0 && nok) {
+          const float vs = p.out_f32 ? v : (float)vb;
+          s += vs;
+          s2 += vs * vs;
+        }
+        const float o = apply_act(v, p.act, p.leak);
+        if (vec) {
+          ctile[ml * CPAD + nl] = f2bf(o);
+        } else if (off >= 0 && nok) {
+          if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
+          else reinterpret_cast<bf16*>(p.C)[off + p.cofs + n] = f2bf(o);
+        }
+      }
+    }
+    if (do_stats) {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (fq == 0) {
+        red[(wm * BN + nl) * 2 + 0] = s;
+        red[(wm * BN + nl) * 2 + 1] = s2;
+      }
+    }
+  }
+  if (do_stats || vec) __syncthreads();
+  if (vec) {
+    constexpr int CPR = BN / 8;
+    bf16* C = reinterpret_cast<bf16*>(p.C);
+    for (int q = tid; q < BM * CPR; q += 256) {
+      const int r = q / CPR, c = q - r * CPR;
+      const int off = rowoff[r];
+      const int n = n0 + 8 * c;
+      if (off >= 0 && n < N)
+        *reinterpret_cast<u32x4*>(C + off + p.cofs + n) = *reinterpret_cast<const u32x4*>(ctile + r * CPAD + 8 * c);
+    }
+  }
+  if (do_stats) {
+    for (int nl = tid; nl < BN; nl += 256) {
+      const int n = n0 + nl;
+      if (n >= N) continue;
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s += red[(w * BN + nl) * 2 + 0];
+        s2 += red[(w * BN + nl) * 2 + 1];
+      }
+      float* dst = p.stats + (size_t)(mt * p.nphases + phase) * 2 * N;
+      dst[n] = s;
+      dst[N + n] = s2;
+    }
+  }
+}
+
+}  // namespace dcg
+
+// ---------------------------------------------------------------------------- host launch
+// v3 configs: cfg = 200 + 10 * (3 - NS) + id  (NS = 3 -> 200..209, NS = 2 -> 210..219)
+#define DCG_IGEMM3_TILES(X) \
+  X(0, 128, 128, 2, 2) X(1, 256, 64, 4, 1) X(2, 64, 256, 1, 4) X(3, 128, 64, 2, 2) \
+  X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2)
+
+extern "C" int dcg_igemm3_tile(int cfg, int* bm, int* bn, int* ns) {
+  if (cfg < 200 || cfg >= 220) return -1;
+  const int id = cfg % 10;
+  *ns = cfg < 210 ? 3 : 2;
+#define X(id_, BM_, BN_, WM_, WN_) if (id == id_) { *bm = BM_; *bn = BN_; return 0; }
+  DCG_IGEMM3_TILES(X)
+#undef X
+  return -1;
+}
+
+template <int BM, int BN, int WM, int WN, int BKN, int NS>
+static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
+  constexpr size_t shm = (size_t)NS * (BM + BN) * 64 * 2;
+  auto k = dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), shm, s, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dcg_igemm3_launch(const dcg::IGemmArgs* a, int cfg, int bkn, unsigned blocks, hipStream_t s) {
+  int bm, bn, ns;
+  if (dcg_igemm3_tile(cfg, &bm, &bn, &ns)) return -1;
+  const int id = cfg % 10;
+#define X(id_, BM_, BN_, WM_, WN_)                                              \
+  if (id == id_) {                                                              \
+    if (ns == 3) return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 3>(a, blocks, s)   \
+                            : launch3<BM_, BN_, WM_, WN_, 0, 3>(a, blocks, s);  \
+    return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 2>(a, blocks, s)                \
+               : launch3<BM_, BN_, WM_, WN_, 0, 2>(a, blocks, s);               \
+  }
+  DCG_IGEMM3_TILES(X)
+#undef X
+  return -1;
+}

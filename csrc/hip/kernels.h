@@ -24,6 +24,11 @@ struct IGemmArgs {
   int nphases, mtiles;
   uint32_t a_bytes, b_bytes;
   const IGemmPhase* ph;     // device table [nphases]
+  // igemm3 only
+  int kb_valid;             // B rows (k) that exist; larger k reads zeros (im2col'd K padding)
+  int splits;               // split-K over workgroups (k tiles split evenly per phase)
+  float* ws;                // [tiles][splits][BM*BN] fp32 slabs (splits > 1)
+  unsigned* counters;       // [tiles] arrival counters, zero between launches
 };
 
 struct WGradArgs {
@@ -42,6 +47,8 @@ struct WGradArgs {
 extern "C" {
 int dcg_igemm_tile(int cfg, int* bm, int* bn);
 int dcg_igemm_launch(const dcg::IGemmArgs* a, int cfg, int mtiles, int ntiles, hipStream_t s);
+int dcg_igemm3_tile(int cfg, int* bm, int* bn, int* ns);
+int dcg_igemm3_launch(const dcg::IGemmArgs* a, int cfg, int bkn, unsigned blocks, hipStream_t s);
 int dcg_wgrad_tile(int cfg, int* bm, int* bn);
 int dcg_wgrad_launch(const dcg::WGradArgs* a, int cfg, int splits, hipStream_t s);
 int dcg_splitk_reduce(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s);
@@ -72,8 +79,8 @@ int dcg_gemv_head(const bf16* x, const float* w, const float* b, float* out, int
 int dcg_head_dgrad(const float* dl, const float* w, bf16* dx, int R, int K, hipStream_t s);
 int dcg_head_wgrad(const bf16* x, const float* dl, float* part, int R, int K, int splits, hipStream_t s);
 int dcg_sum_vec(const float* v, int n, float* out, hipStream_t s);
-int dcg_adam(float* w, const float* g, float* m, float* v, const float* powers, size_t n, float lr, float b1,
-             float b2, float eps, float gscale, hipStream_t s);
+int dcg_adam(float* w, bf16* wbf, const float* g, float* m, float* v, const float* powers, size_t n, float lr,
+             float b1, float b2, float eps, float gscale, hipStream_t s);
 int dcg_step_end(float* pd, float* pg, float b1d, float b2d, float b1g, float b2g, unsigned long long* step,
                  hipStream_t s);
 int dcg_pack(const float* src, int T, int A, int Bd, bf16* nat, bf16* tr, int st, int sb, int sa, hipStream_t s);

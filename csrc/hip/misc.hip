@@ -190,10 +190,12 @@ __global__ void sum_vec_kernel(const float* __restrict__ v, int n, float* __rest
 
 // ---------------------------------------------------------------- TF Adam
 // lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from device powers (= b^t); w -= lr_t*m/(sqrt(v)+eps)
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const float* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v,
-                                                   const float* __restrict__ powers, size_t n, float lr,
-                                                   float b1, float b2, float eps, float gscale) {
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* __restrict__ wbf,
+                                                   const float* __restrict__ g, float* __restrict__ m,
+                                                   float* __restrict__ v, const float* __restrict__ powers, size_t n,
+                                                   float lr, float b1, float b2, float eps, float gscale) {
+  // wbf (optional): bf16 mirror of the updated weights in the SAME flat layout -- the only
+  // weight copy the conv kernels read (they take either operand layout), so no repack pass
   const float lr_t = lr * sqrtf(1.f - powers[1]) / (1.f - powers[0]);
   const size_t n4 = n / 4;
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
@@ -208,12 +210,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const 
     reinterpret_cast<f32x4*>(m)[i] = mv;
     reinterpret_cast<f32x4*>(v)[i] = vv;
     reinterpret_cast<f32x4*>(w)[i] = wv;
+    if (wbf) {
+      bf16x4 o = {(bf16)wv[0], (bf16)wv[1], (bf16)wv[2], (bf16)wv[3]};
+      reinterpret_cast<bf16x4*>(wbf)[i] = o;
+    }
   }
   for (size_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
     const float gv = g[i] * gscale;
     m[i] = b1 * m[i] + (1.f - b1) * gv;
     v[i] = b2 * v[i] + (1.f - b2) * gv * gv;
     w[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps);
+    if (wbf) wbf[i] = (bf16)w[i];
   }
 }
 
@@ -384,9 +391,9 @@ extern "C" int dcg_sum_vec(const float* v, int n, float* out, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_adam(float* w, const float* g, float* m, float* v, const float* powers, size_t n, float lr,
-                        float b1, float b2, float eps, float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, g, m, v, powers, n, lr, b1, b2,
+extern "C" int dcg_adam(float* w, bf16* wbf, const float* g, float* m, float* v, const float* powers, size_t n,
+                        float lr, float b1, float b2, float eps, float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, wbf, g, m, v, powers, n, lr, b1, b2,
                      eps, gscale);
   return (int)hipGetLastError();
 }

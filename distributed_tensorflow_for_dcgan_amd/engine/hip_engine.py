@@ -149,23 +149,11 @@ class HipEngine:
         self.coef.update({name: t(1, C, 3, dtype=torch.float32) for name, C in cfg.g_bn_layers()})
         self.coef_g = {name: t(1, C, 3, dtype=torch.float32) for name, C in cfg.d_bn_layers()}
         self.small_part = t(64, 16, dtype=torch.float32)
-        # ---------------- packed bf16 weights
-        self.wp = {}
-        for L in self.dl:
-            w = self.model.d[L.name + "/w"]
-            nat = t(25, L.cin, L.cout)  # HWIO natural -> dgrad [25][N=ci][Kc=co]
-            if L.cin % 8 == 0:
-                tr = t(25, L.cout, L.cin)  # fwd [25][co][ci]
-            else:
-                tr = t(L.cout, self.kp_d0, zero=True)  # im2col [co][tap*ci]
-            self.wp[L.name] = (nat, tr)
-        for L in self.gl:
-            nat = t(25, L.cout, L.cin)  # fwd [25][co][ci]
-            if L.cout % 8 == 0:
-                tr = t(25, L.cin, L.cout)  # dgrad [25][ci][co]
-            else:
-                tr = t(L.cin, self.kp_g, zero=True)  # im2col [ci][tap*co]
-            self.wp[L.name] = (nat, tr)
+        # ---------------- bf16 weight mirrors: the SAME flat layout as the fp32 masters (TF layouts:
+        # HWIO conv, [kh,kw,out,in] deconv), written by the Adam kernel; every conv GEMM reads
+        # its weight from here in whichever orientation it needs (igemm3 bkn flag)
+        self.wbf_d = self.model.d.like(torch.bfloat16)
+        self.wbf_g = self.model.g.like(torch.bfloat16)
 
     # ------------------------------------------------------------------ program build
     def _stats_buf(self, key, P, C):
@@ -185,28 +173,34 @@ class HipEngine:
         self._build_update(self.progC, "d")
         self._c_split = self.progC.size()
         self._build_update(self.progC, "g")
-        self.progPack = ext.Program()
-        self._build_pack(self.progPack)
+        self.progCast = ext.Program()  # fp32 masters -> bf16 mirrors (init / checkpoint load)
+        for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
+            self.progCast.cast_to_bf16("mirror", _p(ps.flat), 0, _p(pb.flat), ps.flat.numel(), 1.0, 0.0, 0)
         self.progS = None  # sampler program, built lazily
         self.progEval = None
 
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
-               cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None):
-        cfg = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group)
-        prog.igemm(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
-                   ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0)
+               cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None, bkn=False, kb_valid=-1):
+        """One conv-shaped GEMM. Bw is a bf16 weight-mirror view; bkn=True reads it as
+        [tap][K][N] (D forward, G dgrad, im2col'd layers), else as [tap][N][K]."""
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn)
+        if plan is None:
+            raise RuntimeError("no igemm tile for %s (mode %d, N %d, bkn %d)" % (name, mode, N, bkn))
+        cfg, splits = plan
+        prog.igemm_ex(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
+                      ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0, int(bkn), kb_valid, splits)
         return cfg
 
-    def _igemm_stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None):
+    def _igemm_stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None, bkn=False):
         if mode == 1:
             M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
             phases = 4
         else:
             M = Bn * Hout * Wout
             phases = 1
-        cfg = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group)
-        bm, _ = H.IGEMM_CFGS[cfg % 100]
+        cfg, _ = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn)
+        bm, _ = H.tile_of(cfg)
         return -(-M // bm) * phases
 
     def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema):
@@ -249,8 +243,9 @@ class HipEngine:
         prog.colstats("g_bn0.stats", 0, _p(self.g_h0_pre), 0, 0, 0, 0, 0, 0.0, rows0, C0, rpb, rows0, _p(part0), 0)
         self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, rows0 // rpb, update_ema)
         a_prev = self.g_h0
+        Wg, Wd = self.wbf_g, self.wbf_d
         for L in self.gl:
-            nat, tr = self.wp[L.name]
+            nat = Wg[L.name + "/w"]  # [5,5,co,ci] = [tap][N][K]
             pad = same_pads(L.out_hw)[0]
             if L.bn:
                 P = self._igemm_stats_tiles(1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout)
@@ -267,29 +262,31 @@ class HipEngine:
         # D forward on [real | fake]
         prev = self.d_in
         for i, L in enumerate(self.dl):
-            nat, tr = self.wp[L.name]
+            w = Wd[L.name + "/w"]  # HWIO [5,5,ci,co] = [tap][K][N]
             pad = same_pads(L.in_hw)[0]
             rows = B2 * L.out_hw ** 2
             if i == 0 and L.cin % 8 != 0:
                 prog.im2col_s2("d0.im2col", _p(prev), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                L.out_hw, pad, pad, self.kp_d0, 0)
-                self._igemm(prog, L.name, 2, self.d0_col, tr, self.d_a[L.name], B2, 1, 1, self.kp_d0, L.out_hw,
-                            L.out_hw, L.cout, 0, bias=Pd[L.name + "/biases"], act=LRELU)
+                self._igemm(prog, L.name, 2, self.d0_col, w, self.d_a[L.name], B2, 1, 1, self.kp_d0, L.out_hw,
+                            L.out_hw, L.cout, 0, bias=Pd[L.name + "/biases"], act=LRELU, bkn=True,
+                            kb_valid=25 * L.cin)
             elif not L.bn:
-                self._igemm(prog, L.name, 0, prev, tr, self.d_a[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                            L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU)
+                self._igemm(prog, L.name, 0, prev, w, self.d_a[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU, bkn=True)
             else:
                 rpg = B * L.out_hw ** 2
-                if H.pick_igemm_cfg(rows, L.cout, 1, rpg) is not None:
+                if H.igemm_cfg_for(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True) is not None:
                     # BN partial statistics straight from the conv epilogue (tiles never straddle
                     # the real/fake boundary)
-                    P = self._igemm_stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg)
+                    P = self._igemm_stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True)
                     part = self._stats_buf(L.bn, P, L.cout)
-                    self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                                L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg)
+                    self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                                L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg,
+                                bkn=True)
                 else:  # odd sizes: no tile divides the group -> separate group-aligned stats pass
-                    self._igemm(prog, L.name, 0, prev, tr, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                                L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"])
+                    self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                                L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], bkn=True)
                     rpb = self._rows_per_block(rpg, L.cout)
                     P = rows // rpb
                     part = self._stats_buf(L.bn, P, L.cout)
@@ -337,7 +334,7 @@ class HipEngine:
                             gD[L.name + "/w"])
             # data gradient into the previous activation (not needed below layer 0)
             if i > 0:
-                nat, _ = self.wp[L.name]
+                nat = self.wbf_d[L.name + "/w"]
                 P_ = self.dl[i - 1]
                 self._igemm(prog, L.name + ".dgrad", 1, dx, nat, self.d_da[P_.name], B2, L.out_hw, L.out_hw, L.cout,
                             L.in_hw, L.in_hw, L.cin, pad)
@@ -400,7 +397,7 @@ class HipEngine:
                              self.coef_g[L.bn], write_param_grads=False, row_offset_groups=1)
             else:
                 prog.act_bwd("g." + L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
-            nat, _ = self.wp[L.name]
+            nat = self.wbf_d[L.name + "/w"]
             pad = same_pads(L.in_hw)[0]
             if i > 0:
                 P_ = self.dl[i - 1]
@@ -418,19 +415,19 @@ class HipEngine:
         a_prev = self.g_a[self.gl[-2].name] if n > 1 else self.g_h0
         da_prev = self.g_da[self.gl[-2].name] if n > 1 else self.g_da0
         padL = same_pads(Lg.out_hw)[0]
-        _, trL = self.wp[Lg.name]
+        wL = self.wbf_g[Lg.name + "/w"]  # [5,5,co,ci] read as [tap][K=co][N=ci]
         if Lg.cout % 8 != 0:
             prog.im2col_s2("g_out.im2col", _p(self.img_g), _p(self.g_last_col), B, Lg.out_hw, Lg.out_hw, Lg.cout,
                            Lg.in_hw, Lg.in_hw, padL, padL, self.kp_g, 0)
             self._wgrad(prog, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
                         0, gG[Lg.name + "/w"])
-            self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, trL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
-                        Lg.in_hw, Lg.cin, 0)
+            self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, wL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
+                        Lg.in_hw, Lg.cin, 0, bkn=True, kb_valid=25 * Lg.cout)
         else:
             self._wgrad(prog, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
                         Lg.cin, padL, gG[Lg.name + "/w"])
-            self._igemm(prog, Lg.name + ".dgrad", 0, self.img_g, trL, da_prev, B, Lg.out_hw, Lg.out_hw, Lg.cout,
-                        Lg.in_hw, Lg.in_hw, Lg.cin, padL)
+            self._igemm(prog, Lg.name + ".dgrad", 0, self.img_g, wL, da_prev, B, Lg.out_hw, Lg.out_hw, Lg.cout,
+                        Lg.in_hw, Lg.in_hw, Lg.cin, padL, bkn=True)
         for j in range(n - 2, -1, -1):
             L = self.gl[j]
             rows = B * L.out_hw ** 2
@@ -442,9 +439,8 @@ class HipEngine:
             pad = same_pads(L.out_hw)[0]
             self._wgrad(prog, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
                         gG[L.name + "/w"])
-            _, tr = self.wp[L.name]
-            self._igemm(prog, L.name + ".dgrad", 0, dx, tr, dsrc, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw,
-                        L.cin, pad)
+            self._igemm(prog, L.name + ".dgrad", 0, dx, self.wbf_g[L.name + "/w"], dsrc, B, L.out_hw, L.out_hw,
+                        L.cout, L.in_hw, L.in_hw, L.cin, pad, bkn=True)
         # g_bn0 backward + projection gradients
         C0 = cfg.g_base_ch
         rows0 = B * cfg.g_base_hw ** 2
@@ -453,43 +449,25 @@ class HipEngine:
         prog.linear_wgrad("g_h0_lin.wgrad", _p(self.z), _p(self.g_dx0), _p(gG["g_h0_lin/Matrix"]),
                           _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
 
-    # ---- optimiser + repack
+    # ---- optimiser (+ bf16 weight mirrors)
     def _build_update(self, prog, which="dg"):
-        """TF-Adam for D and/or G. The D half (adam_d + D repack) comes first so that under
-        DDP it overlaps with the G-gradient all-reduce still in flight."""
+        """TF-Adam for D and/or G; each Adam also writes the bf16 mirror the conv GEMMs read.
+        The D half comes first so that under DDP it overlaps with the G-gradient all-reduce."""
         gs = 1.0 / self.world
         od, og = self.opt_d, self.opt_g
         if "d" in which:
-            prog.adam("adam_d", _p(self.model.d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
-                      _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0)
-            self._build_pack(prog, "d")
+            prog.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
+                         _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
+                         gs, 0)
         if "g" in which:
-            prog.adam("adam_g", _p(self.model.g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
-                      _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0)
+            prog.adam_bf("adam_g", _p(self.model.g.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
+                         _p(og.v.flat), _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
+                         gs, 0)
             prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
                           _p(self.step_counter), 0)
-            self._build_pack(prog, "g")
-
-    def _build_pack(self, prog, which="dg"):
-        for L in (self.dl if "d" in which else []):
-            w = self.model.d[L.name + "/w"]
-            nat, tr = self.wp[L.name]
-            ci, co = L.cin, L.cout
-            if ci % 8 == 0:
-                prog.pack(L.name + ".pack", _p(w), 25, ci, co, _p(nat), _p(tr), co * ci, ci, 1, 0)
-            else:  # tr[co][tap*ci + a]
-                prog.pack(L.name + ".pack", _p(w), 25, ci, co, _p(nat), _p(tr), ci, self.kp_d0, 1, 0)
-        for L in (self.gl if "g" in which else []):
-            w = self.model.g[L.name + "/w"]
-            nat, tr = self.wp[L.name]
-            co, ci = L.cout, L.cin  # w [25][co][ci]
-            if co % 8 == 0:
-                prog.pack(L.name + ".pack", _p(w), 25, co, ci, _p(nat), _p(tr), ci * co, co, 1, 0)
-            else:
-                prog.pack(L.name + ".pack", _p(w), 25, co, ci, _p(nat), _p(tr), co, self.kp_g, 1, 0)
 
     def _repack_weights_now(self):
-        H.run(self.progPack)
+        H.run(self.progCast)
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ execution
@@ -640,7 +618,7 @@ class HipEngine:
                           B * cfg.g_base_hw ** 2, C0, B * cfg.g_base_hw ** 2, RELU, 0.0, 0)
         prev = h0
         for L in self.gl:
-            nat, _ = self.wp[L.name]
+            nat = self.wbf_g[L.name + "/w"]
             pad = same_pads(L.out_hw)[0]
             if L.bn:
                 xb, ab = t(B, L.out_hw, L.out_hw, L.cout), t(B, L.out_hw, L.out_hw, L.cout)

@@ -68,6 +68,16 @@ def _p(t: Optional[torch.Tensor]) -> int:
 # --------------------------------------------------------------------------- tile policy
 IGEMM_CFGS = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (32, 64), 5: (64, 32),
               6: (32, 32), 7: (128, 16), 8: (64, 16), 9: (256, 64)}
+IGEMM3_TILES = {0: (128, 128), 1: (256, 64), 2: (64, 256), 3: (128, 64), 4: (64, 128), 5: (64, 64)}
+
+
+def tile_of(cfg: int) -> Tuple[int, int]:
+    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..219 igemm3.hip."""
+    if cfg >= 200:
+        return IGEMM3_TILES[cfg % 10]
+    return IGEMM_CFGS[cfg % 100]
+
+
 WGRAD_CFGS = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64), 4: (32, 64), 5: (64, 32), 6: (32, 32)}
 CU_COUNT = 256
 
@@ -97,37 +107,73 @@ def pick_igemm_cfg(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
     return best  # None when no tile divides rows_per_group (caller computes stats separately)
 
 
+def pick_igemm3(M: int, N: int, Kc: int, taps: int, phases: int = 1, rows_per_group: Optional[int] = None,
+                target_blocks: int = 2 * CU_COUNT) -> Optional[Tuple[int, int]]:
+    """(cfg, splits) heuristic for igemm3: the largest 64x64-per-wave tile that fits N, then
+    split-K until ~target_blocks workgroups (each split keeps >= 4 K tiles)."""
+    if N >= 128:
+        order = [200, 201, 203, 205]
+    elif N >= 64:
+        order = [201, 203, 205]
+    else:
+        return None
+    kt = taps * -(-Kc // 64)
+    for c in order:
+        bm, bn = IGEMM3_TILES[c % 10]
+        if rows_per_group is not None and rows_per_group % bm != 0:
+            continue
+        tiles = -(-M // bm) * -(-N // bn) * phases
+        sp = 1
+        while tiles * sp < target_blocks and kt // (sp * 2) >= 4 and sp < 8:
+            sp *= 2
+        if tiles * sp >= target_blocks // 2 or c == order[-1]:
+            return c, sp
+    return None
+
+
 _TUNED = None
 TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "igemm_tuned.json")
 
 
 def tuned_table() -> dict:
     """Per-layer tile choices measured on MI355X by ``benchmarks/bench_kernels.py --write``
-    (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> cfg; cfg >= 100 selects LDS-DMA staging)."""
+    (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> "cfg:splits" (or a bare cfg): cfg < 200 is
+    igemm.hip (+100 = LDS-DMA staging), 200..219 igemm3.hip)."""
     global _TUNED
     if _TUNED is None:
         _TUNED = {}
         if os.environ.get("DCGAN_NO_TUNED") != "1" and os.path.exists(TUNED_PATH):
             import json
             with open(TUNED_PATH) as f:
-                _TUNED = {k: int(v) for k, v in json.load(f).items()}
+                for k, v in json.load(f).items():
+                    c, _, sp = str(v).partition(":")
+                    _TUNED[k] = (int(c), int(sp or 1))
     return _TUNED
 
 
 def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wout: int, N: int,
-                  rows_per_group: Optional[int] = None) -> Optional[int]:
-    """Tile for one implicit-GEMM launch: the tuned entry when present and legal for the
-    BN-statistics grouping, else the occupancy heuristic of :func:`pick_igemm_cfg`."""
+                  rows_per_group: Optional[int] = None, bkn: bool = False) -> Optional[Tuple[int, int]]:
+    """(cfg, splits) for one implicit-GEMM launch: the tuned entry when present and legal
+    (weight layout, BN-statistics grouping), else the heuristics. None when no tile can
+    produce group-aligned statistics (caller computes them in a separate pass)."""
     if mode == 1:
-        M, phases = Bn * (-(-Hout // 2)) * (-(-Wout // 2)), 4
+        M, phases, taps = Bn * (-(-Hout // 2)) * (-(-Wout // 2)), 4, 9
     else:
-        M, phases = Bn * Hout * Wout, 1
-    cfg = tuned_table().get("%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N))
-    if cfg is not None and cfg % 100 in IGEMM_CFGS:
-        bm, _ = IGEMM_CFGS[cfg % 100]
-        if rows_per_group is None or rows_per_group % bm == 0:
-            return cfg
-    return pick_igemm_cfg(M, N, phases, rows_per_group)
+        M, phases, taps = Bn * Hout * Wout, 1, (25 if mode == 0 else 1)
+    ent = tuned_table().get("%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N))
+    if ent is not None:
+        cfg, sp = ent
+        ok = cfg >= 200 or (not bkn and sp == 1 and cfg % 100 in IGEMM_CFGS)
+        if ok and (rows_per_group is None or rows_per_group % tile_of(cfg)[0] == 0):
+            return cfg, sp
+    if N % 8 == 0 and N >= 64:
+        r = pick_igemm3(M, N, Kc, taps, phases, rows_per_group)
+        if r is not None:
+            return r
+    if bkn:
+        return None
+    c = pick_igemm_cfg(M, N, phases, rows_per_group)
+    return None if c is None else (c, 1)
 
 
 def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_COUNT) -> Tuple[int, int]:
@@ -185,61 +231,65 @@ def pack_im2col_weight(w: torch.Tensor, kind: str, kpad: int) -> torch.Tensor:
 
 def conv2d_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                 act: Optional[str] = None, leak: float = 0.2, stats: bool = False, out_f32: bool = False,
-                cfg: Optional[int] = None):
+                cfg: Optional[int] = None, bkn: bool = False, splits: int = 1):
     """TF-SAME stride-2 5x5 conv on the HIP igemm kernel. x bf16 NHWC [B,H,W,Ci] (Ci % 8 == 0),
-    w_packed bf16 [25][co][ci]. Returns y (and per-tile stats partials [P,2,co] if stats)."""
+    w_packed bf16 [25][co][ci] (bkn=True: [25][ci][co], i.e. the HWIO weight itself; cfg >= 200).
+    Returns y (and per-tile stats partials [P,2,co] if stats)."""
     _check_bf16(x, w_packed)
     B, H, W, Ci = x.shape
     Ho, Wo = same_out(H), same_out(W)
     py, px = same_pads(H)[0], same_pads(W)[0]
     M = B * Ho * Wo
     cfg = pick_igemm_cfg(M, cout) if cfg is None else cfg
-    bm, bn = IGEMM_CFGS[cfg % 100]
+    bm, bn = tile_of(cfg)
     y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     mt = -(-M // bm)
     st = torch.empty(mt, 2, cout, device=x.device, dtype=torch.float32) if stats else None
     prog = ext().Program()
-    prog.igemm("conv", 0, _p(x), _p(w_packed), _p(y), B, H, W, Ci, Ho, Wo, cout, py, px, cfg, int(out_f32), cout, 0,
-               _p(bias), ACT[act], leak, _p(st), 0)
+    prog.igemm_ex("conv", 0, _p(x), _p(w_packed), _p(y), B, H, W, Ci, Ho, Wo, cout, py, px, cfg, int(out_f32), cout,
+                  0, _p(bias), ACT[act], leak, _p(st), 0, int(bkn), -1, splits)
     run(prog)
     return (y, st) if stats else y
 
 
 def conv2d_transpose_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, out_hw: Tuple[int, int],
                           bias: Optional[torch.Tensor] = None, act: Optional[str] = None, leak: float = 0.2,
-                          stats: bool = False, out_f32: bool = False, cfg: Optional[int] = None):
+                          stats: bool = False, out_f32: bool = False, cfg: Optional[int] = None,
+                          bkn: bool = False, splits: int = 1):
     """TF-SAME stride-2 5x5 conv_transpose via 4 sub-pixel phases. x bf16 [B,Hi,Wi,Ci],
-    w_packed bf16 [25][co][ci]."""
+    w_packed bf16 [25][co][ci] (bkn=True: [25][ci][co]; cfg >= 200)."""
     _check_bf16(x, w_packed)
     B, Hi, Wi, Ci = x.shape
     Ho, Wo = out_hw
     py, px = same_pads(Ho)[0], same_pads(Wo)[0]
     Mphase = B * (-(-Ho // 2)) * (-(-Wo // 2))
     cfg = pick_igemm_cfg(Mphase, cout, phases=4) if cfg is None else cfg
-    bm, bn = IGEMM_CFGS[cfg % 100]
+    bm, bn = tile_of(cfg)
     y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     prog = ext().Program()
     st = None
     if stats:
         mt = -(-Mphase // bm)
         st = torch.empty(mt * 4, 2, cout, device=x.device, dtype=torch.float32)
-    prog.igemm("deconv", 1, _p(x), _p(w_packed), _p(y), B, Hi, Wi, Ci, Ho, Wo, cout, py, px, cfg, int(out_f32), cout,
-               0, _p(bias), ACT[act], leak, _p(st), 0)
+    prog.igemm_ex("deconv", 1, _p(x), _p(w_packed), _p(y), B, Hi, Wi, Ci, Ho, Wo, cout, py, px, cfg, int(out_f32),
+                  cout, 0, _p(bias), ACT[act], leak, _p(st), 0, int(bkn), -1, splits)
     run(prog)
     return (y, st) if stats else y
 
 
 def gemm_plain(a: torch.Tensor, bt: torch.Tensor, out_f32: bool = False, bias=None, act=None,
-               cfg: Optional[int] = None) -> torch.Tensor:
-    """C[M][N] = A[M][K] . Bt[N][K] (bf16, K % 8 == 0)."""
+               cfg: Optional[int] = None, bkn: bool = False, splits: int = 1) -> torch.Tensor:
+    """C[M][N] = A[M][K] . Bt[N][K] (bf16, K % 8 == 0). bkn=True: bt is B[Kb][N] (n contiguous,
+    Kb <= K rows; rows Kb..K-1 read as zeros -- the im2col K padding)."""
     _check_bf16(a, bt)
     M, K = a.shape
-    N = bt.shape[0]
+    N = bt.shape[1] if bkn else bt.shape[0]
+    kb = bt.shape[0] if bkn else -1
     cfg = pick_igemm_cfg(M, N) if cfg is None else cfg
     c = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     prog = ext().Program()
-    prog.igemm("gemm", 2, _p(a), _p(bt), _p(c), M, 1, 1, K, 1, 1, N, 0, 0, cfg, int(out_f32), N, 0, _p(bias),
-               ACT[act], 0.2, 0, 0)
+    prog.igemm_ex("gemm", 2, _p(a), _p(bt), _p(c), M, 1, 1, K, 1, 1, N, 0, 0, cfg, int(out_f32), N, 0, _p(bias),
+                  ACT[act], 0.2, 0, 0, int(bkn), kb, splits)
     run(prog)
     return c
 

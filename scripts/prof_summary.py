@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=0, help="timed steps at the end of the trace")
-    ap.add_argument("--match", default="dcg::", help="substring of our kernels")
+    ap.add_argument("--match", default="dcg", help="substring of our kernels (mangled names too)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, accum_vgpr_count, "

@@ -115,6 +115,69 @@ def test_im2col_and_plain_gemm_3ch():
     close(y, ref, 2e-3, "im2col conv")
 
 
+IG3 = [200, 201, 202, 203, 204, 205, 210, 211, 212, 213, 214, 215]
+
+
+@pytest.mark.parametrize("bkn", [0, 1])
+def test_igemm3_conv_all_tiles_layouts_splits(bkn):
+    """v3 kernel: every tile / stage count, both weight layouts, split-K 1/3/4 (in-kernel
+    reduction), fused lrelu + BN stats; split-K results are bitwise reproducible."""
+    h = H()
+    B, Hs, Ci, Co = 4, 16, 128, 256
+    x = bf(rnd(B, Hs, Hs, Ci, seed=40))
+    w = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=41))          # HWIO = [25][Ci][Co] = bkn layout
+    wt = h.pack_conv_weight(w.float(), "conv", "fwd")        # [25][Co][Ci]
+    ref_pre = R.conv2d_same(x.float(), w.float())
+    wp = w.reshape(25, Ci, Co).contiguous() if bkn else wt
+    for cfg in IG3:
+        for splits in (1, 3, 4):
+            y, st = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn), splits=splits)
+            tag = "cfg%d bkn%d s%d" % (cfg, bkn, splits)
+            close(y, R.lrelu(ref_pre), 1.5e-2, tag)
+            s = st.sum(0)
+            close(s[0], ref_pre.reshape(-1, Co).sum(0), 2e-3, "sum " + tag)
+            close(s[1], ref_pre.reshape(-1, Co).pow(2).sum(0), 2e-3, "sumsq " + tag)
+            if splits > 1:
+                y2, st2 = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn), splits=splits)
+                assert torch.equal(y, y2) and torch.equal(st, st2), "nondeterministic " + tag
+
+
+@pytest.mark.parametrize("B,Hi,Ho,Ci,Co", [(8, 4, 8, 256, 128), (2, 4, 7, 64, 64), (4, 8, 16, 128, 64)])
+def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
+    h = H()
+    x = bf(rnd(B, Hi, Hi, Ci, seed=42))
+    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=43))  # deconv [5,5,out,in] = [25][N][Kc] (bt layout)
+    bias = rnd(Co, scale=0.1, seed=44)
+    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
+    for cfg in (200, 203, 205, 212, 215):
+        for splits in (1, 2, 5):
+            y = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True, cfg=cfg,
+                                        splits=splits)
+            close(y, ref, 2e-3, "deconv cfg%d s%d" % (cfg, splits))
+    # G dgrad = conv of dy with the deconv weight read k-major ([25][Kc=out][N=in], bkn)
+    xd = rnd(B, Hi, Hi, Ci, seed=45).requires_grad_(True)
+    yd = R.conv2d_transpose_same(xd, w.float(), (Ho, Ho))
+    dy = bf(rnd(B, Ho, Ho, Co, seed=46))
+    (gx,) = torch.autograd.grad(yd, xd, dy.float())
+    for cfg in (200, 205, 213):
+        for splits in (1, 4):
+            out = h.conv2d_same(dy, w.reshape(25, Co, Ci), Ci, out_f32=True, cfg=cfg, bkn=True, splits=splits)
+            close(out, gx, 2e-3, "G dgrad cfg%d s%d" % (cfg, splits))
+
+
+def test_igemm3_plain_im2col_bkn():
+    """3-channel layers: im2col rows [M][80] x the natural weight [75][N] (rows 75..79 -> 0)."""
+    h = H()
+    B, Hs, C, Co = 4, 64, 3, 64
+    x = bf(rnd(B, Hs, Hs, C, seed=47))
+    col = h.im2col_s2(x, 80)
+    w = bf(rnd(5, 5, C, Co, scale=0.05, seed=48))
+    ref = R.conv2d_same(x.float(), w.float()).reshape(-1, Co)
+    for cfg in (201, 203, 205, 211):
+        y = h.gemm_plain(col, w.reshape(75, Co).contiguous(), out_f32=True, cfg=cfg, bkn=True)
+        close(y, ref, 2e-3, "im2col bkn cfg%d" % cfg)
+
+
 def test_wgrad_conv_and_deconv():
     h = H()
     B, Hs, Ci, Co = 4, 16, 64, 128
