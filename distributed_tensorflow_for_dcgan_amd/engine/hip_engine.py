@@ -76,6 +76,7 @@ class HipEngine:
         self.step_counter = torch.zeros(1, dtype=torch.int64, device=device)  # device global step
         self.graph_requested = bool(graph)
         self.graph_enabled = False
+        self._timing = False
         self._graphs: List[Optional[torch.cuda.CUDAGraph]] = []
         self.comm_stream = torch.cuda.Stream(device=device) if world > 1 else None
         self.allreduce_dtype = allreduce_dtype
@@ -478,10 +479,27 @@ class HipEngine:
         """The step as (program, begin, end) segments. Single process: one segment. DDP: the
         collectives sit between segments -- D-grad all-reduce overlaps G backward (B), the
         G-grad all-reduce overlaps D's Adam + repack (C[:split])."""
-        if self.world == 1:
+        if self.world == 1 and not self._timing:
             return [[(self.progA, 0, -1), (self.progB, 0, -1), (self.progC, 0, -1)]]
         return [[(self.progA, 0, -1)], [(self.progB, 0, -1)], [(self.progC, 0, self._c_split)],
                 [(self.progC, self._c_split, -1)]]
+
+    def enable_timing(self) -> None:
+        """Per-phase GPU timers: the step runs as 4 segments with events
+        between them. Call before the first train_step (graphs are captured per segment)."""
+        if self._graphs:
+            raise RuntimeError("enable_timing() must precede the first train_step")
+        self._timing = True
+        self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
+
+    def phase_times(self) -> Dict[str, float]:
+        """Milliseconds of the last step's phases (synchronises on its last event)."""
+        if not self._timing:
+            return {}
+        ev = self._ev
+        ev[6].synchronize()
+        names = ("fwd+D_bwd", "G_bwd", "wait_allreduce_D", "adam_D", "wait_allreduce_G", "adam_G")
+        return {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(names)}
 
     def _run_segment(self, i, st):
         if self.graph_enabled:
@@ -492,17 +510,30 @@ class HipEngine:
 
     def _run_step(self):
         st = self._streams()
-        if self.world == 1:
+        if self.world == 1 and not self._timing:
             self._run_segment(0, st)
             return
+        cs = st[0]
+        tick = (lambda i: self._ev[i].record(cs)) if self._timing else (lambda i: None)
+        ddp = self.world > 1
+        tick(0)
         self._run_segment(0, st)          # fwd + D backward -> grad_d final
-        self._ar_d.launch()
+        tick(1)
+        if ddp:
+            self._ar_d.launch()
         self._run_segment(1, st)          # G backward (overlaps the D all-reduce)
-        self._ar_g.launch()
-        self._ar_d.wait(scale_in_place=False)
-        self._run_segment(2, st)          # Adam D + repack D (overlaps the G all-reduce)
-        self._ar_g.wait(scale_in_place=False)
-        self._run_segment(3, st)          # Adam G, step counter, repack G
+        tick(2)
+        if ddp:
+            self._ar_g.launch()
+            self._ar_d.wait(scale_in_place=False)
+        tick(3)
+        self._run_segment(2, st)          # Adam D -> D bf16 mirror (overlaps the G all-reduce)
+        tick(4)
+        if ddp:
+            self._ar_g.wait(scale_in_place=False)
+        tick(5)
+        self._run_segment(3, st)          # Adam G, step counter, G bf16 mirror
+        tick(6)
 
     def _ensure_comm(self):
         if self.world > 1 and not hasattr(self, "_ar_d"):

@@ -113,6 +113,25 @@ def average_scalars(values: Sequence[float], device: torch.device) -> List[float
     return (t / dist.get_world_size()).tolist()
 
 
+def params_in_sync(tensors: Sequence[torch.Tensor], device: torch.device) -> bool:
+    """Cross-rank divergence check: every rank hashes its parameters (exact
+    bit pattern, order-sensitive), MIN and MAX of the hashes are all-reduced; equal <=> in sync."""
+    if not is_initialized():
+        return True
+    h = torch.zeros(2, dtype=torch.int64, device=tensors[0].device)
+    for i, t in enumerate(tensors):
+        bits = t.detach().contiguous().view(torch.int32).to(torch.int64)
+        w = torch.arange(1, bits.numel() + 1, device=bits.device, dtype=torch.int64) % 65521 + 1
+        h[0] += ((bits * w).sum() * (i + 1)) & 0x3FFFFFFFFFFF
+        h[1] += (bits.sum() * (2 * i + 3)) & 0x3FFFFFFFFFFF
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    lo = h.to(dev).clone()
+    hi = h.to(dev).clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(lo, hi))
+
+
 def make_buckets(numel: int, bucket_elems: int, align: int = 64) -> List[Tuple[int, int]]:
     """Split [0, numel) into contiguous (start, end) buckets of ~bucket_elems, 64-aligned."""
     bucket_elems = max(align, (bucket_elems // align) * align)

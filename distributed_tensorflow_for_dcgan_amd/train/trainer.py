@@ -62,7 +62,8 @@ def run(flags: Flags, out=None) -> int:
     device = _device(flags, cl["local_rank"])
     if device.type == "cuda":
         torch.cuda.set_device(device)
-    D.init_distributed(world, rank, device, cl["master_addr"], cl["master_port"])
+    D.init_distributed(world, rank, device, cl["master_addr"], cl["master_port"],
+                       timeout_s=float(flags.collective_timeout))
     chief = rank == 0
     cfg = config_from_flags(flags)
     B = int(flags.batch_size)
@@ -83,6 +84,15 @@ def run(flags: Flags, out=None) -> int:
               else "load failed!!", file=out)
         if info and not (info.get("adam_d") and info.get("adam_g")):
             print("note: checkpoint has no optimiser state (reference-style); Adam restarts at t=0", file=out)
+
+    if flags.explicitly_set("is_train") and not flags.is_train:
+        try:
+            return _test_mode(engine, flags, cfg, B, device, info, chief, out)
+        finally:
+            D.barrier()
+            D.shutdown()
+    if bool(flags.timing) and hasattr(engine, "enable_timing"):
+        engine.enable_timing()
 
     source = make_source(flags, B, shape, device, rank=rank, world=world)
     sample_source = None
@@ -106,7 +116,9 @@ def run(flags: Flags, out=None) -> int:
         a, b = flags.profile_steps.split(":")
         prof_range = (int(a), int(b))
     prof = None
-    fault_at = int(os.environ.get("DCGAN_FAULT_AT_STEP", "-1"))
+    fault_at = int(os.environ.get("DCGAN_FAULT_AT_STEP", "-1"))  # fault injection
+    if os.environ.get("DCGAN_FAULT_RANK", "") not in ("", str(rank)):
+        fault_at = -1
 
     step = int(engine.global_step)
     start_time = time.time()
@@ -132,6 +144,9 @@ def run(flags: Flags, out=None) -> int:
                 ips = B * world * (step - last_rate_step) / max(1e-9, now - last_rate_t) if step > last_rate_step else 0.0
                 print(STEP_LINE % (step // step_per_epoch, step % step_per_epoch, now - start_time,
                                    L["d_loss"], L["g_loss"]) + ", images/sec: %.1f" % ips, file=out, flush=True)
+                if flags.timing and hasattr(engine, "phase_times"):
+                    print("phase ms: " + ", ".join("%s %.3f" % kv for kv in engine.phase_times().items()),
+                          file=out, flush=True)
                 if summary_due:
                     print("Running Summary operation on the chief.", file=out)
                     rate = (step - last_rate_step) / max(1e-9, now - last_rate_t)
@@ -157,6 +172,9 @@ def run(flags: Flags, out=None) -> int:
                 _sample(engine, flags, sample_source, source, sample_z, step, step_per_epoch, out)
             if chief and save_now:
                 ckpt.save(engine)
+            if int(flags.check_sync_every) > 0 and world > 1 and step % int(flags.check_sync_every) == 0:
+                if not D.params_in_sync([engine.model.g.flat, engine.model.d.flat], device):
+                    raise RuntimeError("DDP divergence: parameters differ across ranks at step %d" % step)
             if fault_at >= 0 and step == fault_at:
                 print("DCGAN_FAULT_AT_STEP=%d: simulated failure" % fault_at, file=out, flush=True)
                 out.flush()
@@ -174,6 +192,44 @@ def run(flags: Flags, out=None) -> int:
             writer.close()
         D.barrier()
         D.shutdown()
+    return 0
+
+
+def _test_mode(engine, flags, cfg, B, device, info, chief, out) -> int:
+    """``--nois_train``: sample-only mode (the flag the reference defines but never reads,
+    ``image_train.py:23``). Restores the newest checkpoint, writes ``num_samples`` images from
+    the EMA-BN sampler as grids, and with ``--visualize`` per-dimension z sweeps and a z
+    interpolation (carpedm20-style DCGAN visualisations)."""
+    if not info:
+        raise SystemExit(" [!] no checkpoint in %s: train a model first, then run with --nois_train"
+                         % flags.checkpoint_dir)
+    if not chief:
+        return 0
+    gen = torch.Generator().manual_seed(int(flags.seed) + 31337)
+    step = int(engine.global_step)
+    n = max(1, int(flags.num_samples))
+    imgs = []
+    while sum(x.shape[0] for x in imgs) < n:
+        z = (torch.rand(B, cfg.z_dim, generator=gen) * 2 - 1).to(device)
+        imgs.append(engine.sampler(z).detach().float().cpu().numpy())
+    arr = np.concatenate(imgs, 0)[:n]
+    path = os.path.join(flags.sample_dir, "test_%06d.png" % step)
+    IM.save_images(arr, (8, 8) if n == 64 else IM.grid_size(n), path)
+    print("[Test] wrote %d samples to %s" % (n, path), file=out, flush=True)
+    if flags.visualize:
+        base = (torch.rand(1, cfg.z_dim, generator=gen) * 2 - 1).repeat(B, 1)
+        sweep = torch.linspace(-1.0, 1.0, B)
+        for d in range(min(cfg.z_dim, 8)):
+            z = base.clone()
+            z[:, d] = sweep
+            x = engine.sampler(z.to(device)).detach().float().cpu().numpy()
+            IM.save_images(x, IM.grid_size(B), os.path.join(flags.sample_dir, "test_arange_%d.png" % d))
+        z0 = torch.rand(1, cfg.z_dim, generator=gen) * 2 - 1
+        z1 = torch.rand(1, cfg.z_dim, generator=gen) * 2 - 1
+        t = torch.linspace(0.0, 1.0, B).unsqueeze(1)
+        x = engine.sampler(((1 - t) * z0 + t * z1).to(device)).detach().float().cpu().numpy()
+        IM.save_images(x, IM.grid_size(B), os.path.join(flags.sample_dir, "test_interp.png"))
+        print("[Visualize] wrote z sweeps and interpolation to %s" % flags.sample_dir, file=out, flush=True)
     return 0
 
 

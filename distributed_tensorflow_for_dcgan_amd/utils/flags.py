@@ -13,6 +13,7 @@ from __future__ import annotations
 import argparse
 import math
 import os
+import sys
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 # (name, type, default, help)  -- reference flags first, in reference order.
@@ -43,7 +44,7 @@ REFERENCE_FLAGS: List[Tuple[str, str, Any, str]] = [
 
 # Additive flags of this framework (not in the reference).
 EXTRA_FLAGS: List[Tuple[str, str, Any, str]] = [
-    ("dtype", "str", "bf16", "compute dtype of the HIP engine: fp32 | bf16"),
+    ("dtype", "str", "bf16", "compute dtype: bf16 | fp16 (dynamic loss scaling) | fp32 (reference engine)"),
     ("device", "str", "auto", "auto | cpu | cuda (cuda == the local MI355X via HIP)"),
     ("synthetic", "bool", False, "use synthetic images of the configured shape instead of TFRecords"),
     ("max_steps", "int", 1200000, "stop after this many global steps (reference hard-codes 1,200,000)"),
@@ -68,6 +69,11 @@ EXTRA_FLAGS: List[Tuple[str, str, Any, str]] = [
     ("log_every", "int", 1, "print the step line every N steps (reference: every step)"),
     ("summaries", "bool", True, "write TensorBoard event files on the chief"),
     ("verbose", "bool", False, "verbose device / placement logging"),
+    ("timing", "bool", False, "per-phase GPU timers (fwd+D bwd / G bwd / optimiser / comm) on log steps"),
+    ("check_sync_every", "int", 0, "every N steps assert that parameters are bit-identical across ranks"),
+    ("cache_on_device", "bool", False, "decode the whole TFRecord dataset once into GPU memory (288 GB HBM)"),
+    ("collective_timeout", "float", 600.0, "seconds before a hung collective is an error (RCCL watchdog)"),
+    ("num_samples", "int", 64, "images per grid in sample-only mode (--nois_train)"),
 ]
 
 ALL_FLAGS = REFERENCE_FLAGS + EXTRA_FLAGS
@@ -76,8 +82,13 @@ ALL_FLAGS = REFERENCE_FLAGS + EXTRA_FLAGS
 class Flags:
     """Attribute bag that also exposes ``__flags`` like TF 0.x's ``FLAGS``."""
 
-    def __init__(self, values: Dict[str, Any]):
+    def __init__(self, values: Dict[str, Any], explicit: Optional[Sequence[str]] = None):
         object.__setattr__(self, "_values", dict(values))
+        object.__setattr__(self, "_explicit", frozenset(explicit or ()))
+
+    def explicitly_set(self, name: str) -> bool:
+        """True when the flag appeared on the command line (``--x``, ``--x=v``, ``--nox``)."""
+        return name in object.__getattribute__(self, "_explicit")
 
     def __getattr__(self, name: str) -> Any:
         values = object.__getattribute__(self, "_values")
@@ -139,8 +150,18 @@ def parse_flags(argv: Optional[Sequence[str]] = None,
                 defaults_override: Optional[Dict[str, Any]] = None) -> Flags:
     """Parse ``argv`` (without the program name). Unknown flags are an error."""
     parser = build_parser(defaults_override)
-    ns = parser.parse_args(list(argv) if argv is not None else None)
-    return Flags(vars(ns))
+    argv = list(argv) if argv is not None else sys.argv[1:]
+    ns = parser.parse_args(argv)
+    names = {n for n, _, _, _ in ALL_FLAGS}
+    explicit = set()
+    for tok in argv:
+        if tok.startswith("--"):
+            key = tok[2:].split("=", 1)[0]
+            if key in names:
+                explicit.add(key)
+            elif key.startswith("no") and key[2:] in names:
+                explicit.add(key[2:])
+    return Flags(vars(ns), explicit)
 
 
 def default_flags(**overrides: Any) -> Flags:

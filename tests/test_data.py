@@ -146,3 +146,24 @@ def test_image_folder_source(tmp_path):
     x = src.next()
     assert x.shape == (4, 8, 8, 3) and float(x.min()) >= -1 and float(x.max()) <= 1
     src.close()
+
+
+def test_device_cached_source_epochs(tmp_path):
+    """--cache_on_device: the shard is decoded once; every epoch is a permutation of it."""
+    from distributed_tensorflow_for_dcgan_amd.data.pipeline import DeviceCachedSource
+    d = tmp_path / "cache"
+    d.mkdir()
+    imgs = np.stack([np.full((4, 4, 1), (i - 12) / 16.0) for i in range(24)])
+    TR.write_image_records(str(d / "a.tfrecords"), imgs[:12])
+    TR.write_image_records(str(d / "b.tfrecords"), imgs[12:])
+    src = DeviceCachedSource(str(d), 6, (4, 4, 1), "cpu", seed=3, threads=2)
+    assert src.n == 24 and src.num_examples == 24
+    seen = []
+    for _ in range(4):
+        b = src.next()
+        assert b.shape == (6, 4, 4, 1)
+        seen += [round(float(x) * 16) + 12 for x in b[:, 0, 0, 0]]
+    assert sorted(seen) == list(range(24))
+    # rank 1 of 2 with sharding gets the other file only
+    s1 = DeviceCachedSource(str(d), 4, (4, 4, 1), "cpu", rank=1, world=2, shard=True, threads=2)
+    assert s1.n == 12

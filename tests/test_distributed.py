@@ -70,8 +70,14 @@ def _worker_ddp(rank, world, port, out_path):
     ar.wait()
     ok_ar = torch.allclose(buf, torch.arange(1000, dtype=torch.float32) * 1.5)
     flag = D.any_rank(rank == 1, dev)
+    # divergence detector: in sync now; a one-ulp change on one rank is caught
+    sync_ok = D.params_in_sync([eng.model.g.flat, eng.model.d.flat], dev)
+    if rank == 1:
+        eng.model.d.flat[7] = torch.nextafter(eng.model.d.flat[7], torch.tensor(1.0))
+    sync_bad = D.params_in_sync([eng.model.g.flat, eng.model.d.flat], dev)
     if rank == 0:
-        torch.save({"update": ok_update, "same": same, "ar": ok_ar, "any": flag}, out_path)
+        torch.save({"update": ok_update, "same": same, "ar": ok_ar, "any": flag, "sync": sync_ok and not sync_bad},
+                   out_path)
     D.shutdown()
 
 
@@ -79,7 +85,7 @@ def test_ddp_gloo_two_ranks(tmp_path):
     out = str(tmp_path / "res.pt")
     mp.spawn(_worker_ddp, args=(2, _free_port(), out), nprocs=2, join=True)
     res = torch.load(out, weights_only=True)
-    assert res == {"update": True, "same": True, "ar": True, "any": True}
+    assert res == {"update": True, "same": True, "ar": True, "any": True, "sync": True}
 
 
 def test_cli_two_processes_gloo(tmp_path):
@@ -90,10 +96,32 @@ def test_cli_two_processes_gloo(tmp_path):
                    MASTER_PORT=str(port), OMP_NUM_THREADS="2")
         cmd = [sys.executable, os.path.join(ROOT, "image_train.py"), "--synthetic", "--output_size=28", "--c_dim=1",
                "--batch_size=4", "--max_steps=3", "--device=cpu", "--checkpoint_dir=%s" % (tmp_path / "ck"),
-               "--sample_dir=%s" % (tmp_path / "s"), "--save_summaries_secs=1000", "--sample_every=2"]
+               "--sample_dir=%s" % (tmp_path / "s"), "--save_summaries_secs=1000", "--sample_every=2",
+               "--check_sync_every=1"]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = [p.communicate(timeout=600)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
     assert "Epoch: [ 0] step: [ 3]" in outs[0]
     assert os.path.exists(tmp_path / "ck" / "model.ckpt-3.index")
     assert os.path.exists(tmp_path / "s" / "train_00_0001.png")
+
+
+def test_launcher_restarts_after_fault_and_resumes(tmp_path):
+    """2 gloo ranks under the restart launcher: the chief dies at step 10 (fault injection,
+    right after its checkpoint at step 10), the launcher stops rank 1 (blocked in the next
+    collective), restarts both; they resume from step 10 and finish at step 14."""
+    cmd = [sys.executable, "-m", "distributed_tensorflow_for_dcgan_amd.launch", "--nproc", "2", "--max_restarts", "2",
+           "--grace", "5", "--", os.path.join(ROOT, "image_train.py"), "--synthetic", "--output_size=28",
+           "--c_dim=1", "--batch_size=4", "--max_steps=14", "--device=cpu",
+           "--checkpoint_dir=%s" % (tmp_path / "ck"), "--sample_dir=%s" % (tmp_path / "s"),
+           "--save_summaries_secs=1000", "--sample_every=0", "--save_model_secs=1e-9"]
+    env = dict(os.environ, OMP_NUM_THREADS="2", DCGAN_FAULT_AT_STEP="10", DCGAN_FAULT_RANK="0",
+               PYTHONPATH=ROOT)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=900,
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stdout
+    assert "[launch] restart 1/2" in p.stdout
+    assert "global_step 10" in p.stdout  # resumed
+    assert os.path.exists(tmp_path / "ck" / "model.ckpt-14.index")

@@ -63,7 +63,7 @@ def conv_grads64(x, w, dy, kind, out_hw=None):
     return torch.autograd.grad(y, [xv, wv], d64(dy))
 
 
-@pytest.mark.parametrize("size,c_dim,B", [(64, 3, 16), (28, 1, 8)])
+@pytest.mark.parametrize("size,c_dim,B", [(64, 3, 16), (28, 1, 8), (128, 3, 4), (256, 3, 4)])
 def test_engine_stagewise(size, c_dim, B):
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     from distributed_tensorflow_for_dcgan_amd.ops import hip as H
@@ -142,7 +142,7 @@ def test_engine_stagewise(size, c_dim, B):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("size,c_dim,B", [(64, 3, 16), (28, 1, 8), (32, 3, 8)])
+@pytest.mark.parametrize("size,c_dim,B", [(64, 3, 16), (28, 1, 8), (32, 3, 8), (128, 3, 8), (256, 3, 8)])
 def test_engine_step_matches_reference(size, c_dim, B):
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     dev = torch.device("cuda", 0)
@@ -179,7 +179,9 @@ def test_engine_step_matches_reference(size, c_dim, B):
     small_sums = {gl_last + "/biases"}  # 3-element sums over all pixels: heavy cancellation
     bad = {k: v for k, v in errs.items() if v > 0.25 and k not in small_sums}
     assert not bad, bad
-    assert sum(errs.values()) / len(errs) < 0.15
+    # bf16 activations + ReLU/LeakyReLU mask flips compound with depth (each stage is checked
+    # to <= 1-3 % against fp64 on the engine's own tensors in test_engine_stagewise)
+    assert sum(errs.values()) / len(errs) < (0.15 if len(cfg.d_layers()) <= 4 else 0.2)
     for name, _ in cfg.g_bn_layers():
         assert rel(eng.model.g_bn.mean[name], ref_model.g_bn.mean[name]) < 5e-2, name
         assert rel(eng.model.g_bn.var[name], ref_model.g_bn.var[name]) < 5e-2, name

@@ -66,3 +66,31 @@ def test_fault_injection_and_restart(tmp_path):
     first = [l for l in out.splitlines() if l.startswith("Epoch:")][0]
     assert "step: [11]" in first
     assert os.path.exists(tmp_path / "ck" / "model.ckpt-25.index")
+
+
+def test_sample_only_mode_and_visualize(tmp_path):
+    """--nois_train restores the newest checkpoint and only samples (+ --visualize sweeps);
+    without a checkpoint it refuses. The reference default (is_train unset) still trains."""
+    common = ["--synthetic", "--output_size=28", "--c_dim=1", "--batch_size=8", "--device=cpu",
+              "--checkpoint_dir=%s" % (tmp_path / "ck"), "--sample_dir=%s" % (tmp_path / "s"),
+              "--save_summaries_secs=1000", "--sample_every=0"]
+    rc, out = _run(common + ["--nois_train"])
+    assert rc != 0 and "train a model first" in out
+    rc, out = _run(common + ["--max_steps=2"])
+    assert rc == 0 and len([l for l in out.splitlines() if l.startswith("Epoch:")]) == 2, out
+    rc, out = _run(common + ["--is_train=false", "--visualize", "--num_samples=16"])
+    assert rc == 0, out
+    assert "[Test] wrote 16 samples" in out and not [l for l in out.splitlines() if l.startswith("Epoch:")]
+    assert os.path.exists(tmp_path / "s" / "test_000002.png")
+    assert os.path.exists(tmp_path / "s" / "test_arange_0.png") and os.path.exists(tmp_path / "s" / "test_interp.png")
+
+
+def test_device_cache_source_and_timing_flags(tmp_path):
+    data = str(tmp_path / "train")
+    _dataset(data, n=48)
+    rc, out = _run(["--data_dir=%s" % data, "--output_size=28", "--c_dim=1", "--batch_size=8", "--device=cpu",
+                    "--checkpoint_dir=%s" % (tmp_path / "ck"), "--sample_dir=%s" % (tmp_path / "s"),
+                    "--cache_on_device", "--timing", "--save_summaries_secs=1000", "--sample_every=0",
+                    "--max_steps=3", "--loader_threads=2"])
+    assert rc == 0, out
+    assert len([l for l in out.splitlines() if l.startswith("Epoch:")]) == 3
