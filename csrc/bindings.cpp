@@ -21,6 +21,19 @@
 
 #include "hip/kernels.h"
 
+// The fp16 build of the same kernels (csrc/build.py compiles every .hip twice): identical C
+// signatures -- element pointers are 16-bit either way -- with a `_f16` suffix.
+#undef DCG_API
+#define DCG_API(name) name##_f16
+extern "C" {
+#include "hip/launchers.inc"
+}
+#undef DCG_API
+#define DCG_API(name) name
+
+// launcher of the Program's element type (bf16 or fp16)
+#define KF(fn) (f16_ ? fn##_f16 : fn)
+
 namespace py = pybind11;
 using namespace dcg;
 
@@ -41,6 +54,9 @@ struct Op {
 
 class Program {
  public:
+  explicit Program(bool f16 = false) : f16_(f16) {}
+  bool f16() const { return f16_; }
+
   ~Program() {
     for (void* p : dev_allocs_) (void)hipFree(p);
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
@@ -113,8 +129,8 @@ class Program {
     if (kb_valid > Kc) throw std::runtime_error("kb_valid > Kc");
     std::vector<IGemmPhase> ph;
     IGemmArgs a{};
-    a.A = P<const bf16>(A); a.Bn = Bn; a.H = Hin; a.W = Win; a.Kc = Kc;
-    a.Bw = P<const bf16>(Bw); a.N = N;
+    a.A = P<const elem_t>(A); a.Bn = Bn; a.H = Hin; a.W = Win; a.Kc = Kc;
+    a.Bw = P<const elem_t>(Bw); a.N = N;
     a.C = P<void>(C); a.out_f32 = out_f32; a.outH = Hout; a.outW = Wout; a.ldc = ldc; a.cofs = cofs;
     a.bias = P<const float>(bias); a.act = act; a.leak = leak; a.stats = P<float>(stats);
     size_t a_elems, b_elems;
@@ -177,8 +193,8 @@ class Program {
     a.kb_valid = kb_valid;
     a.splits = splits;
     if (!v3)
-      return add(name, stream, [a, cfg, mtiles, ntiles](hipStream_t s) {
-        return dcg_igemm_launch(&a, cfg, mtiles, ntiles, s);
+      return add(name, stream, [this, a, cfg, mtiles, ntiles](hipStream_t s) {
+        return KF(dcg_igemm_launch)(&a, cfg, mtiles, ntiles, s);
       });
     const size_t tiles = (size_t)mtiles * ntiles * a.nphases;
     if (splits > 1) {  // per-op workspace + zeroed arrival counters (reset by the kernel itself)
@@ -193,7 +209,7 @@ class Program {
       a.counters = reinterpret_cast<unsigned*>(ctr);
     }
     const unsigned blocks = (unsigned)(tiles * splits);
-    return add(name, stream, [a, cfg, bkn, blocks](hipStream_t s) { return dcg_igemm3_launch(&a, cfg, bkn, blocks, s); });
+    return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); });
   }
   int last_mtiles() const { return last_mtiles_; }
   int last_nphases() const { return last_nphases_; }
@@ -205,8 +221,8 @@ class Program {
             int Nc, int pad, int cfg, int splits, uintptr_t slabs, uintptr_t dst, size_t dst_elems, float scale,
             int stream) {
     WGradArgs a{};
-    a.G = P<const bf16>(G); a.Hg = Hg; a.Wg = Wg; a.Mc = Mc;
-    a.Dm = P<const bf16>(Dm); a.Nc = Nc;
+    a.G = P<const elem_t>(G); a.Hg = Hg; a.Wg = Wg; a.Mc = Mc;
+    a.Dm = P<const elem_t>(Dm); a.Nc = Nc;
     a.K = Bn * Hd * Wd; a.plain = mode == 2; a.pl = pad; a.ntaps = mode == 2 ? 1 : 25;
     a.out = P<float>(slabs);
     const int KT = (a.K + 63) / 64;
@@ -221,13 +237,13 @@ class Program {
     if (dst_elems > n) throw std::runtime_error("wgrad dst larger than result");
     float* slab = P<float>(slabs);
     float* d = P<float>(dst);
-    add(name, stream, [a, cfg, splits](hipStream_t s) { return dcg_wgrad_launch(&a, cfg, splits, s); });
+    add(name, stream, [this, a, cfg, splits](hipStream_t s) { return KF(dcg_wgrad_launch)(&a, cfg, splits, s); });
     // plain mode may carry padded rows (im2col K padding): reduce only the first dst_elems of
     // each slab's leading part -- rows are m-major so the valid prefix is contiguous.
-    return add(name + ".reduce", stream, [slab, splits, n, d, dst_elems, scale](hipStream_t s) {
-      if (dst_elems == n) return dcg_splitk_reduce(slab, splits, n, d, scale, s);
+    return add(name + ".reduce", stream, [this, slab, splits, n, d, dst_elems, scale](hipStream_t s) {
+      if (dst_elems == n) return KF(dcg_splitk_reduce)(slab, splits, n, d, scale, s);
       // strided variant: reduce the whole slab into itself (slab 0) then copy the valid prefix
-      int rc = dcg_splitk_reduce(slab, splits, n, slab, scale, s);
+      int rc = KF(dcg_splitk_reduce)(slab, splits, n, slab, scale, s);
       if (rc) return rc;
       return (int)hipMemcpyAsync(d, slab, dst_elems * sizeof(float), hipMemcpyDeviceToDevice, s);
     });
@@ -238,7 +254,7 @@ class Program {
                int act, float leak, int R, int C, int rows_per_block, int rows_per_group, uintptr_t part,
                int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_colstats(mode, P<const bf16>(x), P<const bf16>(dy), P<const bf16>(y), P<const float>(mean),
+      return KF(dcg_colstats)(mode, P<const elem_t>(x), P<const elem_t>(dy), P<const elem_t>(y), P<const float>(mean),
                           P<const float>(rstd), act, leak, R, C, rows_per_block, rows_per_group, P<float>(part), s);
     });
   }
@@ -246,7 +262,7 @@ class Program {
                   uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
                   uintptr_t ema_mean, uintptr_t ema_var, float decay, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_bn_finalize(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+      return KF(dcg_bn_finalize)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                              P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
                              P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, s);
     });
@@ -254,14 +270,14 @@ class Program {
   int bn_coef_eval(std::string name, int C, uintptr_t gamma, uintptr_t beta, float eps, uintptr_t mean,
                    uintptr_t var, float debias, uintptr_t scale, uintptr_t shift, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_bn_coef_eval(C, P<const float>(gamma), P<const float>(beta), eps, P<const float>(mean),
+      return KF(dcg_bn_coef_eval)(C, P<const float>(gamma), P<const float>(beta), eps, P<const float>(mean),
                               P<const float>(var), debias, P<float>(scale), P<float>(shift), s);
     });
   }
   int bn_apply_act(std::string name, uintptr_t x, uintptr_t y, uintptr_t scale, uintptr_t shift, int R, int C,
                    int rows_per_group, int act, float leak, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_bn_apply_act(P<const bf16>(x), P<bf16>(y), P<const float>(scale), P<const float>(shift), R, C,
+      return KF(dcg_bn_apply_act)(P<const elem_t>(x), P<elem_t>(y), P<const float>(scale), P<const float>(shift), R, C,
                               rows_per_group, act, leak, s);
     });
   }
@@ -269,7 +285,7 @@ class Program {
                       uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
                       int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_bn_bwd_finalize(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+      return KF(dcg_bn_bwd_finalize)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                                  P<const float>(mean), P<const float>(rstd), P<float>(dgamma), P<float>(dbeta),
                                  P<float>(coef), s);
     });
@@ -277,114 +293,119 @@ class Program {
   int bn_bwd_apply(std::string name, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t coef, uintptr_t dx, int R,
                    int C, int rows_per_group, int act, float leak, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_bn_bwd_apply(P<const bf16>(dy), P<const bf16>(y), P<const bf16>(x), P<const float>(coef),
-                              P<bf16>(dx), R, C, rows_per_group, act, leak, s);
+      return KF(dcg_bn_bwd_apply)(P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x), P<const float>(coef),
+                              P<elem_t>(dx), R, C, rows_per_group, act, leak, s);
     });
   }
   int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_act_bwd(P<const bf16>(dy), P<const bf16>(y), P<bf16>(dx), n, act, leak, s);
+      return KF(dcg_act_bwd)(P<const elem_t>(dy), P<const elem_t>(y), P<elem_t>(dx), n, act, leak, s);
     });
   }
   int sum_partials(std::string name, uintptr_t part, int Pn, int stride, int C, uintptr_t dst, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_sum_partials(P<const float>(part), Pn, stride, C, P<float>(dst), s);
+      return KF(dcg_sum_partials)(P<const float>(part), Pn, stride, C, P<float>(dst), s);
     });
   }
   int colsum_small(std::string name, uintptr_t x, int R, int C, uintptr_t part, int blocks, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_colsum_small(P<const bf16>(x), R, C, P<float>(part), blocks, s);
+      return KF(dcg_colsum_small)(P<const elem_t>(x), R, C, P<float>(part), blocks, s);
     });
   }
 
   // ------------------------------------------------------------------ heads, losses, optimiser
   int gan_loss(std::string name, uintptr_t logits, int B, uintptr_t out, uintptr_t dl_d, uintptr_t dl_g,
-               uintptr_t prob, int stream) {
+               uintptr_t prob, int stream, uintptr_t ls) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_gan_loss(P<const float>(logits), B, P<float>(out), P<float>(dl_d), P<float>(dl_g),
-                          P<float>(prob), s);
+      return KF(dcg_gan_loss)(P<const float>(logits), B, P<float>(out), P<float>(dl_d), P<float>(dl_g),
+                          P<float>(prob), P<const float>(ls), s);
     });
   }
   int linear_fwd(std::string name, uintptr_t z, uintptr_t W, uintptr_t b, uintptr_t out, int B, int K, int N,
                  int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_linear_fwd(P<const float>(z), P<const float>(W), P<const float>(b), P<bf16>(out), B, K, N, s);
+      return KF(dcg_linear_fwd)(P<const float>(z), P<const float>(W), P<const float>(b), P<elem_t>(out), B, K, N, s);
     });
   }
   int linear_wgrad(std::string name, uintptr_t z, uintptr_t dh, uintptr_t dW, uintptr_t db, int B, int K, int N,
                    int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_linear_wgrad(P<const float>(z), P<const bf16>(dh), P<float>(dW), P<float>(db), B, K, N, s);
+      return KF(dcg_linear_wgrad)(P<const float>(z), P<const elem_t>(dh), P<float>(dW), P<float>(db), B, K, N, s);
     });
   }
   int gemv_head(std::string name, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int R, int K, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_gemv_head(P<const bf16>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, s);
+      return KF(dcg_gemv_head)(P<const elem_t>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, s);
     });
   }
   int head_dgrad(std::string name, uintptr_t dl, uintptr_t w, uintptr_t dx, int R, int K, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_head_dgrad(P<const float>(dl), P<const float>(w), P<bf16>(dx), R, K, s);
+      return KF(dcg_head_dgrad)(P<const float>(dl), P<const float>(w), P<elem_t>(dx), R, K, s);
     });
   }
   int head_wgrad(std::string name, uintptr_t x, uintptr_t dl, uintptr_t part, int R, int K, int splits,
                  uintptr_t dW, uintptr_t db, int stream) {
     add(name, stream, [=](hipStream_t s) {
-      return dcg_head_wgrad(P<const bf16>(x), P<const float>(dl), P<float>(part), R, K, splits, s);
+      return KF(dcg_head_wgrad)(P<const elem_t>(x), P<const float>(dl), P<float>(part), R, K, splits, s);
     });
     add(name + ".reduce", stream, [=](hipStream_t s) {
-      return dcg_splitk_reduce(P<const float>(part), splits, (size_t)K, P<float>(dW), 1.f, s);
+      return KF(dcg_splitk_reduce)(P<const float>(part), splits, (size_t)K, P<float>(dW), 1.f, s);
     });
-    return add(name + ".bias", stream, [=](hipStream_t s) { return dcg_sum_vec(P<const float>(dl), R, P<float>(db), s); });
+    return add(name + ".bias", stream, [=](hipStream_t s) { return KF(dcg_sum_vec)(P<const float>(dl), R, P<float>(db), s); });
   }
   int adam(std::string name, uintptr_t w, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers, size_t n, float lr,
            float b1, float b2, float eps, float gscale, int stream) {
-    return adam_bf(name, w, 0, g, m, v, powers, n, lr, b1, b2, eps, gscale, stream);
+    return adam_bf(name, w, 0, g, m, v, powers, n, lr, b1, b2, eps, gscale, stream, 0);
   }
-  // + bf16 mirror of the updated weights (same flat layout)
+  // + elem_t mirror of the updated weights (same flat layout)
   int adam_bf(std::string name, uintptr_t w, uintptr_t wbf, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers,
-              size_t n, float lr, float b1, float b2, float eps, float gscale, int stream) {
+              size_t n, float lr, float b1, float b2, float eps, float gscale, int stream, uintptr_t ls) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_adam(P<float>(w), P<bf16>(wbf), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers),
-                      n, lr, b1, b2, eps, gscale, s);
+      return KF(dcg_adam)(P<float>(w), P<elem_t>(wbf), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers),
+                      n, lr, b1, b2, eps, gscale, P<const float>(ls), s);
     });
   }
+  // dynamic loss scaling: flag ls[1] if any gradient is non-finite
+  int nonfinite_check(std::string name, uintptr_t g, size_t n, uintptr_t ls, int stream) {
+    return add(name, stream, [=](hipStream_t s) { return KF(dcg_nonfinite_check)(P<const float>(g), n, P<float>(ls), s); });
+  }
   int step_end(std::string name, uintptr_t pd, uintptr_t pg, float b1d, float b2d, float b1g, float b2g,
-               uintptr_t step, int stream) {
+               uintptr_t step, int stream, uintptr_t ls, int growth_interval) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_step_end(P<float>(pd), P<float>(pg), b1d, b2d, b1g, b2g, P<unsigned long long>(step), s);
+      return KF(dcg_step_end)(P<float>(pd), P<float>(pg), b1d, b2d, b1g, b2g, P<unsigned long long>(step), P<float>(ls),
+                          growth_interval, s);
     });
   }
   int pack(std::string name, uintptr_t src, int T, int A, int Bd, uintptr_t nat, uintptr_t tr, int st, int sb, int sa,
            int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_pack(P<const float>(src), T, A, Bd, P<bf16>(nat), P<bf16>(tr), st, sb, sa, s);
+      return KF(dcg_pack)(P<const float>(src), T, A, Bd, P<elem_t>(nat), P<elem_t>(tr), st, sb, sa, s);
     });
   }
   int philox_uniform(std::string name, uintptr_t out, size_t n, uint64_t seed, uintptr_t step, uint64_t stream_id,
                      float lo, float hi, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_philox_uniform(P<float>(out), n, seed, P<const unsigned long long>(step), stream_id, lo, hi, s);
+      return KF(dcg_philox_uniform)(P<float>(out), n, seed, P<const unsigned long long>(step), stream_id, lo, hi, s);
     });
   }
   int im2col_s2(std::string name, uintptr_t src, uintptr_t dst, int Bn, int H, int W, int C, int Ho, int Wo, int pl_y,
                 int pl_x, int Kpad, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_im2col_s2(P<const bf16>(src), P<bf16>(dst), Bn, H, W, C, Ho, Wo, pl_y, pl_x, Kpad, s);
+      return KF(dcg_im2col_s2)(P<const elem_t>(src), P<elem_t>(dst), Bn, H, W, C, Ho, Wo, pl_y, pl_x, Kpad, s);
     });
   }
   int cast_to_bf16(std::string name, uintptr_t src, int src_dtype, uintptr_t dst, size_t n, float scale, float shift,
                    int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_cast_to_bf16(P<const void>(src), src_dtype, P<bf16>(dst), n, scale, shift, s);
+      return KF(dcg_cast_to_bf16)(P<const void>(src), src_dtype, P<elem_t>(dst), n, scale, shift, s);
     });
   }
   int cast_bf16_f32(std::string name, uintptr_t src, uintptr_t dst, size_t n, int stream) {
-    return add(name, stream, [=](hipStream_t s) { return dcg_cast_bf16_f32(P<const bf16>(src), P<float>(dst), n, s); });
+    return add(name, stream, [=](hipStream_t s) { return KF(dcg_cast_bf16_f32)(P<const elem_t>(src), P<float>(dst), n, s); });
   }
   int splitk_reduce(std::string name, uintptr_t src, int splits, size_t n, uintptr_t dst, float scale, int stream) {
     return add(name, stream, [=](hipStream_t s) {
-      return dcg_splitk_reduce(P<const float>(src), splits, n, P<float>(dst), scale, s);
+      return KF(dcg_splitk_reduce)(P<const float>(src), splits, n, P<float>(dst), scale, s);
     });
   }
 
@@ -397,6 +418,7 @@ class Program {
   std::vector<void*> dev_allocs_;
   std::vector<hipEvent_t> events_;
   int last_mtiles_ = 0, last_nphases_ = 0;
+  bool f16_ = false;  // element type of every activation / weight-mirror pointer: fp16, else bf16
 };
 
 static py::tuple igemm_tile(int cfg) {
@@ -430,7 +452,8 @@ PYBIND11_MODULE(_dcgan_hip, m) {
   m.def("device_arch", &device_arch);
   m.attr("built_for") = "gfx950";
   py::class_<Program>(m, "Program")
-      .def(py::init<>())
+      .def(py::init<bool>(), py::arg("f16") = false)
+      .def_property_readonly("f16", &Program::f16)
       .def("size", &Program::size)
       .def("name", &Program::name)
       .def("run", &Program::run, py::arg("streams"), py::arg("begin") = 0, py::arg("end") = -1)
@@ -453,15 +476,21 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("act_bwd", &Program::act_bwd)
       .def("sum_partials", &Program::sum_partials)
       .def("colsum_small", &Program::colsum_small)
-      .def("gan_loss", &Program::gan_loss)
+      .def("gan_loss", &Program::gan_loss, py::arg("name"), py::arg("logits"), py::arg("B"), py::arg("out"),
+           py::arg("dl_d"), py::arg("dl_g"), py::arg("prob"), py::arg("stream"), py::arg("ls") = 0)
       .def("linear_fwd", &Program::linear_fwd)
       .def("linear_wgrad", &Program::linear_wgrad)
       .def("gemv_head", &Program::gemv_head)
       .def("head_dgrad", &Program::head_dgrad)
       .def("head_wgrad", &Program::head_wgrad)
       .def("adam", &Program::adam)
-      .def("adam_bf", &Program::adam_bf)
-      .def("step_end", &Program::step_end)
+      .def("adam_bf", &Program::adam_bf, py::arg("name"), py::arg("w"), py::arg("wbf"), py::arg("g"), py::arg("m"),
+           py::arg("v"), py::arg("powers"), py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+           py::arg("gscale"), py::arg("stream"), py::arg("ls") = 0)
+      .def("step_end", &Program::step_end, py::arg("name"), py::arg("pd"), py::arg("pg"), py::arg("b1d"),
+           py::arg("b2d"), py::arg("b1g"), py::arg("b2g"), py::arg("step"), py::arg("stream"), py::arg("ls") = 0,
+           py::arg("growth_interval") = 2000)
+      .def("nonfinite_check", &Program::nonfinite_check)
       .def("pack", &Program::pack)
       .def("philox_uniform", &Program::philox_uniform)
       .def("im2col_s2", &Program::im2col_s2)

@@ -50,16 +50,18 @@ def _run(cmd):
 
 def build_hip(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
-    hdrs = [os.path.join(CSRC, "hip", h) for h in os.listdir(os.path.join(CSRC, "hip")) if h.endswith(".h")]
+    hdrs = [os.path.join(CSRC, "hip", h) for h in os.listdir(os.path.join(CSRC, "hip"))
+            if h.endswith((".h", ".inc"))]
     srcs = sorted(os.path.join(CSRC, "hip", f) for f in os.listdir(os.path.join(CSRC, "hip")) if f.endswith(".hip"))
     common = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC]
     jobs_list = []
     objs = []
-    for s in srcs:
-        o = os.path.join(BUILD, os.path.basename(s) + ".o")
-        objs.append(o)
-        if _newer([s] + hdrs, o):
-            jobs_list.append([HIPCC] + common + ["-c", s, "-o", o])
+    for s in srcs:  # every kernel file twice: bf16 element type, and fp16 (-DDCG_F16, *_f16 symbols)
+        for tag, defs in (("", []), (".f16", ["-DDCG_F16"])):
+            o = os.path.join(BUILD, os.path.basename(s) + tag + ".o")
+            objs.append(o)
+            if _newer([s] + hdrs, o):
+                jobs_list.append([HIPCC] + common + defs + ["-c", s, "-o", o])
     binding = os.path.join(CSRC, "bindings.cpp")
     bo = os.path.join(BUILD, "bindings.o")
     objs.append(bo)

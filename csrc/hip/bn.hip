@@ -1,13 +1,13 @@
 // BatchNorm (TF batch_norm_with_global_normalization semantics) and
-// activation kernels for gfx950, NHWC bf16 activations, fp32 statistics.
+// activation kernels for gfx950, NHWC elem_t activations, fp32 statistics.
 //
 // Forward:  conv epilogue (igemm) or colstats -> per-tile partial sum / sum^2
 //           -> bn_finalize (fp64 combine, biased variance, EMA update of the moving averages,
 //              scale = gamma*rsqrt(var+eps), shift = beta - mean*scale)
-//           -> bn_apply_act (y = act(x*scale + shift), 8 x bf16 per thread)
+//           -> bn_apply_act (y = act(x*scale + shift), 8 x elem_t per thread)
 // Backward: colstats mode 1 (partials of sum g and sum g*xhat, g = dy*act'(y))
 //           -> bn_bwd_finalize (d gamma, d beta into the flat fp32 gradient; per-group coefs)
-//           -> bn_bwd_apply (dx = A*g + Bx*x + Cc, bf16)
+//           -> bn_bwd_apply (dx = A*g + Bx*x + Cc, elem_t)
 // Every reduction is two-stage with fixed order -> bitwise deterministic, no float atomics.
 // "groups" split the rows into equal contiguous parts with independent statistics, which is
 // how D(real) and D(fake) run as one 2B batch with the reference's per-call BN statistics.
@@ -17,17 +17,17 @@
 
 namespace dcg {
 
-__device__ __forceinline__ void load8(const bf16* p, float* f) {
+__device__ __forceinline__ void load8(const elem_t* p, float* f) {
   const u32x4 v = *reinterpret_cast<const u32x4*>(p);
-  const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+  const elem8 b = __builtin_bit_cast(elem8, v);
 #pragma unroll
   for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
 }
 
-__device__ __forceinline__ void store8(bf16* p, const float* f) {
-  bf16x8 b;
+__device__ __forceinline__ void store8(elem_t* p, const float* f) {
+  elem8 b;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) b[i] = (bf16)f[i];
+  for (int i = 0; i < 8; ++i) b[i] = (elem_t)f[i];
   *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, b);
 }
 
@@ -44,8 +44,8 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
 // mode 2: (sum x, 0)                  -- plain column sums (bias gradients)
 // Block: 256 threads = (C/8) channel vectors x LANES row lanes; each block covers
 // rows_per_block rows and writes one partial row pair [2][C].
-__global__ __launch_bounds__(256) void colstats_kernel(int mode, const bf16* __restrict__ x,
-                                                       const bf16* __restrict__ dy, const bf16* __restrict__ y,
+__global__ __launch_bounds__(256) void colstats_kernel(int mode, const elem_t* __restrict__ x,
+                                                       const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
                                                        int act, float leak, int R, int C, int rows_per_block,
                                                        int rows_per_group, float* __restrict__ part) {
@@ -202,7 +202,7 @@ __global__ void bn_coef_eval_kernel(int C, const float* __restrict__ gamma, cons
 
 // ---------------------------------------------------------------- BN apply + activation
 // nv = R*C/8 vectors; vector v: row = v / C8, channel base = (v % C8) * 8, group = row / rpg
-__global__ __launch_bounds__(256) void bn_apply_act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+__global__ __launch_bounds__(256) void bn_apply_act_kernel(const elem_t* __restrict__ x, elem_t* __restrict__ y,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift, uint32_t nv, int C,
                                                            FastDiv fd_c8, FastDiv fd_rpg, int act, float leak) {
@@ -255,9 +255,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
-                                                           const bf16* __restrict__ x,
-                                                           const float* __restrict__ coef, bf16* __restrict__ dx,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
+                                                           const elem_t* __restrict__ x,
+                                                           const float* __restrict__ coef, elem_t* __restrict__ dx,
                                                            uint32_t nv, int C, FastDiv fd_c8, FastDiv fd_rpg, int act,
                                                            float leak) {
   for (uint32_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += gridDim.x * 256) {
@@ -279,8 +279,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
 
 // ---------------------------------------------------------------- activation backward (no BN)
 // dx = dy * act'(y); 8 per thread + scalar tail
-__global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
-                                                      bf16* __restrict__ dx, size_t n, int act, float leak) {
+__global__ __launch_bounds__(256) void act_bwd_kernel(const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
+                                                      elem_t* __restrict__ dx, size_t n, int act, float leak) {
   const size_t nv = n / 8;
   for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
     float dv[8], yv[8];
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ d
     store8(dx + v * 8, dv);
   }
   for (size_t i = nv * 8 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-    dx[i] = (bf16)((float)dy[i] * act_grad_from_out((float)y[i], act, leak));
+    dx[i] = (elem_t)((float)dy[i] * act_grad_from_out((float)y[i], act, leak));
 }
 
 // sum over partial rows -> dst[C]; grid ceil(C/16), block 256
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 }
 
 // column sums for a small channel count (C <= 16), e.g. dbias of a 3-channel image gradient
-__global__ __launch_bounds__(256) void colsum_small_kernel(const bf16* __restrict__ x, int R, int C,
+__global__ __launch_bounds__(256) void colsum_small_kernel(const elem_t* __restrict__ x, int R, int C,
                                                            float* __restrict__ part) {
   __shared__ float red[256][17];
   float s[16];
@@ -331,7 +331,7 @@ static inline unsigned ew_blocks(size_t nvec) {
   return (unsigned)(b ? b : 1);
 }
 
-extern "C" int dcg_colstats(int mode, const bf16* x, const bf16* dy, const bf16* y, const float* mean,
+extern "C" int DCG_API(dcg_colstats)(int mode, const elem_t* x, const elem_t* dy, const elem_t* y, const float* mean,
                             const float* rstd, int act, float leak, int R, int C, int rows_per_block,
                             int rows_per_group, float* part, hipStream_t s) {
   if (C % 8 || C > 2048) return -2;
@@ -343,7 +343,7 @@ extern "C" int dcg_colstats(int mode, const bf16* x, const bf16* dy, const bf16*
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_bn_finalize(const float* part, int ppg, int groups, int C, double count, const float* gamma,
+extern "C" int DCG_API(dcg_bn_finalize)(const float* part, int ppg, int groups, int C, double count, const float* gamma,
                                const float* beta, float eps, float* mean, float* rstd, float* scale, float* shift,
                                float* ema_mean, float* ema_var, float decay, hipStream_t s) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16, groups), dim3(256), 0, s, part, ppg, groups, C, count,
@@ -351,14 +351,14 @@ extern "C" int dcg_bn_finalize(const float* part, int ppg, int groups, int C, do
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_bn_coef_eval(int C, const float* gamma, const float* beta, float eps, const float* mean,
+extern "C" int DCG_API(dcg_bn_coef_eval)(int C, const float* gamma, const float* beta, float eps, const float* mean,
                                 const float* var, float debias, float* scale, float* shift, hipStream_t s) {
   hipLaunchKernelGGL(bn_coef_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, eps, mean, var,
                      debias, scale, shift);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_bn_apply_act(const bf16* x, bf16* y, const float* scale, const float* shift, int R, int C,
+extern "C" int DCG_API(dcg_bn_apply_act)(const elem_t* x, elem_t* y, const float* scale, const float* shift, int R, int C,
                                 int rows_per_group, int act, float leak, hipStream_t s) {
   if (C % 8) return -2;
   const size_t nv = (size_t)R * C / 8;
@@ -368,7 +368,7 @@ extern "C" int dcg_bn_apply_act(const bf16* x, bf16* y, const float* scale, cons
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_bn_bwd_finalize(const float* part, int ppg, int groups, int C, float count, const float* gamma,
+extern "C" int DCG_API(dcg_bn_bwd_finalize)(const float* part, int ppg, int groups, int C, float count, const float* gamma,
                                    const float* mean, const float* rstd, float* dgamma, float* dbeta, float* coef,
                                    hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, ppg, groups, C, count,
@@ -376,7 +376,7 @@ extern "C" int dcg_bn_bwd_finalize(const float* part, int ppg, int groups, int C
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_bn_bwd_apply(const bf16* dy, const bf16* y, const bf16* x, const float* coef, bf16* dx, int R,
+extern "C" int DCG_API(dcg_bn_bwd_apply)(const elem_t* dy, const elem_t* y, const elem_t* x, const float* coef, elem_t* dx, int R,
                                 int C, int rows_per_group, int act, float leak, hipStream_t s) {
   if (C % 8) return -2;
   const size_t nv = (size_t)R * C / 8;
@@ -386,17 +386,17 @@ extern "C" int dcg_bn_bwd_apply(const bf16* dy, const bf16* y, const bf16* x, co
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t n, int act, float leak, hipStream_t s) {
+extern "C" int DCG_API(dcg_act_bwd)(const elem_t* dy, const elem_t* y, elem_t* dx, size_t n, int act, float leak, hipStream_t s) {
   hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_blocks(n / 8 + 1)), dim3(256), 0, s, dy, y, dx, n, act, leak);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_sum_partials(const float* part, int P, int stride, int C, float* dst, hipStream_t s) {
+extern "C" int DCG_API(dcg_sum_partials)(const float* part, int P, int stride, int C, float* dst, hipStream_t s) {
   hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, P, stride, C, dst);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_colsum_small(const bf16* x, int R, int C, float* part, int blocks, hipStream_t s) {
+extern "C" int DCG_API(dcg_colsum_small)(const elem_t* x, int R, int C, float* part, int blocks, hipStream_t s) {
   if (C > 16) return -2;
   hipLaunchKernelGGL(colsum_small_kernel, dim3(blocks), dim3(256), 0, s, x, R, C, part);
   return (int)hipGetLastError();

@@ -1,5 +1,12 @@
 // Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels of this framework.
-// Wave = 64 lanes. bf16 MFMA fragments use the v_mfma_f32_16x16x32_bf16 lane maps:
+//
+// Element type: every kernel file is compiled TWICE by csrc/build.py -- once with elem_t =
+// bf16 (the default training dtype) and once with -DDCG_F16, elem_t = fp16 (the 256x256 fp16
+// config, with dynamic loss scaling in the engine). The fp16 build lives in namespace dcg_f16
+// and its C launchers carry a `_f16` suffix (DCG_API), so both coexist in one .so and the
+// Program picks one set per engine. MFMA: v_mfma_f32_16x16x32_{bf16,f16} (same lane maps,
+// same cycles).
+// Wave = 64 lanes. 16x16x32 MFMA fragment lane maps:
 //   A: lane l holds A[row l&15][k = 8*(l>>4) + j], j = 0..7
 //   B: lane l holds B[k = 8*(l>>4) + j][col l&15]
 //   C: lane l holds C[row 4*(l>>4) + r][col l&15], r = 0..3
@@ -7,10 +14,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef __bf16 bf16;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#ifdef DCG_F16
+typedef _Float16 elem_t;
+typedef _Float16 elem8 __attribute__((ext_vector_type(8)));
+typedef _Float16 elem4 __attribute__((ext_vector_type(4)));
+typedef _Float16 elem2 __attribute__((ext_vector_type(2)));
+#define DCG_MFMA_16x16x32 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#define DCG_API(name) name##_f16
+#define dcg dcg_f16
+#else
+typedef __bf16 elem_t;
+typedef __bf16 elem8 __attribute__((ext_vector_type(8)));
+typedef __bf16 elem4 __attribute__((ext_vector_type(4)));
+typedef __bf16 elem2 __attribute__((ext_vector_type(2)));
+#define DCG_MFMA_16x16x32 __builtin_amdgcn_mfma_f32_16x16x32_bf16
+#define DCG_API(name) name
+#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -22,8 +41,8 @@ namespace dcg {
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
 
-__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
-__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+__device__ __forceinline__ float bf2f(elem_t x) { return (float)x; }
+__device__ __forceinline__ elem_t f2bf(float x) { return (elem_t)x; }
 
 __device__ __forceinline__ float apply_act(float v, int act, float leak) {
   switch (act) {

@@ -1,4 +1,4 @@
-// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC, bf16 in / fp32 acc.
+// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC, elem_t in / fp32 acc.
 //
 // One kernel family covers every conv-shaped op of the DCGAN step:
 //   * TF-'SAME' stride-2 5x5 conv (D forward, G dgrad)          mode "conv":   25 taps, sstride 2
@@ -8,7 +8,7 @@
 //   * plain GEMM C[M][N] = A[M][K] . Bt[N][K]                    mode "plain" (im2col'd 3-channel
 //     layers, 1 tap).
 // GEMM view: rows m = output pixels of one phase, cols n = output channels, k = (tap, channel).
-// Weights are pre-packed bf16 [25][N][Kc] (k contiguous per output channel), so both operands
+// Weights are pre-packed elem_t [25][N][Kc] (k contiguous per output channel), so both operands
 // are "K-contiguous rows" and every fragment is one 16-byte ds_read_b128.
 //
 // Block = 256 threads (4 waves, WM x WN wave grid), tile BM x BN x 64, two LDS stages, one
@@ -23,10 +23,10 @@
 // 16x16x32 A/B fragment maps. A-operand gathers use buffer loads whose out-of-range offset
 // returns zeros, which implements the conv zero padding with no branches.
 //
-// Fused epilogue: + bias, per-channel BN partial statistics (sum, sum^2 of the stored bf16
+// Fused epilogue: + bias, per-channel BN partial statistics (sum, sum^2 of the stored elem_t
 // value over the tile's rows, per (M-tile, phase) for a deterministic finalize), activation
 // (relu / lrelu / tanh), pixel scatter of the phase, output staged through LDS and written as
-// 16-byte row segments (bf16, N % 8 == 0) or element-wise (fp32 / narrow N).
+// 16-byte row segments (elem_t, N % 8 == 0) or element-wise (fp32 / narrow N).
 #include "kernels.h"
 
 namespace dcg {
@@ -183,23 +183,23 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     const u32x4* sb = sa + BM * 8;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[FM], bfr[FN];
+      elem8 af[FM], bfr[FN];
       const int c = ks * 4 + fq;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * TM + i * 16 + fr;
-        af[i] = __builtin_bit_cast(bf16x8, sa[r * 8 + (c ^ (r & 7))]);
+        af[i] = __builtin_bit_cast(elem8, sa[r * 8 + (c ^ (r & 7))]);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * TN + j * 16 + fr;
-        bfr[j] = __builtin_bit_cast(bf16x8, sb[r * 8 + (c ^ (r & 7))]);
+        bfr[j] = __builtin_bit_cast(elem8, sb[r * 8 + (c ^ (r & 7))]);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = DCG_MFMA_16x16x32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < KT) store_tile(buf ^ 1);
     if constexpr (STAGING) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -207,11 +207,11 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   }
 
   // ------------------------------------------------------------------ epilogue
-  // LDS reuse: rowoff[BM] ints | red[WM][BN][2] floats | C tile [BM][BN + 8] bf16
+  // LDS reuse: rowoff[BM] ints | red[WM][BN][2] floats | C tile [BM][BN + 8] elem_t
   int* rowoff = reinterpret_cast<int*>(lds);
   float* red = reinterpret_cast<float*>(lds) + BM;
   constexpr int CPAD = BN + 8;
-  bf16* ctile = reinterpret_cast<bf16*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
+  elem_t* ctile = reinterpret_cast<elem_t*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
   static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= 2 * STAGE * 16, "epilogue LDS");
   for (int r = tid; r < BM; r += 256) {
     const int m = m0 + r;
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   __syncthreads();
 
   const bool do_stats = p.stats != nullptr;
-  // vector store path: bf16 output, whole 8-channel groups, aligned destination
+  // vector store path: elem_t output, whole 8-channel groups, aligned destination
   const bool vec = !p.out_f32 && (BN % 8 == 0) && (N % 8 == 0) && (p.ldc % 8 == 0) && (p.cofs % 8 == 0);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -249,9 +249,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
         const int ml = wm * TM + i * 16 + fq * 4 + r;
         const int off = rowoff[ml];
         const float v = acc[i][j][r] + bv;
-        const bf16 vb = f2bf(v);
+        const elem_t vb = f2bf(v);
         if (off >= 0 && nok) {
-          // statistics of exactly the stored (bf16-rounded) tensor, so BN forward/backward
+          // statistics of exactly the stored (elem_t-rounded) tensor, so BN forward/backward
           // see one consistent x
           const float vs = p.out_f32 ? v : (float)vb;
           s += vs;
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
           ctile[ml * CPAD + nl] = f2bf(o);
         } else if (off >= 0 && nok) {
           if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
-          else reinterpret_cast<bf16*>(p.C)[off + p.cofs + n] = f2bf(o);
+          else reinterpret_cast<elem_t*>(p.C)[off + p.cofs + n] = f2bf(o);
         }
       }
     }
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   if (do_stats || vec) __syncthreads();
   if (vec) {
     constexpr int CPR = BN / 8;  // 16-byte chunks per row
-    bf16* C = reinterpret_cast<bf16*>(p.C);
+    elem_t* C = reinterpret_cast<elem_t*>(p.C);
     for (int q = tid; q < BM * CPR; q += 256) {
       const int r = q / CPR, c = q - r * CPR;
       const int off = rowoff[r];
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   X(4, 32, 64, 2, 2) X(5, 64, 32, 2, 2) X(6, 32, 32, 2, 2) X(7, 128, 16, 4, 1) \
   X(8, 64, 16, 4, 1) X(9, 256, 64, 4, 1)
 
-extern "C" int dcg_igemm_tile(int cfg, int* bm, int* bn) {
+extern "C" int DCG_API(dcg_igemm_tile)(int cfg, int* bm, int* bn) {
   const int c = cfg % 100;
 #define X(id, BM_, BN_, WM_, WN_) if (c == id) { *bm = BM_; *bn = BN_; return 0; }
   DCG_IGEMM_CONFIGS(X)
@@ -324,7 +324,7 @@ extern "C" int dcg_igemm_tile(int cfg, int* bm, int* bn) {
   return -1;
 }
 
-extern "C" int dcg_igemm_launch(const dcg::IGemmArgs* a, int cfg, int mtiles, int ntiles, hipStream_t s) {
+extern "C" int DCG_API(dcg_igemm_launch)(const dcg::IGemmArgs* a, int cfg, int mtiles, int ntiles, hipStream_t s) {
   dim3 grid(mtiles, ntiles, a->nphases);
   const int c = cfg % 100;
   const bool glds = cfg >= 100;

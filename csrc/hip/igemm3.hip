@@ -2,7 +2,7 @@
 // deterministic split-K + either weight layout. Same conv/deconv/plain semantics and fused
 // epilogue as igemm.hip (read that header first); what changes is how the K loop is fed.
 //
-// Why: a 16x16x32 bf16 MFMA takes 16 cycles/SIMD and a ds_read_b128 costs 4 LDS cycles/CU
+// Why: a 16x16x32 elem_t MFMA takes 16 cycles/SIMD and a ds_read_b128 costs 4 LDS cycles/CU
 // (256 B/clk). With 4 waves of TMxTN wave tiles, LDS time / MFMA time = 16 (TM + TN) / (TM TN):
 // 1.0 for 32x32 wave tiles (igemm.hip's 64x64 blocks -> LDS-bound), 0.5 for 64x64. So the
 // main tiles here are 128x128 (2x2 waves), 256x64 (4x1) and 64x256 (1x4), all 64x64 per wave.
@@ -20,7 +20,7 @@
 //   BKN = 0: Bw[tap][N][Kc] (k contiguous) -> fragments via ds_read_b128, like igemm.hip;
 //   BKN = 1: Bw[tap][Kc][N] (n contiguous) -> the LDS tile is k-major and fragments are read
 //            with the gfx950 transposing read ds_read_b64_tr_b16 (as in wgrad.hip).
-// With both layouts available, every GEMM of the step reads the ONE bf16 mirror of the TF
+// With both layouts available, every GEMM of the step reads the ONE elem_t mirror of the TF
 // weight layout (HWIO conv / [kh,kw,out,in] deconv) that Adam writes: no repack kernels.
 //
 // Workgroup -> tile mapping is XCD-aware: workgroups are dispatched round-robin over the 8
@@ -213,12 +213,12 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[FM], bfr[FN];
+      elem8 af[FM], bfr[FN];
       const int c = ks * 4 + fq;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * TM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
+        af[i] = *reinterpret_cast<const elem8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
       }
       if constexpr (BKN) {
 #pragma unroll
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
             const int c8 = (wn * TN + j * 16) / 4 + p4;
             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 LDS_PTR(s16x4, sb + r * SB + ((c8 ^ kn_swz<SB>(r)) * 8)));
-            const bf16x4 vb = __builtin_bit_cast(bf16x4, v);
+            const elem4 vb = __builtin_bit_cast(elem4, v);
 #pragma unroll
             for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = vb[e];
           }
@@ -238,14 +238,14 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int r = wn * TN + j * 16 + fr;
-          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
+          bfr[j] = *reinterpret_cast<const elem8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
         }
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = DCG_MFMA_16x16x32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
 
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   int* rowoff = reinterpret_cast<int*>(lds);
   float* red = reinterpret_cast<float*>(lds) + BM;
   constexpr int CPAD = BN + 8;
-  bf16* ctile = reinterpret_cast<bf16*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
+  elem_t* ctile = reinterpret_cast<elem_t*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
   static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= NS * STAGE, "epilogue LDS");
   for (int r = tid; r < BM; r += 256) {
     const int m = m0 + r;
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
         const int ml = wm * TM + i * 16 + fq * 4 + r;
         const int off = rowoff[ml];
         const float v = acc[i][j][r] + bv;
-        const bf16 vb = f2bf(v);
+        const elem_t vb = f2bf(v);
         if (off >= 0 && nok) {
           const float vs = p.out_f32 ? v : (float)vb;
           s += vs;
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
           ctile[ml * CPAD + nl] = f2bf(o);
         } else if (off >= 0 && nok) {
           if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
-          else reinterpret_cast<bf16*>(p.C)[off + p.cofs + n] = f2bf(o);
+          else reinterpret_cast<elem_t*>(p.C)[off + p.cofs + n] = f2bf(o);
         }
       }
     }
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   if (do_stats || vec) __syncthreads();
   if (vec) {
     constexpr int CPR = BN / 8;
-    bf16* C = reinterpret_cast<bf16*>(p.C);
+    elem_t* C = reinterpret_cast<elem_t*>(p.C);
     for (int q = tid; q < BM * CPR; q += 256) {
       const int r = q / CPR, c = q - r * CPR;
       const int off = rowoff[r];
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   X(0, 128, 128, 2, 2) X(1, 256, 64, 4, 1) X(2, 64, 256, 1, 4) X(3, 128, 64, 2, 2) \
   X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2)
 
-extern "C" int dcg_igemm3_tile(int cfg, int* bm, int* bn, int* ns) {
+extern "C" int DCG_API(dcg_igemm3_tile)(int cfg, int* bm, int* bn, int* ns) {
   if (cfg < 200 || cfg >= 220) return -1;
   const int id = cfg % 10;
   *ns = cfg < 210 ? 3 : 2;
@@ -429,9 +429,9 @@ static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_igemm3_launch(const dcg::IGemmArgs* a, int cfg, int bkn, unsigned blocks, hipStream_t s) {
+extern "C" int DCG_API(dcg_igemm3_launch)(const dcg::IGemmArgs* a, int cfg, int bkn, unsigned blocks, hipStream_t s) {
   int bm, bn, ns;
-  if (dcg_igemm3_tile(cfg, &bm, &bn, &ns)) return -1;
+  if (DCG_API(dcg_igemm3_tile)(cfg, &bm, &bn, &ns)) return -1;
   const int id = cfg % 10;
 #define X(id_, BM_, BN_, WM_, WN_)                                              \
   if (id == id_) {                                                              \

@@ -3,7 +3,7 @@
 //   * linear layers: G projection z->h0 (K1), its weight gradient (K2), D's 1-output head
 //     (GEMV) and its gradients
 //   * TF-form Adam over a flat fp32 buffer + device-side beta powers (K17, graph-capturable)
-//   * bf16 weight packing (natural + per-tap transposed / im2col-ordered copies)
+//   * elem_t weight packing (natural + per-tap transposed / im2col-ordered copies)
 //   * Philox-4x32-10 z ~ U(-1,1) keyed by a device step counter (K19, graph-capturable)
 //   * stride-2 TF-SAME im2col for 3-channel tensors, dtype casts
 #include "kernels.h"
@@ -15,10 +15,13 @@ namespace dcg {
 // dl_d[2B] = d d_loss / d logit; dl_g[B] = d g_loss / d logit_fake; prob[2B] = sigmoid.
 __global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__ logits, int B,
                                                        float* __restrict__ out, float* __restrict__ dl_d,
-                                                       float* __restrict__ dl_g, float* __restrict__ prob) {
+                                                       float* __restrict__ dl_g, float* __restrict__ prob,
+                                                       const float* __restrict__ ls) {
   __shared__ float red[3][256];
   float lr = 0.f, lf = 0.f, lg = 0.f;
   const float invB = 1.f / (float)B;
+  // fp16 training: the gradient seeds carry the dynamic loss scale ls[0] (the losses do not)
+  const float gB = ls ? ls[0] * invB : invB;
   for (int i = threadIdx.x; i < 2 * B; i += 256) {
     const float x = logits[i];
     const float sp = log1pf(expf(-fabsf(x)));
@@ -26,12 +29,12 @@ __global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__
     if (prob) prob[i] = sg;
     if (i < B) {
       lr += fmaxf(x, 0.f) - x + sp;          // target 1
-      dl_d[i] = (sg - 1.f) * invB;
+      dl_d[i] = (sg - 1.f) * gB;
     } else {
       lf += fmaxf(x, 0.f) + sp;              // target 0
       lg += fmaxf(x, 0.f) - x + sp;          // target 1 (non-saturating G loss)
-      dl_d[i] = sg * invB;
-      dl_g[i - B] = (sg - 1.f) * invB;
+      dl_d[i] = sg * gB;
+      dl_g[i - B] = (sg - 1.f) * gB;
     }
   }
   red[0][threadIdx.x] = lr;
@@ -50,10 +53,10 @@ __global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------- linear: out = z @ W + b
-// z fp32 [B][K], W fp32 [K][N], out bf16 [B][N]; block = 256 columns x RB rows
+// z fp32 [B][K], W fp32 [K][N], out elem_t [B][N]; block = 256 columns x RB rows
 template <int RB>
 __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ z, const float* __restrict__ W,
-                                                         const float* __restrict__ bias, bf16* __restrict__ out,
+                                                         const float* __restrict__ bias, elem_t* __restrict__ out,
                                                          int B, int K, int N) {
   extern __shared__ float zs[];  // [RB][K]
   const int n = blockIdx.x * 256 + threadIdx.x;
@@ -86,12 +89,12 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
   const float b = bias ? bias[n] : 0.f;
 #pragma unroll
   for (int r = 0; r < RB; ++r)
-    if (r0 + r < B) out[(size_t)(r0 + r) * N + n] = (bf16)(acc[r] + b);
+    if (r0 + r < B) out[(size_t)(r0 + r) * N + n] = (elem_t)(acc[r] + b);
 }
 
 // dW[K][N] = z^T @ dh (fp32 out), db[N] = sum_b dh; block = 256 columns x KC k-rows
 template <int KC>
-__global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ z, const bf16* __restrict__ dh,
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ z, const elem_t* __restrict__ dh,
                                                            float* __restrict__ dW, float* __restrict__ db, int B,
                                                            int K, int N) {
   extern __shared__ float zs[];  // [B][KC]
@@ -119,8 +122,8 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
   if (db && blockIdx.y == 0) db[n] = sb;
 }
 
-// D head: logits[r] = sum_k x[r][k] * w[k] + b ; one wave per row, x bf16 [R][K], K % 512 == 0
-__global__ __launch_bounds__(256) void gemv_head_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+// D head: logits[r] = sum_k x[r][k] * w[k] + b ; one wave per row, x elem_t [R][K], K % 512 == 0
+__global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ b, float* __restrict__ out, int R,
                                                         int K) {
   const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256) void gemv_head_kernel(const bf16* __restrict__
   float s = 0.f;
   for (int k = lane * 8; k < K; k += 512) {
     const u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)wave * K + k);
-    const bf16x8 xb = __builtin_bit_cast(bf16x8, v);
+    const elem8 xb = __builtin_bit_cast(elem8, v);
     const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + k);
     const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + k + 4);
     s += (float)xb[0] * w0[0] + (float)xb[1] * w0[1] + (float)xb[2] * w0[2] + (float)xb[3] * w0[3] +
@@ -138,23 +141,23 @@ __global__ __launch_bounds__(256) void gemv_head_kernel(const bf16* __restrict__
   if (lane == 0) out[wave] = s + b[0];
 }
 
-// dx[r][k] = dl[r] * w[k] (bf16), 8 per thread
+// dx[r][k] = dl[r] * w[k] (elem_t), 8 per thread
 __global__ __launch_bounds__(256) void head_dgrad_kernel(const float* __restrict__ dl, const float* __restrict__ w,
-                                                         bf16* __restrict__ dx, int R, int K) {
+                                                         elem_t* __restrict__ dx, int R, int K) {
   const size_t nv = (size_t)R * K / 8;
   for (size_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (size_t)gridDim.x * 256) {
     const size_t e = v * 8;
     const int r = (int)(e / K), k = (int)(e - (size_t)r * K);
     const float g = dl[r];
-    bf16x8 o;
+    elem8 o;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (bf16)(g * w[k + i]);
+    for (int i = 0; i < 8; ++i) o[i] = (elem_t)(g * w[k + i]);
     *reinterpret_cast<u32x4*>(dx + e) = __builtin_bit_cast(u32x4, o);
   }
 }
 
 // head weight-grad partials: part[split][K] = sum_{r in split} x[r][k] * dl[r]
-__global__ __launch_bounds__(256) void head_wgrad_kernel(const bf16* __restrict__ x, const float* __restrict__ dl,
+__global__ __launch_bounds__(256) void head_wgrad_kernel(const elem_t* __restrict__ x, const float* __restrict__ dl,
                                                          float* __restrict__ part, int R, int K, int rows_per_split) {
   const int k8 = blockIdx.x * 256 + threadIdx.x;
   const int split = blockIdx.y;
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const bf16* __restrict_
   for (int r = r0; r < r1; ++r) {
     const float g = dl[r];
     const u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)r * K + k8 * 8);
-    const bf16x8 xb = __builtin_bit_cast(bf16x8, v);
+    const elem8 xb = __builtin_bit_cast(elem8, v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] += (float)xb[i] * g;
   }
@@ -190,11 +193,18 @@ __global__ void sum_vec_kernel(const float* __restrict__ v, int n, float* __rest
 
 // ---------------------------------------------------------------- TF Adam
 // lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from device powers (= b^t); w -= lr_t*m/(sqrt(v)+eps)
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* __restrict__ wbf,
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, elem_t* __restrict__ wbf,
                                                    const float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, const float* __restrict__ powers, size_t n,
-                                                   float lr, float b1, float b2, float eps, float gscale) {
-  // wbf (optional): bf16 mirror of the updated weights in the SAME flat layout -- the only
+                                                   float lr, float b1, float b2, float eps, float gscale,
+                                                   const float* __restrict__ ls) {
+  // dynamic loss scaling (fp16): ls = [scale, overflow flag, good steps]; an overflowed step
+  // is skipped entirely (weights, slots and the bf16/fp16 mirror untouched), else unscale
+  if (ls) {
+    if (ls[1] != 0.f) return;
+    gscale /= ls[0];
+  }
+  // wbf (optional): elem_t mirror of the updated weights in the SAME flat layout -- the only
   // weight copy the conv kernels read (they take either operand layout), so no repack pass
   const float lr_t = lr * sqrtf(1.f - powers[1]) / (1.f - powers[0]);
   const size_t n4 = n / 4;
@@ -211,8 +221,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* 
     reinterpret_cast<f32x4*>(v)[i] = vv;
     reinterpret_cast<f32x4*>(w)[i] = wv;
     if (wbf) {
-      bf16x4 o = {(bf16)wv[0], (bf16)wv[1], (bf16)wv[2], (bf16)wv[3]};
-      reinterpret_cast<bf16x4*>(wbf)[i] = o;
+      elem4 o = {(elem_t)wv[0], (elem_t)wv[1], (elem_t)wv[2], (elem_t)wv[3]};
+      reinterpret_cast<elem4*>(wbf)[i] = o;
     }
   }
   for (size_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
@@ -220,24 +230,52 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16* 
     m[i] = b1 * m[i] + (1.f - b1) * gv;
     v[i] = b2 * v[i] + (1.f - b2) * gv * gv;
     w[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps);
-    if (wbf) wbf[i] = (bf16)w[i];
+    if (wbf) wbf[i] = (elem_t)w[i];
   }
 }
 
 // after both Adams: beta powers *= beta (TF variable update) and the global step counter
 __global__ void step_end_kernel(float* __restrict__ pd, float* __restrict__ pg, float b1d, float b2d, float b1g,
-                                float b2g, unsigned long long* __restrict__ step) {
+                                float b2g, unsigned long long* __restrict__ step, float* __restrict__ ls,
+                                int growth_interval) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
-    if (pd) { pd[0] *= b1d; pd[1] *= b2d; }
-    if (pg) { pg[0] *= b1g; pg[1] *= b2g; }
+    bool skipped = false;
+    if (ls) {  // dynamic loss scale: halve on overflow, double after growth_interval good steps
+      skipped = ls[1] != 0.f;
+      if (skipped) {
+        ls[0] = fmaxf(ls[0] * 0.5f, 1.f);
+        ls[2] = 0.f;
+      } else if ((ls[2] += 1.f) >= (float)growth_interval) {
+        ls[0] = fminf(ls[0] * 2.f, 16777216.f);
+        ls[2] = 0.f;
+      }
+      ls[1] = 0.f;
+    }
+    if (!skipped) {  // a skipped step does not advance the Adam beta powers
+      if (pd) { pd[0] *= b1d; pd[1] *= b2d; }
+      if (pg) { pg[0] *= b1g; pg[1] *= b2g; }
+    }
     if (step) step[0] += 1ull;
   }
 }
 
+// overflow detection for dynamic loss scaling: any non-finite gradient sets ls[1]
+__global__ __launch_bounds__(256) void nonfinite_check_kernel(const float* __restrict__ g, size_t n,
+                                                              float* __restrict__ ls) {
+  bool bad = false;
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(g)[i];
+    bad |= !(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]));
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) bad |= !isfinite(g[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) ls[1] = 1.f;  // benign race: every writer stores 1
+}
+
 // ---------------------------------------------------------------- weight packing
-// src fp32 [T][A][Bd] -> nat bf16 (same order, optional) and tr bf16 at t*st + b*sb + a*sa
+// src fp32 [T][A][Bd] -> nat elem_t (same order, optional) and tr elem_t at t*st + b*sb + a*sa
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, uint32_t n, FastDiv fd_b,
-                                                   FastDiv fd_a, bf16* __restrict__ nat, bf16* __restrict__ tr,
+                                                   FastDiv fd_a, elem_t* __restrict__ nat, elem_t* __restrict__ tr,
                                                    int st, int sb, int sa) {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const float v = src[i];
@@ -245,8 +283,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
     const uint32_t b = i - ta * fd_b.d;
     const uint32_t t = fdiv(ta, fd_a);
     const uint32_t a = ta - t * fd_a.d;
-    if (nat) nat[i] = (bf16)v;
-    if (tr) tr[t * st + b * sb + a * sa] = (bf16)v;
+    if (nat) nat[i] = (elem_t)v;
+    if (tr) tr[t * st + b * sb + a * sa] = (elem_t)v;
   }
 }
 
@@ -286,8 +324,8 @@ __global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__
 }
 
 // ---------------------------------------------------------------- im2col (stride 2, TF SAME)
-// src bf16 [B][H][W][C] -> dst bf16 [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad
-__global__ __launch_bounds__(256) void im2col_s2_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int B,
+// src elem_t [B][H][W][C] -> dst elem_t [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad
+__global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict__ src, elem_t* __restrict__ dst, int B,
                                                         int H, int W, int C, int Ho, int Wo, int pl_y, int pl_x,
                                                         int Kpad) {
   const int kv = Kpad / 8;
@@ -298,7 +336,7 @@ __global__ __launch_bounds__(256) void im2col_s2_kernel(const bf16* __restrict__
     const int ox = (int)(row % Wo);
     const size_t t1 = row / Wo;
     const int oy = (int)(t1 % Ho), b = (int)(t1 / Ho);
-    bf16x8 o;
+    elem8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = v * 8 + j;
@@ -310,25 +348,25 @@ __global__ __launch_bounds__(256) void im2col_s2_kernel(const bf16* __restrict__
         if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
           val = (float)src[(((size_t)b * H + iy) * W + ix) * C + c];
       }
-      o[j] = (bf16)val;
+      o[j] = (elem_t)val;
     }
     *reinterpret_cast<u32x4*>(dst + row * Kpad + v * 8) = __builtin_bit_cast(u32x4, o);
   }
 }
 
 // ---------------------------------------------------------------- casts
-__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ s, bf16* __restrict__ d, size_t n) {
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (bf16)s[i];
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ s, elem_t* __restrict__ d, size_t n) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (elem_t)s[i];
 }
-__global__ __launch_bounds__(256) void cast_f64_bf16_kernel(const double* __restrict__ s, bf16* __restrict__ d, size_t n) {
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (bf16)(float)s[i];
+__global__ __launch_bounds__(256) void cast_f64_bf16_kernel(const double* __restrict__ s, elem_t* __restrict__ d, size_t n) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (elem_t)(float)s[i];
 }
-__global__ __launch_bounds__(256) void cast_u8_bf16_kernel(const uint8_t* __restrict__ s, bf16* __restrict__ d, size_t n,
+__global__ __launch_bounds__(256) void cast_u8_bf16_kernel(const uint8_t* __restrict__ s, elem_t* __restrict__ d, size_t n,
                                                            float scale, float shift) {
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-    d[i] = (bf16)((float)s[i] * scale + shift);
+    d[i] = (elem_t)((float)s[i] * scale + shift);
 }
-__global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const bf16* __restrict__ s, float* __restrict__ d, size_t n) {
+__global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const elem_t* __restrict__ s, float* __restrict__ d, size_t n) {
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (float)s[i];
 }
 
@@ -342,13 +380,13 @@ static inline unsigned grid_for(size_t n, size_t per = 256) {
   return (unsigned)(b ? b : 1);
 }
 
-extern "C" int dcg_gan_loss(const float* logits, int B, float* out, float* dl_d, float* dl_g, float* prob,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(gan_loss_kernel, dim3(1), dim3(256), 0, s, logits, B, out, dl_d, dl_g, prob);
+extern "C" int DCG_API(dcg_gan_loss)(const float* logits, int B, float* out, float* dl_d, float* dl_g, float* prob,
+                                      const float* ls, hipStream_t s) {
+  hipLaunchKernelGGL(gan_loss_kernel, dim3(1), dim3(256), 0, s, logits, B, out, dl_d, dl_g, prob, ls);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_linear_fwd(const float* z, const float* W, const float* b, bf16* out, int B, int K, int N,
+extern "C" int DCG_API(dcg_linear_fwd)(const float* z, const float* W, const float* b, elem_t* out, int B, int K, int N,
                               hipStream_t s) {
   constexpr int RB = 8;  // (N/256) x (B/8) = 512 blocks for the 64x64 model at B=128
   dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
@@ -356,7 +394,7 @@ extern "C" int dcg_linear_fwd(const float* z, const float* W, const float* b, bf
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_linear_wgrad(const float* z, const bf16* dh, float* dW, float* db, int B, int K, int N,
+extern "C" int DCG_API(dcg_linear_wgrad)(const float* z, const elem_t* dh, float* dW, float* db, int B, int K, int N,
                                 hipStream_t s) {
   constexpr int KC = 4;  // 4 k-rows per block: (N/256) x (K/4) = 800 blocks for the 64x64 model
   if ((size_t)B * KC * sizeof(float) > 65536) return -2;
@@ -365,19 +403,19 @@ extern "C" int dcg_linear_wgrad(const float* z, const bf16* dh, float* dW, float
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_gemv_head(const bf16* x, const float* w, const float* b, float* out, int R, int K, hipStream_t s) {
+extern "C" int DCG_API(dcg_gemv_head)(const elem_t* x, const float* w, const float* b, float* out, int R, int K, hipStream_t s) {
   if (K % 512) return -2;
   hipLaunchKernelGGL(gemv_head_kernel, dim3((R + 3) / 4), dim3(256), 0, s, x, w, b, out, R, K);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_head_dgrad(const float* dl, const float* w, bf16* dx, int R, int K, hipStream_t s) {
+extern "C" int DCG_API(dcg_head_dgrad)(const float* dl, const float* w, elem_t* dx, int R, int K, hipStream_t s) {
   if (K % 8) return -2;
   hipLaunchKernelGGL(head_dgrad_kernel, dim3(grid_for((size_t)R * K / 8)), dim3(256), 0, s, dl, w, dx, R, K);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_head_wgrad(const bf16* x, const float* dl, float* part, int R, int K, int splits,
+extern "C" int DCG_API(dcg_head_wgrad)(const elem_t* x, const float* dl, float* part, int R, int K, int splits,
                               hipStream_t s) {
   if (K % 8) return -2;
   const int rps = (R + splits - 1) / splits;
@@ -386,25 +424,32 @@ extern "C" int dcg_head_wgrad(const bf16* x, const float* dl, float* part, int R
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_sum_vec(const float* v, int n, float* out, hipStream_t s) {
+extern "C" int DCG_API(dcg_sum_vec)(const float* v, int n, float* out, hipStream_t s) {
   hipLaunchKernelGGL(sum_vec_kernel, dim3(1), dim3(256), 0, s, v, n, out);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_adam(float* w, bf16* wbf, const float* g, float* m, float* v, const float* powers, size_t n,
-                        float lr, float b1, float b2, float eps, float gscale, hipStream_t s) {
+extern "C" int DCG_API(dcg_adam)(float* w, elem_t* wbf, const float* g, float* m, float* v, const float* powers,
+                                  size_t n, float lr, float b1, float b2, float eps, float gscale, const float* ls,
+                                  hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, wbf, g, m, v, powers, n, lr, b1, b2,
-                     eps, gscale);
+                     eps, gscale, ls);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_step_end(float* pd, float* pg, float b1d, float b2d, float b1g, float b2g,
-                            unsigned long long* step, hipStream_t s) {
-  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(64), 0, s, pd, pg, b1d, b2d, b1g, b2g, step);
+extern "C" int DCG_API(dcg_step_end)(float* pd, float* pg, float b1d, float b2d, float b1g, float b2g,
+                                      unsigned long long* step, float* ls, int growth_interval, hipStream_t s) {
+  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(64), 0, s, pd, pg, b1d, b2d, b1g, b2g, step, ls,
+                     growth_interval);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_pack(const float* src, int T, int A, int Bd, bf16* nat, bf16* tr, int st, int sb, int sa,
+extern "C" int DCG_API(dcg_nonfinite_check)(const float* g, size_t n, float* ls, hipStream_t s) {
+  hipLaunchKernelGGL(nonfinite_check_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, g, n, ls);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_pack)(const float* src, int T, int A, int Bd, elem_t* nat, elem_t* tr, int st, int sb, int sa,
                         hipStream_t s) {
   const size_t n = (size_t)T * A * Bd;
   if (n >= 0x80000000ull) return -3;
@@ -413,14 +458,14 @@ extern "C" int dcg_pack(const float* src, int T, int A, int Bd, bf16* nat, bf16*
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_philox_uniform(float* out, size_t n, uint64_t seed, const unsigned long long* step,
+extern "C" int DCG_API(dcg_philox_uniform)(float* out, size_t n, uint64_t seed, const unsigned long long* step,
                                   uint64_t stream_id, float lo, float hi, hipStream_t s) {
   hipLaunchKernelGGL(philox_uniform_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, out, n, seed, step,
                      stream_id, lo, hi);
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_im2col_s2(const bf16* src, bf16* dst, int B, int H, int W, int C, int Ho, int Wo, int pl_y,
+extern "C" int DCG_API(dcg_im2col_s2)(const elem_t* src, elem_t* dst, int B, int H, int W, int C, int Ho, int Wo, int pl_y,
                              int pl_x, int Kpad, hipStream_t s) {
   if (Kpad % 8) return -2;
   hipLaunchKernelGGL(im2col_s2_kernel, dim3(grid_for((size_t)B * Ho * Wo * (Kpad / 8))), dim3(256), 0, s, src, dst,
@@ -428,7 +473,7 @@ extern "C" int dcg_im2col_s2(const bf16* src, bf16* dst, int B, int H, int W, in
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_cast_to_bf16(const void* src, int src_dtype, bf16* dst, size_t n, float scale, float shift,
+extern "C" int DCG_API(dcg_cast_to_bf16)(const void* src, int src_dtype, elem_t* dst, size_t n, float scale, float shift,
                                 hipStream_t s) {
   // src_dtype: 0 f32, 1 f64, 2 u8 (x*scale+shift)
   if (src_dtype == 0)
@@ -443,7 +488,7 @@ extern "C" int dcg_cast_to_bf16(const void* src, int src_dtype, bf16* dst, size_
   return (int)hipGetLastError();
 }
 
-extern "C" int dcg_cast_bf16_f32(const bf16* src, float* dst, size_t n, hipStream_t s) {
+extern "C" int DCG_API(dcg_cast_bf16_f32)(const elem_t* src, float* dst, size_t n, hipStream_t s) {
   hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n);
   return (int)hipGetLastError();
 }

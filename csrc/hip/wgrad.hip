@@ -1,5 +1,5 @@
 // Weight-gradient ("wgrad") for the TF-'SAME' stride-2 5x5 conv and
-// conv_transpose on CDNA4 MFMA, NHWC, bf16 in / fp32 out.
+// conv_transpose on CDNA4 MFMA, NHWC, elem_t in / fp32 out.
 //
 // Both cases have the same form (G = the operand read at stride-2 shifted pixels, Dm = the
 // operand read at its own pixels, k = pixels of Dm):
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     const char* sd = sg + BK * SG;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[FM], bfr[FN];
+      elem8 af[FM], bfr[FN];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r = ks * 32 + 8 * g4 + 4 * h + q4;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
           const int c8 = (wm * TM + i * 16) / 4 + p4;
           const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               LDS_PTR(s16x4, sg + r * SG + ((c8 ^ wg_swz<SG>(r)) * 8)));
-          const bf16x4 vb = __builtin_bit_cast(bf16x4, v);
+          const elem4 vb = __builtin_bit_cast(elem4, v);
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][4 * h + e] = vb[e];
         }
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
           const int c8 = (wn * TN + j * 16) / 4 + p4;
           const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               LDS_PTR(s16x4, sd + r * SD + ((c8 ^ wg_swz<SD>(r)) * 8)));
-          const bf16x4 vb = __builtin_bit_cast(bf16x4, v);
+          const elem4 vb = __builtin_bit_cast(elem4, v);
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = vb[e];
         }
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = DCG_MFMA_16x16x32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < kt1) store_tile(buf ^ 1);
     __syncthreads();
@@ -211,16 +211,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* src, in
 #define DCG_WGRAD_CONFIGS(X) \
   X(0, 128, 128) X(1, 64, 128) X(2, 128, 64) X(3, 64, 64) X(4, 32, 64) X(5, 64, 32) X(6, 32, 32)
 
-extern "C" int dcg_wgrad_tile(int cfg, int* bm, int* bn) {
+extern "C" int DCG_API(dcg_wgrad_tile)(int cfg, int* bm, int* bn) {
 #define X(id, BM_, BN_) if (cfg == id) { *bm = BM_; *bn = BN_; return 0; }
   DCG_WGRAD_CONFIGS(X)
 #undef X
   return -1;
 }
 
-extern "C" int dcg_wgrad_launch(const dcg::WGradArgs* a, int cfg, int splits, hipStream_t s) {
+extern "C" int DCG_API(dcg_wgrad_launch)(const dcg::WGradArgs* a, int cfg, int splits, hipStream_t s) {
   int bm = 0, bn = 0;
-  if (dcg_wgrad_tile(cfg, &bm, &bn)) return -1;
+  if (DCG_API(dcg_wgrad_tile)(cfg, &bm, &bn)) return -1;
   const int ntm = (a->Mc + bm - 1) / bm, ntn = (a->Nc + bn - 1) / bn;
   dim3 grid(ntm * ntn, a->ntaps, splits);
 #define X(id, BM_, BN_) \
@@ -231,7 +231,7 @@ extern "C" int dcg_wgrad_launch(const dcg::WGradArgs* a, int cfg, int splits, hi
   return -1;
 }
 
-extern "C" int dcg_splitk_reduce(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s) {
+extern "C" int DCG_API(dcg_splitk_reduce)(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s) {
   const size_t n4 = n / 4;
   if (splits >= 64) {
     hipLaunchKernelGGL(dcg::splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16 + 1)), dim3(256), 0, s, src,

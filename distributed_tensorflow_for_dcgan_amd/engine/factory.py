@@ -117,7 +117,7 @@ def build_engine(cfg: DCGANConfig, batch_size: int, device: torch.device, engine
                  allreduce_dtype: str = "fp32", lr: float = 2e-4, beta1: float = 0.5,
                  zero_debias: bool = False, bucket_mb: float = 8.0):
     if engine == "auto":
-        engine = "hip" if device.type == "cuda" else "reference"
+        engine = "hip" if device.type == "cuda" and dtype in ("bf16", "fp16") else "reference"
     if engine == "reference":
         return ReferenceEngine(cfg, batch_size, device, seed=seed, lr=lr, beta1=beta1,
                                zero_debias=zero_debias, rank=rank, world=world)

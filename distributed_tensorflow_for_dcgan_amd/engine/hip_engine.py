@@ -47,13 +47,19 @@ def _kpad(c: int) -> int:
 class HipEngine:
     name = "hip"
     dtype_name = "bf16"
+    INIT_LOSS_SCALE = 32768.0   # fp16 dynamic loss scaling (TF/Keras LossScaleOptimizer defaults)
+    LOSS_SCALE_GROWTH = 2000
 
     def __init__(self, cfg: DCGANConfig, batch_size: int, device: torch.device, dtype: str = "bf16",
                  seed: int = 0, lr: float = 2e-4, beta1: float = 0.5, zero_debias: bool = False, rank: int = 0,
                  world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 8.0,
                  rank_seeded_z: bool = True, **_):
-        if dtype != "bf16":
-            raise ValueError("the HIP engine computes in bf16 (fp32 master weights / statistics)")
+        if dtype not in ("bf16", "fp16"):
+            raise ValueError("the HIP engine computes in bf16 or fp16 (fp32 master weights / statistics / "
+                             "accumulation); fp32 runs on --engine=reference")
+        self.dtype_name = dtype
+        self.f16 = dtype == "fp16"
+        self.edt = torch.float16 if self.f16 else torch.bfloat16
         if device.type != "cuda":
             raise ValueError("HipEngine needs a GPU")
         self.ext = H.ext()
@@ -86,7 +92,8 @@ class HipEngine:
         self._repack_weights_now()
 
     # ------------------------------------------------------------------ buffers
-    def _t(self, *shape, dtype=torch.bfloat16, zero=False):
+    def _t(self, *shape, dtype=None, zero=False):
+        dtype = self.edt if dtype is None else dtype
         f = torch.zeros if zero else torch.empty
         return f(*shape, dtype=dtype, device=self.device)
 
@@ -153,8 +160,12 @@ class HipEngine:
         # ---------------- bf16 weight mirrors: the SAME flat layout as the fp32 masters (TF layouts:
         # HWIO conv, [kh,kw,out,in] deconv), written by the Adam kernel; every conv GEMM reads
         # its weight from here in whichever orientation it needs (igemm3 bkn flag)
-        self.wbf_d = self.model.d.like(torch.bfloat16)
-        self.wbf_g = self.model.g.like(torch.bfloat16)
+        self.wbf_d = self.model.d.like(self.edt)
+        self.wbf_g = self.model.g.like(self.edt)
+        # fp16: dynamic loss scale state [scale, overflow flag, good steps] (device-resident, so
+        # the whole step incl. skip / halve / grow stays inside the captured graphs)
+        self.loss_scale = (torch.tensor([self.INIT_LOSS_SCALE, 0.0, 0.0], dtype=torch.float32, device=self.device)
+                           if self.f16 else None)
 
     # ------------------------------------------------------------------ program build
     def _stats_buf(self, key, P, C):
@@ -165,16 +176,16 @@ class HipEngine:
     def _build(self):
         ext = self.ext
         self._keep: List[torch.Tensor] = []
-        self.progA = ext.Program()
-        self.progB = ext.Program()
-        self.progC = ext.Program()
+        self.progA = ext.Program(self.f16)
+        self.progB = ext.Program(self.f16)
+        self.progC = ext.Program(self.f16)
         self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
         self._build_d_backward_dloss(self.progA)
         self._build_gloss_and_g_backward(self.progB)
         self._build_update(self.progC, "d")
         self._c_split = self.progC.size()
         self._build_update(self.progC, "g")
-        self.progCast = ext.Program()  # fp32 masters -> bf16 mirrors (init / checkpoint load)
+        self.progCast = ext.Program(self.f16)  # fp32 masters -> bf16/fp16 mirrors (init / checkpoint load)
         for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
             self.progCast.cast_to_bf16("mirror", _p(ps.flat), 0, _p(pb.flat), ps.flat.numel(), 1.0, 0.0, 0)
         self.progS = None  # sampler program, built lazily
@@ -299,7 +310,8 @@ class HipEngine:
         lin = cfg.d_lin_name
         prog.gemv_head("d_head", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits), B2,
                        cfg.d_lin_in, 0)
-        prog.gan_loss("loss", _p(self.logits), B, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob), 0)
+        prog.gan_loss("loss", _p(self.logits), B, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob), 0,
+                      _p(self.loss_scale))
 
     # ---- D backward for d_loss (2B rows, both groups) -> all D gradients
     def _build_d_backward_dloss(self, prog):
@@ -452,20 +464,29 @@ class HipEngine:
 
     # ---- optimiser (+ bf16 weight mirrors)
     def _build_update(self, prog, which="dg"):
-        """TF-Adam for D and/or G; each Adam also writes the bf16 mirror the conv GEMMs read.
-        The D half comes first so that under DDP it overlaps with the G-gradient all-reduce."""
+        """TF-Adam for D and/or G; each Adam also writes the bf16/fp16 mirror the conv GEMMs
+        read. bf16: the D half comes first so that under DDP it overlaps with the G-gradient
+        all-reduce. fp16: one overflow check over both (all-reduced) gradients gates both
+        Adams, so everything runs in the G half (after the last all-reduce)."""
         gs = 1.0 / self.world
         od, og = self.opt_d, self.opt_g
+        ls = _p(self.loss_scale)
+        if self.f16:
+            if "g" not in which:
+                return
+            prog.nonfinite_check("ls.check_d", _p(self.grad_d.flat), self.grad_d.flat.numel(), ls, 0)
+            prog.nonfinite_check("ls.check_g", _p(self.grad_g.flat), self.grad_g.flat.numel(), ls, 0)
+            which = "dg"
         if "d" in which:
             prog.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
                          _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
-                         gs, 0)
+                         gs, 0, ls)
         if "g" in which:
             prog.adam_bf("adam_g", _p(self.model.g.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
                          _p(og.v.flat), _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
-                         gs, 0)
+                         gs, 0, ls)
             prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
-                          _p(self.step_counter), 0)
+                          _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
 
     def _repack_weights_now(self):
         H.run(self.progCast)
@@ -503,7 +524,8 @@ class HipEngine:
 
     def _run_segment(self, i, st):
         if self.graph_enabled:
-            self._graphs[i].replay()
+            if self._graphs[i] is not None:
+                self._graphs[i].replay()
         else:
             for prog, b, e in self._segments()[i]:
                 H.run(prog, st, b, e)
@@ -549,6 +571,9 @@ class HipEngine:
             torch.cuda.synchronize(self.device)
             graphs = []
             for seg in self._segments():
+                if all((p.size() if e < 0 else e) <= b for p, b, e in seg):
+                    graphs.append(None)  # empty segment (fp16: no separate D update)
+                    continue
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     cs = torch.cuda.current_stream(self.device)
@@ -625,7 +650,7 @@ class HipEngine:
 
     def _build_sampler(self):
         cfg, B = self.cfg, self.B
-        prog = self.ext.Program()
+        prog = self.ext.Program(self.f16)
         Pg = self.model.g
         t = self._t
         self._s_bufs = {}
@@ -670,7 +695,7 @@ class HipEngine:
         """Sample-time d_loss / g_loss (image_train.py:181-184) in train-mode BN but WITHOUT
         mutating the moving averages (documented deviation)."""
         if self.progEval is None:
-            prog = self.ext.Program()
+            prog = self.ext.Program(self.f16)
             self._ev_z = self._t(self.B, self.cfg.z_dim, dtype=torch.float32)
             self._build_forward(prog, update_ema=False, z=self._ev_z, train_z=False)
             self.progEval = prog

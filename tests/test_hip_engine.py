@@ -32,9 +32,9 @@ def d64(t):
     return t.detach().double()
 
 
-def w64(t):
-    """weights as the kernels see them (bf16-packed)"""
-    return t.detach().to(torch.bfloat16).double()
+def w64(t, edt=torch.bfloat16):
+    """weights as the kernels see them (the bf16 / fp16 mirror)"""
+    return t.detach().to(edt).double()
 
 
 def bn_act_bwd64(x, dy, gamma, beta, act, groups=1):
@@ -52,10 +52,10 @@ def bn_act_bwd64(x, dy, gamma, beta, act, groups=1):
     return gx, (dyg * xhat).sum(0), dyg.sum(0)
 
 
-def conv_grads64(x, w, dy, kind, out_hw=None):
+def conv_grads64(x, w, dy, kind, out_hw=None, edt=torch.bfloat16):
     """(dx, dw) of a TF-SAME conv (kind 'conv', HWIO w) or conv_transpose ('deconv')."""
     xv = d64(x).clone().requires_grad_(True)
-    wv = w64(w).clone().requires_grad_(True)
+    wv = w64(w, edt).clone().requires_grad_(True)
     if kind == "conv":
         y = R.conv2d_same(xv, wv)
     else:
@@ -63,13 +63,17 @@ def conv_grads64(x, w, dy, kind, out_hw=None):
     return torch.autograd.grad(y, [xv, wv], d64(dy))
 
 
-@pytest.mark.parametrize("size,c_dim,B", [(64, 3, 16), (28, 1, 8), (128, 3, 4), (256, 3, 4)])
-def test_engine_stagewise(size, c_dim, B):
+@pytest.mark.parametrize("size,c_dim,B,dtype", [(64, 3, 16, "bf16"), (28, 1, 8, "bf16"), (128, 3, 4, "bf16"),
+                                                (256, 3, 4, "bf16"), (64, 3, 16, "fp16"), (256, 3, 4, "fp16")])
+def test_engine_stagewise(size, c_dim, B, dtype):
+    """fp16 runs with the dynamic loss scale in the gradient seeds: every stage is compared
+    against a recomputation from the engine's own (scaled) inputs, so the scale cancels."""
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     from distributed_tensorflow_for_dcgan_amd.ops import hip as H
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig(output_size=size, c_dim=c_dim)
-    eng = HipEngine(cfg, B, dev, graph=False, seed=3)
+    eng = HipEngine(cfg, B, dev, graph=False, seed=3, dtype=dtype)
+    edt = eng.edt
     real = (torch.rand(B, size, size, c_dim, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     eng.set_batch(real)
     st = [torch.cuda.current_stream()]
@@ -93,7 +97,7 @@ def test_engine_stagewise(size, c_dim, B):
             rep["d %s dgamma" % L.bn] = rel(gD[L.bn + "/gamma"], dgam)
             rep["d %s dbeta" % L.bn] = rel(gD[L.bn + "/beta"], dbet)
         src = eng.d_in if i == 0 else eng.d_a[dl[i - 1].name]
-        gx, gw = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name], "conv")
+        gx, gw = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name], "conv", edt=edt)
         rep["d %s dW" % L.name] = rel(gD[L.name + "/w"], gw)
         if i > 0:
             rep["d %s dgrad" % L.name] = rel(eng.d_da[dl[i - 1].name], gx)
@@ -107,7 +111,7 @@ def test_engine_stagewise(size, c_dim, B):
                                     Pd[L.bn + "/beta"], "lrelu")
             rep["g %s bn dx" % L.name] = rel(eng.d_dx[L.name][B:], gx)
         src = eng.d_in[B:] if i == 0 else eng.d_a[dl[i - 1].name][B:]
-        gx, _ = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name][B:], "conv")
+        gx, _ = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name][B:], "conv", edt=edt)
         rep["g %s dgrad" % L.name] = rel(eng.img_grad if i == 0 else eng.d_da[dl[i - 1].name][B:], gx)
     fake = d64(eng.fake)
     img_g = d64(eng.img_grad) * (1 - fake * fake)
@@ -123,7 +127,7 @@ def test_engine_stagewise(size, c_dim, B):
             rep["G %s dgamma" % L.bn] = rel(gG[L.bn + "/gamma"], dgam)
             rep["G %s dbeta" % L.bn] = rel(gG[L.bn + "/beta"], dbet)
         Bx = src.reshape(B, L.in_hw, L.in_hw, L.cin)
-        gx, gw = conv_grads64(Bx, Pg[L.name + "/w"], dy, "deconv", (L.out_hw, L.out_hw))
+        gx, gw = conv_grads64(Bx, Pg[L.name + "/w"], dy, "deconv", (L.out_hw, L.out_hw), edt=edt)
         rep["G %s dW" % L.name] = rel(gG[L.name + "/w"], gw)
         dsrc = eng.g_da[gl[j - 1].name] if j > 0 else eng.g_da0
         rep["G %s dgrad" % L.name] = rel(dsrc.reshape(gx.shape), gx)
@@ -134,7 +138,7 @@ def test_engine_stagewise(size, c_dim, B):
     rep["G bn0 dx"] = rel(eng.g_dx0.reshape(gx.shape), gx)
     rep["G lin dW"] = rel(gG["g_h0_lin/Matrix"], d64(eng.z).t() @ d64(eng.g_dx0))
     rep["G lin db"] = rel(gG["g_h0_lin/bias"], d64(eng.g_dx0).sum(0))
-    print("\nstagewise relative errors (%dx%dx%d, B=%d):" % (size, size, c_dim, B))
+    print("\nstagewise relative errors (%dx%dx%d, B=%d, %s):" % (size, size, c_dim, B, dtype))
     for k, v in rep.items():
         print("  %-28s %.5f" % (k, v))
     # BN-backward stages see derivative-mask flips of near-zero bf16 pre-activations -> 3 %
@@ -251,3 +255,59 @@ def test_engine_sampler_and_eval():
     ev = eng.eval_losses(real, z)
     assert torch.equal(before, eng.model.d_bn.flat)  # no EMA mutation
     assert ev["d_loss"] == ev["d_loss"]
+
+
+def test_engine_fp16_loss_scaling():
+    """fp16 engine: a good step keeps the scale and counts it; an overflowing step (scale forced
+    to 1e38 -> inf gradients) is skipped -- weights, Adam slots, beta powers untouched -- and
+    halves the scale; the step after trains again. Graph replay included."""
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    dev = torch.device("cuda", 0)
+    cfg = DCGANConfig()
+    eng = HipEngine(cfg, 16, dev, seed=1, dtype="fp16")
+    real = (torch.rand(16, 64, 64, 3, generator=torch.Generator().manual_seed(2)) * 2 - 1).to(dev)
+    eng.set_batch(real)
+    eng.train_step()
+    eng.train_step()  # second step replays the captured graphs
+    torch.cuda.synchronize()
+    ls = eng.loss_scale.tolist()
+    assert ls[0] == HipEngine.INIT_LOSS_SCALE and ls[1] == 0.0 and ls[2] == 2.0, ls
+    assert all(torch.isfinite(torch.tensor(list(eng.last_losses().values()))))
+    w0, m0 = eng.model.g.flat.clone(), eng.opt_g.m.flat.clone()
+    p0 = eng.opt_d.powers.clone()
+    eng.loss_scale[0] = 1e38
+    eng.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(eng.model.g.flat, w0) and torch.equal(eng.opt_g.m.flat, m0)
+    assert torch.equal(eng.opt_d.powers, p0)
+    ls = eng.loss_scale.tolist()
+    assert ls[0] == float(torch.tensor(1e38) * 0.5) and ls[1] == 0.0 and ls[2] == 0.0, ls
+    eng.loss_scale[0] = 1024.0
+    eng.train_step()
+    torch.cuda.synchronize()
+    assert not torch.equal(eng.model.g.flat, w0)
+    assert eng.global_step == 4
+
+
+def test_engine_fp16_step_matches_reference():
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    dev = torch.device("cuda", 0)
+    cfg = DCGANConfig()
+    B = 16
+    eng = HipEngine(cfg, B, dev, graph=False, seed=3, dtype="fp16")
+    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
+    real = real.to(torch.float16).float()
+    eng.set_batch(real)
+    ref_model = DCGAN(cfg, device=dev, seed=3)
+    eng.train_step()
+    torch.cuda.synchronize()
+    out, gd, gg = ReferenceStep(ref_model).compute_grads(real, eng.z.clone())
+    L = eng.last_losses()
+    for k in ("d_loss_real", "d_loss_fake", "g_loss", "d_loss"):
+        r = float(out[k].detach())
+        assert abs(L[k] - r) <= 2e-2 * max(1.0, abs(r)), (k, L[k], r)
+    scale = HipEngine.INIT_LOSS_SCALE  # raw engine grads carry the loss scale
+    e_d = rel(eng.grad_d.flat / scale, gd)
+    e_g = rel(eng.grad_g.flat / scale, gg)
+    print("fp16 whole-step relative grad error: D %.4f G %.4f" % (e_d, e_g))
+    assert e_d < 0.1 and e_g < 0.15
