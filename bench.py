@@ -30,7 +30,7 @@ def parse():
     p.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
     p.add_argument("--output_size", type=int, default=64)
     p.add_argument("--c_dim", type=int, default=3)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--engine", default="hip", choices=["hip", "reference"])
     p.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip engine)")
     p.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
@@ -88,7 +88,10 @@ def main():
     ms = dt / args.steps * 1e3
     if rank == 0:
         res = {
-            "metric": "images/sec (whole node), 64x64 DCGAN bs=128/GPU at 1/2/4/8 MI355X",
+            "metric": ("images/sec (whole node), 64x64 DCGAN bs=128/GPU at 1/2/4/8 MI355X"
+                       if (cfg.output_size, cfg.c_dim, args.batch_size) == (64, 3, 128)
+                       else "images/sec (whole node), %dx%dx%d DCGAN bs=%d/GPU"
+                       % (cfg.output_size, cfg.output_size, cfg.c_dim, args.batch_size)),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": args.gpus,
@@ -101,8 +104,8 @@ def main():
             "dtype": getattr(eng, "dtype_name", args.dtype),
             "data": "synthetic (uniform[-1,1] images of shape [B,%d,%d,%d]; random-init weights)"
                     % (cfg.output_size, cfg.output_size, cfg.c_dim),
-            "config": {"model": "DCGAN-%dx%dx%d (G 5,135,363 / D 4,316,545 params)"
-                       % (cfg.output_size, cfg.output_size, cfg.c_dim),
+            "config": {"model": "DCGAN-{0}x{0}x{1} (G {2:,} / D {3:,} params)".format(
+                           cfg.output_size, cfg.c_dim, cfg.param_counts()["g"], cfg.param_counts()["d"]),
                        "global_batch": args.batch_size * args.gpus, "per_gpu_batch": args.batch_size,
                        "seq_len": None, "parallelism": "dp%d" % args.gpus, "engine": eng.name,
                        "hip_graph": bool(getattr(eng, "graph_enabled", False)),

@@ -175,8 +175,8 @@ class Program {
     } else {
       throw std::runtime_error("bad igemm mode");
     }
-    if (a_elems * 2 >= 0x80000000ull || b_elems * 2 >= 0x80000000ull)
-      throw std::runtime_error("igemm operand exceeds the 2 GiB buffer-descriptor range");
+    if (a_elems * 2 >= OOB || b_elems * 2 >= OOB)
+      throw std::runtime_error("igemm operand exceeds the 3.875 GiB buffer-descriptor range");
     a.a_bytes = (uint32_t)(a_elems * 2); a.b_bytes = (uint32_t)(b_elems * 2);
     a.nphases = (int)ph.size();
     int maxM = 0;
@@ -229,8 +229,8 @@ class Program {
     a.kt_per_split = (KT + splits - 1) / splits;
     const size_t g_elems = mode == 2 ? (size_t)a.K * Mc : (size_t)Bn * Hg * Wg * Mc;
     const size_t d_elems = (size_t)a.K * Nc;
-    if (g_elems * 2 >= 0x80000000ull || d_elems * 2 >= 0x80000000ull)
-      throw std::runtime_error("wgrad operand exceeds the 2 GiB buffer-descriptor range");
+    if (g_elems * 2 >= OOB || d_elems * 2 >= OOB)
+      throw std::runtime_error("wgrad operand exceeds the 3.875 GiB buffer-descriptor range");
     a.g_bytes = (uint32_t)(g_elems * 2); a.d_bytes = (uint32_t)(d_elems * 2);
     a.fd_hw = fastdiv_make(Hd * Wd); a.fd_w = fastdiv_make(Wd); a.Hd = Hd; a.Wd = Wd;
     const size_t n = (size_t)a.ntaps * Mc * Nc;

@@ -72,7 +72,7 @@ __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t o
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
-constexpr uint32_t OOB = 0x80000000u;  // any offset past the descriptor size
+constexpr uint32_t OOB = 0xF8000000u;  // any offset past the descriptor size (operands < OOB bytes)
 
 // 16-byte LDS-DMA: buffer_load_dwordx4 ... lds. The wave's 64 lanes write 1 KiB contiguously at
 // `lds` (wave-uniform) + 16 * lane; the global offset is per lane (out of range -> zeros).
