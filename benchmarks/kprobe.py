@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--cfgs", default="210:1")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--stamps", action="store_true", help="per-workgroup s_memtime phase breakdown (igemm3)")
     a = ap.parse_args()
     ext = H.ext()
     dev = torch.device("cuda", 0)
@@ -40,6 +41,10 @@ def main():
     fl = flops(mode, Bn, Hin, Win, Kc, Hout, Wout, N)
     for spec in a.cfgs.split(","):
         c, sp = (int(x) for x in spec.split(":"))
+        stamps = None
+        if a.stamps:
+            stamps = torch.zeros(1 << 20, dtype=torch.int64, device=dev)
+            os.environ["DCGAN_IGEMM_STAMPS"] = str(stamps.data_ptr())
         p = ext.Program()
         p.igemm_ex(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad,
                    c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn if c >= 200 else 0, kb if c >= 200 else -1, sp)
@@ -53,6 +58,17 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
         print("%s cfg %d:%d  %.1f us  %.0f TF/s" % (name, c, sp, us, fl / us / 1e6), flush=True)
+        if stamps is not None:
+            os.environ.pop("DCGAN_IGEMM_STAMPS", None)
+            stamps.zero_()
+            H.run(p)
+            torch.cuda.synchronize()
+            st = stamps.view(-1, 8).cpu()
+            st = st[(st[:, 0] > 0) & (st[:, 3] > 0)].double()
+            seg = {"decode": (0, 7), "prologue": (7, 1), "K loop": (1, 2), "split/sync": (2, 4),
+                   "frag epilogue": (4, 5), "barrier": (5, 6), "stores+stats": (6, 3), "total": (0, 3)}
+            print("  stamps (%d WGs, median cycles): " % st.shape[0] + ", ".join(
+                "%s %d" % (k, (st[:, b] - st[:, a]).median()) for k, (a, b) in seg.items()), flush=True)
 
 
 if __name__ == "__main__":

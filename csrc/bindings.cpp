@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdlib>
 #include <functional>
 #include <memory>
 #include <stdexcept>
@@ -178,7 +179,18 @@ class Program {
     if (a_elems * 2 >= OOB || b_elems * 2 >= OOB)
       throw std::runtime_error("igemm operand exceeds the 3.875 GiB buffer-descriptor range");
     a.a_bytes = (uint32_t)(a_elems * 2); a.b_bytes = (uint32_t)(b_elems * 2);
+    for (auto& q : ph)
+      for (int t = 0; t < q.ntaps; ++t)
+        q.tap[t] = (q.dy[t] & 0xff) | ((q.dx[t] & 0xff) << 8) | ((int)q.wtap[t] << 16);
     a.nphases = (int)ph.size();
+    if (a.nphases > 4) throw std::runtime_error("igemm: more than 4 phases");
+    for (int i = 0; i < a.nphases; ++i) {
+      const IGemmPhase& q = ph[i];
+      IGemmPhaseK& k = a.phk[i];
+      k.Hq = q.Hq; k.Wq = q.Wq; k.M = q.M; k.iy0_off = q.iy0_off; k.ix0_off = q.ix0_off;
+      k.oy_off = q.oy_off; k.ox_off = q.ox_off; k.ntaps = q.ntaps; k.fd_hw = q.fd_hw; k.fd_w = q.fd_w;
+      for (int t = 0; t < 25; ++t) k.tap[t] = q.tap[t];
+    }
     int maxM = 0;
     for (auto& p : ph) maxM = std::max(maxM, p.M);
     const int mtiles = (maxM + bm - 1) / bm, ntiles = (N + bn - 1) / bn;
@@ -192,6 +204,8 @@ class Program {
     last_nphases_ = a.nphases;
     a.kb_valid = kb_valid;
     a.splits = splits;
+    if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
+    if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
     if (!v3)
       return add(name, stream, [this, a, cfg, mtiles, ntiles](hipStream_t s) {
         return KF(dcg_igemm_launch)(&a, cfg, mtiles, ntiles, s);

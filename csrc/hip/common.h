@@ -82,6 +82,23 @@ __device__ __forceinline__ void buf_load16_lds(__amdgpu_buffer_rsrc_t r, void* l
 #endif
 }
 
+// The same 16-byte LDS-DMA as inline asm. hipcc cannot tell which LDS bytes a DMA writes, so
+// after the builtin form it waits vmcnt(0) before the next ds_read of ANY LDS address -- which
+// drains the tile just issued for the NEXT k-step and serialises load and compute. Hidden in
+// asm, the DMA is invisible to its waitcnt pass; the caller orders it with explicit counted
+// `s_waitcnt vmcnt(N)` + barrier (and must not mix it with compiler-visible vector loads in
+// the same pipelined span). M0 write -> LDS-DMA needs one wait state (s_nop 0).
+__device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(la), "v"(off), "s"(r) : "memory", "m0");
+#pragma clang diagnostic pop
+#endif
+}
+
 // Unsigned division by a runtime-invariant divisor (round-up multiply method, exact for all
 // 32-bit n). Host computes {mul, shift} with fastdiv_make().
 struct FastDiv {

@@ -1,0 +1,95 @@
+// Fused conv-GEMM epilogue shared by igemm.hip and igemm3.hip: + bias, per-channel BN partial
+// statistics of the stored value, activation, pixel scatter (rowoff), output staged through
+// LDS for 16-byte row stores.
+//
+// Compile-time activation / store mode: a runtime `switch (act)` inside the 64-element loop was
+// expanded per element by hipcc (incl. an inlined tanh) into ~200 scalar branches per thread --
+// measured 16k cycles per 128x128 workgroup, a quarter of its lifetime. The caller dispatches
+// ONCE on (act, vec) and every variant below is straight-line code (validity by selects).
+#pragma once
+#include "kernels.h"
+
+namespace dcg {
+
+template <int ACT>
+__device__ __forceinline__ float act_ct(float v, float leak) {
+  if constexpr (ACT == ACT_RELU) return fmaxf(v, 0.f);
+  else if constexpr (ACT == ACT_LRELU) return fmaxf(v, leak * v);
+  else if constexpr (ACT == ACT_TANH) return tanhf(v);
+  else return v;
+}
+
+// acc[FM][FN] of a (WM x WN)-wave tile, wave (wm, wn), lane (fr, fq). rowoff[BM] (LDS) holds each
+// tile row's output element offset or -1; red[WM][BN][2] and ctile[BM][BN + 8] are LDS scratch.
+template <int ACT, bool VEC, int FM, int FN, int TM, int TN, int BN>
+__device__ __forceinline__ void frag_epilogue(const f32x4 (&acc)[FM][FN], const IGemmArgs& p, const int* rowoff,
+                                              float* red, elem_t* ctile, int wm, int wn, int fr, int fq, int n0,
+                                              bool do_stats) {
+  constexpr int CPAD = BN + 8;
+  const int N = p.N;
+  // the 4 consecutive rows of each M fragment: one 16-byte LDS read per fragment
+  int ro[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int4 v = *reinterpret_cast<const int4*>(rowoff + wm * TM + i * 16 + fq * 4);
+    ro[i][0] = v.x; ro[i][1] = v.y; ro[i][2] = v.z; ro[i][3] = v.w;
+  }
+  const bool f32out = p.out_f32 != 0;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = wn * TN + j * 16 + fr;
+    const int n = n0 + nl;
+    const bool nok = n < N;
+    const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
+    float s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int off = ro[i][r];
+        const bool valid = off >= 0 && nok;
+        const float v = acc[i][j][r] + bv;
+        // statistics of exactly the stored (rounded) tensor: BN forward and backward see one x
+        const float vs = f32out ? v : (float)f2bf(v);
+        s += valid ? vs : 0.f;
+        s2 += valid ? vs * vs : 0.f;
+        const float o = act_ct<ACT>(v, p.leak);
+        if constexpr (VEC) {
+          ctile[(wm * TM + i * 16 + fq * 4 + r) * CPAD + nl] = f2bf(o);
+        } else if (valid) {
+          if (f32out) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
+          else reinterpret_cast<elem_t*>(p.C)[off + p.cofs + n] = f2bf(o);
+        }
+      }
+    }
+    if (do_stats) {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (fq == 0) {
+        red[(wm * BN + nl) * 2 + 0] = s;
+        red[(wm * BN + nl) * 2 + 1] = s2;
+      }
+    }
+  }
+}
+
+// one uniform dispatch on (act, vec) around the straight-line variants
+template <int FM, int FN, int TM, int TN, int BN>
+__device__ __forceinline__ void frag_epilogue_dispatch(const f32x4 (&acc)[FM][FN], const IGemmArgs& p,
+                                                       const int* rowoff, float* red, elem_t* ctile, int wm, int wn,
+                                                       int fr, int fq, int n0, bool do_stats, bool vec) {
+#define DCG_EPI(A)                                                                                         \
+  if (vec) frag_epilogue<A, true, FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats); \
+  else frag_epilogue<A, false, FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats);
+  switch (p.act) {
+    case ACT_RELU: DCG_EPI(ACT_RELU) break;
+    case ACT_LRELU: DCG_EPI(ACT_LRELU) break;
+    case ACT_TANH: DCG_EPI(ACT_TANH) break;
+    default: DCG_EPI(ACT_NONE) break;
+  }
+#undef DCG_EPI
+}
+
+}  // namespace dcg

@@ -27,7 +27,7 @@
 // value over the tile's rows, per (M-tile, phase) for a deterministic finalize), activation
 // (relu / lrelu / tanh), pixel scatter of the phase, output staged through LDS and written as
 // 16-byte row segments (elem_t, N % 8 == 0) or element-wise (fp32 / narrow N).
-#include "kernels.h"
+#include "epilogue.h"
 
 namespace dcg {
 
@@ -235,48 +235,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const bool do_stats = p.stats != nullptr;
   // vector store path: elem_t output, whole 8-channel groups, aligned destination
   const bool vec = !p.out_f32 && (BN % 8 == 0) && (N % 8 == 0) && (p.ldc % 8 == 0) && (p.cofs % 8 == 0);
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int nl = wn * TN + j * 16 + fr;
-    const int n = n0 + nl;
-    const bool nok = n < N;
-    const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
-    float s = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ml = wm * TM + i * 16 + fq * 4 + r;
-        const int off = rowoff[ml];
-        const float v = acc[i][j][r] + bv;
-        const elem_t vb = f2bf(v);
-        if (off >= 0 && nok) {
-          // statistics of exactly the stored (elem_t-rounded) tensor, so BN forward/backward
-          // see one consistent x
-          const float vs = p.out_f32 ? v : (float)vb;
-          s += vs;
-          s2 += vs * vs;
-        }
-        const float o = apply_act(v, p.act, p.leak);
-        if (vec) {
-          ctile[ml * CPAD + nl] = f2bf(o);
-        } else if (off >= 0 && nok) {
-          if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
-          else reinterpret_cast<elem_t*>(p.C)[off + p.cofs + n] = f2bf(o);
-        }
-      }
-    }
-    if (do_stats) {
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (fq == 0) {
-        red[(wm * BN + nl) * 2 + 0] = s;
-        red[(wm * BN + nl) * 2 + 1] = s2;
-      }
-    }
-  }
+  frag_epilogue_dispatch<FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats, vec);
   if (do_stats || vec) __syncthreads();
   if (vec) {
     constexpr int CPR = BN / 8;  // 16-byte chunks per row

@@ -26,7 +26,7 @@
 // Workgroup -> tile mapping is XCD-aware: workgroups are dispatched round-robin over the 8
 // XCDs, so workgroup b works on tile (b % 8) * (T / 8) + b / 8, which gives every XCD a
 // contiguous run of tiles (neighbouring output pixels share input rows in that XCD's L2).
-#include "kernels.h"
+#include "epilogue.h"
 
 namespace dcg {
 
@@ -76,6 +76,9 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  // diagnostics: [start, K loop start, K loop end, end] per workgroup (off in production)
+  unsigned long long* stamp = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memtime();
 
   // ---- tile decode (XCD-aware): t -> (phase, mt, nt, split), split fastest
   const int S = p.splits;
@@ -91,8 +94,8 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   const int phase = r_ / p.mtiles;
   const int tile_id = (phase * p.mtiles + mt) * ntn + nt;
 
-  const IGemmPhase* ph = p.ph + phase;
-  const int M = ph->M;
+  const IGemmPhaseK& ph = p.phk[phase];  // kernarg segment: scalar loads
+  const int M = ph.M;
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= M) {  // phase with fewer rows (odd output sizes): its stats slot must still be defined
     if (p.stats && split == 0) {
@@ -103,16 +106,18 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     return;
   }
   const int Kc = p.Kc, N = p.N;
-  const int ntaps = p.plain ? 1 : ph->ntaps;
+  const int ntaps = p.plain ? 1 : ph.ntaps;
   const int kt_per_tap = (Kc + BK - 1) / BK;
   const int KT = ntaps * kt_per_tap;
   const int kps = (KT + S - 1) / S;  // per phase: deconv phases have 9 / 6 / 6 / 4 taps
+  if (stamp && tid == 0) stamp[7] = __builtin_amdgcn_s_memtime();
   const int kt0 = split * kps;
   const int kt1 = min(KT, kt0 + kps);
   const int nk = max(0, kt1 - kt0);
 
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, p.b_bytes);
+  // ablation (timing only, outputs wrong): a zero-size descriptor drops every load through it
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, (p.ablate & 1) ? 0u : p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, (p.ablate & 2) ? 0u : p.b_bytes);
 
   // ---- A rows of this lane: piece q = wave + 4 i, row = 8 q + lane / 8, slot = lane & 7,
   //      global 16-byte chunk = slot ^ (row & 7)
@@ -127,12 +132,12 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     if (p.plain) {
       a_base[i] = m * Kc; a_iy[i] = 0; a_ix[i] = 0;
     } else {
-      const uint32_t b = fdiv((uint32_t)m, ph->fd_hw);
-      const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph->Hq * ph->Wq);
-      const uint32_t qy = fdiv(rem, ph->fd_w);
-      const uint32_t qx = rem - qy * (uint32_t)ph->Wq;
-      a_iy[i] = (int)qy * p.sstride + ph->iy0_off;
-      a_ix[i] = (int)qx * p.sstride + ph->ix0_off;
+      const uint32_t b = fdiv((uint32_t)m, ph.fd_hw);
+      const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph.Hq * ph.Wq);
+      const uint32_t qy = fdiv(rem, ph.fd_w);
+      const uint32_t qx = rem - qy * (uint32_t)ph.Wq;
+      a_iy[i] = (int)qy * p.sstride + ph.iy0_off;
+      a_ix[i] = (int)qx * p.sstride + ph.ix0_off;
       a_base[i] = (((int)b * p.H + a_iy[i]) * p.W + a_ix[i]) * Kc;
     }
   }
@@ -147,7 +152,12 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     char* sa = lds + slot * STAGE;
     char* sb = sa + A_BYTES;
     int dy = 0, dx = 0, wt = 0;
-    if (!p.plain) { dy = ph->dy[cur_ti]; dx = ph->dx[cur_ti]; wt = ph->wtap[cur_ti]; }
+    if (!p.plain) {
+      const int ti = ph.tap[cur_ti];  // scalar load (kernarg): no vector load inside the pipelined loop
+      dy = (int)(signed char)(ti & 0xff);
+      dx = (int)(signed char)((ti >> 8) & 0xff);
+      wt = ti >> 16;
+    }
     const int cc = cur_c0 + a_chunk * 8;
     const bool kval = cc < Kc;
     const int tap_delta = (dy * p.W + dx) * Kc;
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
         if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
           off = (uint32_t)(a_base[i] + tap_delta + cc) * 2u;
       }
-      buf_load16_lds(ra, sa + (wave + 4 * i) * 1024, off);
+      dma16_asm(ra, sa + (wave + 4 * i) * 1024, off);
     }
 #pragma unroll
     for (int i = 0; i < PPW_B; ++i) {
@@ -177,7 +187,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
         const int c = cur_c0 + a_chunk * 8;
         if (n < N && c < Kc && c < p.kb_valid) off = (uint32_t)((wt * N + n) * Kc + c) * 2u;
       }
-      buf_load16_lds(rb, sb + q * 1024, off);
+      dma16_asm(rb, sb + q * 1024, off);
     }
     cur_c0 += BK;
     if (cur_c0 >= Kc) { cur_c0 = 0; ++cur_ti; }
@@ -195,6 +205,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 
   const int fr = lane & 15, fq = lane >> 4;
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memtime();
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt landed for this wave; younger tiles (up to NS-2 of them) may stay in flight
     if constexpr (NS >= 3) {
@@ -211,14 +222,16 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS);
     const char* sa = lds + (kt % NS) * STAGE;
     const char* sb = sa + A_BYTES;
+    // all fragments of the k-tile first (both k32 halves: the second half's LDS reads are in
+    // flight while the first half's MFMAs run), then one prioritised MFMA cluster
+    elem8 af[2][FM], bfr[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      elem8 af[FM], bfr[FN];
       const int c = ks * 4 + fq;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * TM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const elem8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
+        af[ks][i] = *reinterpret_cast<const elem8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
       }
       if constexpr (BKN) {
 #pragma unroll
@@ -231,24 +244,29 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
                 LDS_PTR(s16x4, sb + r * SB + ((c8 ^ kn_swz<SB>(r)) * 8)));
             const elem4 vb = __builtin_bit_cast(elem4, v);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = vb[e];
+            for (int e = 0; e < 4; ++e) bfr[ks][j][4 * h + e] = vb[e];
           }
         }
       } else {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int r = wn * TN + j * 16 + fr;
-          bfr[j] = *reinterpret_cast<const elem8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
+          bfr[ks][j] = *reinterpret_cast<const elem8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
         }
       }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = DCG_MFMA_16x16x32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = DCG_MFMA_16x16x32(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   }
 
+  if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memtime();
   // ------------------------------------------------------------------ split-K hand-off
   if (S > 1) {
     // flag word in the (now idle) dynamic LDS: a static __shared__ would shift the 16-byte
@@ -314,61 +332,25 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
       if (p.plain) {
         off = m * p.ldc;
       } else {
-        const uint32_t b = fdiv((uint32_t)m, ph->fd_hw);
-        const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph->Hq * ph->Wq);
-        const uint32_t qy = fdiv(rem, ph->fd_w);
-        const uint32_t qx = rem - qy * (uint32_t)ph->Wq;
-        const int y = (int)qy * p.ostride + ph->oy_off, x = (int)qx * p.ostride + ph->ox_off;
+        const uint32_t b = fdiv((uint32_t)m, ph.fd_hw);
+        const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph.Hq * ph.Wq);
+        const uint32_t qy = fdiv(rem, ph.fd_w);
+        const uint32_t qx = rem - qy * (uint32_t)ph.Wq;
+        const int y = (int)qy * p.ostride + ph.oy_off, x = (int)qx * p.ostride + ph.ox_off;
         off = (((int)b * p.outH + y) * p.outW + x) * p.ldc;
       }
     }
     rowoff[r] = off;
   }
   __syncthreads();
+  if (stamp && tid == 0) stamp[4] = __builtin_amdgcn_s_memtime();
 
   const bool do_stats = p.stats != nullptr;
   const bool vec = !p.out_f32 && (N % 8 == 0) && (p.ldc % 8 == 0) && (p.cofs % 8 == 0);
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int nl = wn * TN + j * 16 + fr;
-    const int n = n0 + nl;
-    const bool nok = n < N;
-    const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
-    float s = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ml = wm * TM + i * 16 + fq * 4 + r;
-        const int off = rowoff[ml];
-        const float v = acc[i][j][r] + bv;
-        const elem_t vb = f2bf(v);
-        if (off >= 0 && nok) {
-          const float vs = p.out_f32 ? v : (float)vb;
-          s += vs;
-          s2 += vs * vs;
-        }
-        const float o = apply_act(v, p.act, p.leak);
-        if (vec) {
-          ctile[ml * CPAD + nl] = f2bf(o);
-        } else if (off >= 0 && nok) {
-          if (p.out_f32) reinterpret_cast<float*>(p.C)[off + p.cofs + n] = o;
-          else reinterpret_cast<elem_t*>(p.C)[off + p.cofs + n] = f2bf(o);
-        }
-      }
-    }
-    if (do_stats) {
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (fq == 0) {
-        red[(wm * BN + nl) * 2 + 0] = s;
-        red[(wm * BN + nl) * 2 + 1] = s2;
-      }
-    }
-  }
+  frag_epilogue_dispatch<FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats, vec);
+  if (stamp && tid == 0) stamp[5] = __builtin_amdgcn_s_memtime();
   if (do_stats || vec) __syncthreads();
+  if (stamp && tid == 0) stamp[6] = __builtin_amdgcn_s_memtime();
   if (vec) {
     constexpr int CPR = BN / 8;
     elem_t* C = reinterpret_cast<elem_t*>(p.C);
@@ -395,6 +377,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
       dst[N + n] = s2;
     }
   }
+  if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memtime();
 }
 
 }  // namespace dcg

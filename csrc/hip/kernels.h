@@ -13,6 +13,16 @@ struct IGemmPhase {
   signed char dy[25], dx[25];
   short wtap[25];
   short pad_;
+  int tap[25];              // packed (dy & 0xff) | (dx & 0xff) << 8 | wtap << 16 (igemm3: staged in LDS)
+};
+
+// Compact per-phase table passed BY VALUE in the kernel arguments (igemm3): uniform reads of it
+// are scalar loads from the kernarg segment, instead of dependent vector loads from a device
+// table (which cost ~1-2k cycles each in a workgroup's prologue / epilogue).
+struct IGemmPhaseK {
+  int Hq, Wq, M, iy0_off, ix0_off, oy_off, ox_off, ntaps;
+  FastDiv fd_hw, fd_w;
+  int tap[25];              // packed (dy & 0xff) | (dx & 0xff) << 8 | wtap << 16
 };
 
 struct IGemmArgs {
@@ -29,6 +39,9 @@ struct IGemmArgs {
   int splits;               // split-K over workgroups (k tiles split evenly per phase)
   float* ws;                // [tiles][splits][BM*BN] fp32 slabs (splits > 1)
   unsigned* counters;       // [tiles] arrival counters, zero between launches
+  int ablate;               // timing-only builds: bit0 drops A loads, bit1 drops B loads (0 = normal)
+  unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime at 4 points (nullptr = off)
+  IGemmPhaseK phk[4];       // igemm3: the phase table by value
 };
 
 struct WGradArgs {

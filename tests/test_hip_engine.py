@@ -76,7 +76,7 @@ def test_engine_stagewise(size, c_dim, B, dtype):
     edt = eng.edt
     real = (torch.rand(B, size, size, c_dim, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     eng.set_batch(real)
-    st = [torch.cuda.current_stream()]
+    st = eng._streams()  # main + side stream (weight gradients run concurrently)
     H.run(eng.progA, st)          # forward + d_loss backward (D grads final)
     torch.cuda.synchronize()
     Pd, Pg, gD, gG = eng.model.d, eng.model.g, eng.grad_d, eng.grad_g
