@@ -379,6 +379,14 @@ class Program {
                       n, lr, b1, b2, eps, gscale, P<const float>(ls), s);
     });
   }
+  // TF-SAME stride-2 5x5 conv_transpose with 1..4 output channels (direct VALU kernel)
+  int narrow_deconv(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int Hi, int Wi,
+                    int C, int Ho, int Wo, int N, int pad, int act, float leak, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_narrow_deconv)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B, Hi,
+                                   Wi, C, Ho, Wo, N, pad, act, leak, s);
+    });
+  }
   // dynamic loss scaling: flag ls[1] if any gradient is non-finite
   int nonfinite_check(std::string name, uintptr_t g, size_t n, uintptr_t ls, int stream) {
     return add(name, stream, [=](hipStream_t s) { return KF(dcg_nonfinite_check)(P<const float>(g), n, P<float>(ls), s); });
@@ -505,6 +513,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("b2d"), py::arg("b1g"), py::arg("b2g"), py::arg("step"), py::arg("stream"), py::arg("ls") = 0,
            py::arg("growth_interval") = 2000)
       .def("nonfinite_check", &Program::nonfinite_check)
+      .def("narrow_deconv", &Program::narrow_deconv)
       .def("pack", &Program::pack)
       .def("philox_uniform", &Program::philox_uniform)
       .def("im2col_s2", &Program::im2col_s2)

@@ -85,13 +85,18 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   const int ntn = (p.N + BN - 1) / BN;
   const int total = p.mtiles * ntn * p.nphases * S;
   int t = blockIdx.x;
-  if ((total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);
+  {  // bijective XCD remap: workgroups b, b+8, b+16, ... (one XCD) get a contiguous run of t
+    const int q = total >> 3, rr = total & 7, xcd = t & 7;
+    t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+  }
+  // split fastest (a tile's slabs on one XCD), then PHASE (deconv phases have 9/6/6/4 taps: a
+  // phase-slowest order would give whole XCDs the 9-tap phase), then n, then m
   const int split = t % S;
   int r_ = t / S;
+  const int phase = r_ % p.nphases;
+  r_ /= p.nphases;
   const int nt = r_ % ntn;
-  r_ /= ntn;
-  const int mt = r_ % p.mtiles;
-  const int phase = r_ / p.mtiles;
+  const int mt = r_ / ntn;
   const int tile_id = (phase * p.mtiles + mt) * ntn + nt;
 
   const IGemmPhaseK& ph = p.phk[phase];  // kernarg segment: scalar loads

@@ -1,0 +1,144 @@
+// Narrow-output TF-SAME stride-2 5x5 conv_transpose (N = 1..4 output channels), direct on VALU:
+// the two 3-channel GEMMs of the step -- G's last layer (64 -> 3, + bias + tanh) and D layer 0's
+// data gradient for the fake half (64 -> 3) -- where an MFMA tile pads N=3 to 16 (5x waste;
+// measured 29 TF/s, 43 us each at B=128).
+//
+// Workgroup = one output tile of 16x16 pixels of one image = the 4 sub-pixel phases x an 8x8
+// grid; wave w computes phase w (so every lane of a wave walks the same tap list and the weight
+// reads are LDS broadcasts). The input halo (<= 12x12 pixels x C channels) and all 25 x N x C
+// weights are staged once in LDS; each lane accumulates its pixel's N outputs in fp32 with
+// v_dot2_f32_bf16 (2 MACs / instruction) over 8-channel 16-byte chunks.
+#include "kernels.h"
+
+namespace dcg {
+
+constexpr int NW_TILE = 16;   // output tile edge
+constexpr int NW_HALO = 12;   // input tile edge (covers the taps of all 4 phases, pad <= 2)
+
+template <int K>
+__device__ __forceinline__ float dot2k(const elem8 a, const elem8 b, float acc) {
+#ifdef DCG_F16
+  return __builtin_amdgcn_fdot2(__builtin_shufflevector(a, a, K, K + 1), __builtin_shufflevector(b, b, K, K + 1), acc,
+                                false);
+#else
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, K, K + 1),
+                                         __builtin_shufflevector(b, b, K, K + 1), acc, false);
+#endif
+}
+
+__device__ __forceinline__ float dot8(const elem8 a, const elem8 b, float acc) {
+  acc = dot2k<0>(a, b, acc);
+  acc = dot2k<2>(a, b, acc);
+  acc = dot2k<4>(a, b, acc);
+  return dot2k<6>(a, b, acc);
+}
+
+template <int N, int CT8>  // CT8 = C / 8 when fixed at compile time (0 = runtime C)
+__global__ __launch_bounds__(256) void narrow_deconv_kernel(const elem_t* __restrict__ x, const elem_t* __restrict__ w,
+                                                            const float* __restrict__ bias, elem_t* __restrict__ y,
+                                                            int Hi, int Wi, int C, int Ho, int Wo, int pad, int act,
+                                                            float leak, int tiles_x, int tiles_per_img) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int C8 = CT8 > 0 ? CT8 : (C >> 3);
+  const int swz = ((C8 & (C8 - 1)) == 0) ? ((C8 - 1) & 7) : 0;  // chunk XOR (power-of-2 chunk counts)
+  elem8* xs = reinterpret_cast<elem8*>(smem);                         // [HALO*HALO][C8] (chunk-swizzled)
+  elem8* ws = xs + NW_HALO * NW_HALO * C8;                            // [25][N][C8]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / tiles_per_img;
+  const int trem = blockIdx.x - b * tiles_per_img;
+  const int ty0 = (trem / tiles_x) * NW_TILE, tx0 = (trem % tiles_x) * NW_TILE;
+  // input rows/cols needed: iy = (oy + pad - ky) / 2 for oy in [ty0, ty0 + 16), ky in [0, 5)
+  const int iy_lo = (ty0 + pad - 4) >> 1, ix_lo = (tx0 + pad - 4) >> 1;  // floor division (>> on negatives)
+
+  // ---- stage input halo (zero outside the image) and weights
+  const elem8 zero8 = {};
+  for (int q = tid; q < NW_HALO * NW_HALO * C8; q += 256) {
+    const int pix = q / C8, c = q - pix * C8;
+    const int iy = iy_lo + pix / NW_HALO, ix = ix_lo + pix % NW_HALO;
+    elem8 v = zero8;
+    if ((unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
+      v = *reinterpret_cast<const elem8*>(x + (((size_t)b * Hi + iy) * Wi + ix) * C + c * 8);
+    xs[pix * C8 + (c ^ (pix & swz))] = v;
+  }
+  for (int q = tid; q < 25 * N * C8; q += 256) ws[q] = reinterpret_cast<const elem8*>(w)[q];
+  __syncthreads();
+
+  // ---- this lane's output pixel: phase (py, px) = wave, grid position = lane
+  const int py = wave >> 1, px = wave & 1;
+  const int oy = ty0 + 2 * (lane >> 3) + py, ox = tx0 + 2 * (lane & 7) + px;
+  const int kys = (oy + pad) & 1, kxs = (ox + pad) & 1;  // tap parities of this phase
+  float acc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = 0.f;
+  for (int ky = kys; ky < 5; ky += 2) {
+    const int iy = ((oy + pad - ky) >> 1) - iy_lo;
+    for (int kx = kxs; kx < 5; kx += 2) {
+      const int ix = ((ox + pad - kx) >> 1) - ix_lo;
+      const int pix = iy * NW_HALO + ix;
+      const elem8* xr = xs + pix * C8;
+      const elem8* wr = ws + (ky * 5 + kx) * N * C8;
+      if constexpr (CT8 > 0) {
+        // fixed channel count: the tap's N x C weights in registers (one broadcast read each),
+        // then one input read + 4N dot2 per 8-channel chunk
+        elem8 wv[N][CT8];
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+#pragma unroll
+          for (int c = 0; c < CT8; ++c) wv[n][c] = wr[n * CT8 + c];
+#pragma unroll
+        for (int c = 0; c < CT8; ++c) {
+          const elem8 xv = xr[c ^ (pix & swz)];
+#pragma unroll
+          for (int n = 0; n < N; ++n) acc[n] = dot8(xv, wv[n][c], acc[n]);
+        }
+      } else {
+        for (int c = 0; c < C8; ++c) {
+          const elem8 xv = xr[c ^ (pix & swz)];
+#pragma unroll
+          for (int n = 0; n < N; ++n) acc[n] = dot8(xv, wr[n * C8 + c], acc[n]);
+        }
+      }
+    }
+  }
+  if (oy < Ho && ox < Wo) {
+    elem_t* dst = y + (((size_t)b * Ho + oy) * Wo + ox) * N;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      float v = acc[n] + (bias ? bias[n] : 0.f);
+      dst[n] = f2bf(apply_act(v, act, leak));
+    }
+  }
+}
+
+}  // namespace dcg
+
+extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, const float* bias, elem_t* y, int B,
+                                          int Hi, int Wi, int C, int Ho, int Wo, int N, int pad, int act, float leak,
+                                          hipStream_t s) {
+  // the 12x12 halo covers oy in [ty0, ty0+16) for pad <= 2; C a multiple of 8 up to 256
+  if (pad < 0 || pad > 2 || C % 8 || C > 256 || N < 1 || N > 4) return -2;
+  const int tiles_x = (Wo + dcg::NW_TILE - 1) / dcg::NW_TILE, tiles_y = (Ho + dcg::NW_TILE - 1) / dcg::NW_TILE;
+  const size_t shm = (size_t)(dcg::NW_HALO * dcg::NW_HALO + 25 * N) * C * sizeof(elem_t);
+  if (shm > 160 * 1024) return -2;
+  dim3 grid(B * tiles_x * tiles_y);
+#define NW_LAUNCH(NN)                                                                                          \
+  {                                                                                                            \
+    auto k = C == 64 ? dcg::narrow_deconv_kernel<NN, 8> : dcg::narrow_deconv_kernel<NN, 0>;                    \
+    static bool attr[2] = {false, false};                                                                      \
+    if (!attr[C == 64]) {                                                                                      \
+      hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return (int)e;                                                                      \
+      attr[C == 64] = true;                                                                                    \
+    }                                                                                                          \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm, s, x, w, bias, y, Hi, Wi, C, Ho, Wo, pad, act, leak, tiles_x,  \
+                       tiles_x * tiles_y);                                                                     \
+  }
+  switch (N) {
+    case 1: NW_LAUNCH(1) break;
+    case 2: NW_LAUNCH(2) break;
+    case 3: NW_LAUNCH(3) break;
+    default: NW_LAUNCH(4) break;
+  }
+#undef NW_LAUNCH
+  return (int)hipGetLastError();
+}

@@ -207,6 +207,15 @@ class HipEngine:
                       ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0, int(bkn), kb_valid, splits)
         return cfg
 
+    def _deconv_out(self, prog, name, x, w, y, B, L, pad, bias, act):
+        """G's output layer: the direct narrow kernel for RGB / gray outputs, else the igemm."""
+        if L.cout <= 4 and L.cin % 8 == 0 and L.cin <= 256:
+            prog.narrow_deconv(name, _p(x), _p(w), _p(bias), _p(y), B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw,
+                               L.cout, pad, act, self.cfg.lrelu_leak, 0)
+        else:
+            self._igemm(prog, name, 1, x, w, y, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad,
+                        bias=bias, act=act)
+
     def _igemm_stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None, bkn=False):
         if mode == 1:
             M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
@@ -272,8 +281,7 @@ class HipEngine:
                              update_ema)
                 a_prev = self.g_a[L.name]
             else:  # last: + bias, tanh, written into the fake half of D's input
-                self._igemm(prog, L.name, 1, a_prev, nat, self.fake, B, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], act=TANH)
+                self._deconv_out(prog, L.name, a_prev, nat, self.fake, B, L, pad, Pg[L.name + "/biases"], TANH)
         # D forward on [real | fake]
         prev = self.d_in
         for i, L in enumerate(self.dl):
@@ -447,8 +455,12 @@ class HipEngine:
                 self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, half(self.d_da[P_.name]), B, L.out_hw,
                             L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
             else:
-                self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw, L.out_hw,
-                            L.cout, L.in_hw, L.in_hw, L.cin, pad)
+                if L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
+                    prog.narrow_deconv("g." + L.name + ".dgrad_img", _p(dx), _p(nat), 0, _p(self.img_grad), B,
+                                       L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, NONE, 0.0, 0)
+                else:
+                    self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw,
+                                L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
         # ---------------- G backward
         n = len(self.gl)
         Lg = self.gl[-1]
@@ -719,8 +731,7 @@ class HipEngine:
                                   RELU, 0.0, 0)
                 prev = ab
             else:
-                self._igemm(prog, "s." + L.name, 1, prev, nat, self._s_out, B, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], act=TANH)
+                self._deconv_out(prog, "s." + L.name, prev, nat, self._s_out, B, L, pad, Pg[L.name + "/biases"], TANH)
         self.progS = prog
 
     def eval_losses(self, real: torch.Tensor, z: torch.Tensor) -> Dict[str, float]:

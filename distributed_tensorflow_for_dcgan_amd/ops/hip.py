@@ -202,7 +202,8 @@ def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_
 # --------------------------------------------------------------------------- one-shot wrappers
 def _check_bf16(*ts):
     for t in ts:
-        if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous() or not t.is_cuda):
+        if t is not None and (t.dtype not in (torch.bfloat16, torch.float16) or not t.is_contiguous()
+                              or not t.is_cuda):
             raise ValueError("expected contiguous cuda bf16 tensor, got %s %s" % (t.dtype, t.device))
 
 
@@ -275,6 +276,23 @@ def conv2d_transpose_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, ou
                   cout, 0, _p(bias), ACT[act], leak, _p(st), 0, int(bkn), -1, splits)
     run(prog)
     return (y, st) if stats else y
+
+
+def narrow_deconv(x: torch.Tensor, w: torch.Tensor, out_hw: Tuple[int, int], bias: Optional[torch.Tensor] = None,
+                  act: Optional[str] = None, leak: float = 0.2) -> torch.Tensor:
+    """TF-SAME stride-2 5x5 conv_transpose with N <= 4 output channels on the direct VALU
+    kernel. x [B,Hi,Wi,C] (C % 8 == 0), w [25][N][C] (the TF deconv layout [5,5,N,C], or a
+    conv's HWIO [5,5,N=ci,C=co] for its data gradient)."""
+    _check_bf16(x, w)
+    B, Hi, Wi, C = x.shape
+    N = w.numel() // (25 * C)
+    Ho, Wo = out_hw
+    y = torch.empty(B, Ho, Wo, N, device=x.device, dtype=x.dtype)
+    prog = ext().Program(x.dtype == torch.float16)
+    prog.narrow_deconv("narrow", _p(x), _p(w), _p(bias), _p(y), B, Hi, Wi, C, Ho, Wo, N, same_pads(Ho)[0],
+                       ACT[act], leak, 0)
+    run(prog)
+    return y
 
 
 def gemm_plain(a: torch.Tensor, bt: torch.Tensor, out_f32: bool = False, bias=None, act=None,

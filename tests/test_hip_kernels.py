@@ -366,3 +366,23 @@ def test_philox_uniform_range_and_determinism():
     assert torch.equal(out1, out2)
     assert out1.min() >= -1 and out1.max() < 1
     assert abs(out1.mean().item()) < 0.03 and abs(out1.std().item() - 1 / math.sqrt(3)) < 0.02
+
+
+@pytest.mark.parametrize("B,Hi,Ho,C,N,dtype", [(4, 32, 64, 64, 3, "bf16"), (2, 4, 7, 64, 3, "bf16"),
+                                                (3, 14, 28, 64, 1, "bf16"), (2, 16, 32, 128, 3, "fp16")])
+def test_narrow_deconv(B, Hi, Ho, C, N, dtype):
+    """Direct VALU conv_transpose for N <= 4 outputs (G's RGB layer, D layer-0 data gradient):
+    bias + tanh, odd sizes (pad 2), 1 channel, fp16 build."""
+    h = H()
+    edt = torch.float16 if dtype == "fp16" else torch.bfloat16
+    x = rnd(B, Hi, Hi, C, seed=60).to(edt)
+    w = (rnd(5, 5, N, C, scale=0.05, seed=61)).to(edt)
+    bias = rnd(N, scale=0.1, seed=62)
+    y = h.narrow_deconv(x, w, (Ho, Ho), bias=bias, act="tanh")
+    ref = torch.tanh(R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias))
+    close(y, ref, 1e-2, "narrow deconv")
+    # as the data gradient of a conv with HWIO weight [5,5,N,C]
+    xg = rnd(B, Ho, Ho, N, seed=63).requires_grad_(True)
+    yc = R.conv2d_same(xg, w.float())
+    (gx,) = torch.autograd.grad(yc, xg, x.float())
+    close(h.narrow_deconv(x, w, (Ho, Ho)), gx, 1e-2, "narrow as conv dgrad")
