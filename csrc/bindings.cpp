@@ -117,7 +117,9 @@ class Program {
   // (bkn = 1 reads Bw as [tap][Kc][N]; kb_valid = number of real B k-rows; splits = split-K).
   int igemm_ex(std::string name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win, int Kc,
                int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
-               uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits) {
+               uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
+               uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
+               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f) {
     int bm = 0, bn = 0, ns = 0;
     const bool v3 = cfg >= 200;
     if (v3 ? dcg_igemm3_tile(cfg, &bm, &bn, &ns) : dcg_igemm_tile(cfg, &bm, &bn))
@@ -204,6 +206,18 @@ class Program {
     last_nphases_ = a.nphases;
     a.kb_valid = kb_valid;
     a.splits = splits;
+    if (bnb_x) {
+      const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
+      if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 16384 > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
+        throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
+      if (!stats || bnb_rpg <= 0 || !bnb_y || !bnb_mean || !bnb_rstd)
+        throw std::runtime_error("igemm bnb: needs stats, rows-per-group, y, mean, rstd");
+      for (auto& q : ph)  // tiles must not straddle a BN group (a phase's rows are (b, qy, qx))
+        if (bnb_rpg % bm || q.M % bnb_rpg) throw std::runtime_error("igemm bnb: tile rows must divide the group");
+      a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
+      a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
+      a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
+    }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
     if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
     if (!v3)
@@ -485,7 +499,13 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("memset", &Program::memset)
       .def("copy", &Program::copy)
       .def("igemm", &Program::igemm)
-      .def("igemm_ex", &Program::igemm_ex)
+      .def("igemm_ex", &Program::igemm_ex, py::arg("name"), py::arg("mode"), py::arg("A"), py::arg("Bw"), py::arg("C"),
+           py::arg("Bn"), py::arg("Hin"), py::arg("Win"), py::arg("Kc"), py::arg("Hout"), py::arg("Wout"), py::arg("N"),
+           py::arg("pad_y"), py::arg("pad_x"), py::arg("cfg"), py::arg("out_f32"), py::arg("ldc"), py::arg("cofs"),
+           py::arg("bias"), py::arg("act"), py::arg("leak"), py::arg("stats"), py::arg("stream"), py::arg("bkn"),
+           py::arg("kb_valid"), py::arg("splits"), py::arg("bnb_x") = 0, py::arg("bnb_y") = 0,
+           py::arg("bnb_mean") = 0, py::arg("bnb_rstd") = 0, py::arg("bnb_rpg") = 0, py::arg("bnb_act") = 0,
+           py::arg("bnb_leak") = 0.f)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)

@@ -21,10 +21,10 @@ __device__ __forceinline__ float act_ct(float v, float leak) {
 
 // acc[FM][FN] of a (WM x WN)-wave tile, wave (wm, wn), lane (fr, fq). rowoff[BM] (LDS) holds each
 // tile row's output element offset or -1; red[WM][BN][2] and ctile[BM][BN + 8] are LDS scratch.
-template <int ACT, bool VEC, int FM, int FN, int TM, int TN, int BN>
+template <int ACT, bool VEC, int FM, int FN, int TM, int TN, int BN, bool BNB = false>
 __device__ __forceinline__ void frag_epilogue(const f32x4 (&acc)[FM][FN], const IGemmArgs& p, const int* rowoff,
                                               float* red, elem_t* ctile, int wm, int wn, int fr, int fq, int n0,
-                                              bool do_stats) {
+                                              bool do_stats, int m0 = 0) {
   constexpr int CPAD = BN + 8;
   const int N = p.N;
   // the 4 consecutive rows of each M fragment: one 16-byte LDS read per fragment
@@ -42,6 +42,13 @@ __device__ __forceinline__ void frag_epilogue(const f32x4 (&acc)[FM][FN], const 
     const bool nok = n < N;
     const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
     float s = 0.f, s2 = 0.f;
+    float bmu = 0.f, brs = 0.f;
+    const float bslope = p.bnb_act == ACT_LRELU ? p.bnb_leak : 0.f;  // relu / lrelu derivative below 0
+    if constexpr (BNB) {
+      const int g = m0 / p.bnb_rpg;
+      bmu = nok ? p.bnb_mean[g * N + n] : 0.f;
+      brs = nok ? p.bnb_rstd[g * N + n] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -51,8 +58,16 @@ __device__ __forceinline__ void frag_epilogue(const f32x4 (&acc)[FM][FN], const 
         const float v = acc[i][j][r] + bv;
         // statistics of exactly the stored (rounded) tensor: BN forward and backward see one x
         const float vs = f32out ? v : (float)f2bf(v);
-        s += valid ? vs : 0.f;
-        s2 += valid ? vs * vs : 0.f;
+        if constexpr (BNB) {
+          const int idx = valid ? off + p.cofs + n : 0;
+          const float ya = (float)p.bnb_y[idx], xa = (float)p.bnb_x[idx];
+          const float gv = vs * (ya > 0.f ? 1.f : bslope);
+          s += valid ? gv : 0.f;
+          s2 += valid ? gv * (xa - bmu) * brs : 0.f;
+        } else {
+          s += valid ? vs : 0.f;
+          s2 += valid ? vs * vs : 0.f;
+        }
         const float o = act_ct<ACT>(v, p.leak);
         if constexpr (VEC) {
           ctile[(wm * TM + i * 16 + fq * 4 + r) * CPAD + nl] = f2bf(o);
@@ -79,7 +94,11 @@ __device__ __forceinline__ void frag_epilogue(const f32x4 (&acc)[FM][FN], const 
 template <int FM, int FN, int TM, int TN, int BN>
 __device__ __forceinline__ void frag_epilogue_dispatch(const f32x4 (&acc)[FM][FN], const IGemmArgs& p,
                                                        const int* rowoff, float* red, elem_t* ctile, int wm, int wn,
-                                                       int fr, int fq, int n0, bool do_stats, bool vec) {
+                                                       int fr, int fq, int n0, bool do_stats, bool vec, int m0) {
+  if (p.bnb_x) {  // data-gradient GEMM feeding a BN backward: C tile only; stats in vec_store_bnb
+    frag_epilogue<ACT_NONE, true, FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, false);
+    return;
+  }
 #define DCG_EPI(A)                                                                                         \
   if (vec) frag_epilogue<A, true, FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats); \
   else frag_epilogue<A, false, FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats);
@@ -90,6 +109,65 @@ __device__ __forceinline__ void frag_epilogue_dispatch(const f32x4 (&acc)[FM][FN
     default: DCG_EPI(ACT_NONE) break;
   }
 #undef DCG_EPI
+}
+
+// Store pass of a data-gradient GEMM that feeds a BN + activation backward: 16-byte row stores
+// of the C tile (LDS) and, in the same pass, 16-byte loads of the layer's x and y at the same
+// offsets -> per-channel partial sums (sum g, sum g*xhat), g = dL/da * act'(y) -- the statistics
+// the BN backward needs, without a separate pass over three tensors. Each thread owns one fixed
+// 8-channel chunk; row lanes are reduced through LDS scratch (red2, 16 KiB) in a fixed order.
+// Requires elem_t output with N % 8 == 0 (the caller checks) and a tile inside one BN group.
+template <int BM, int BN>
+__device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* rowoff, const elem_t* ctile,
+                                              float* red2, int n0, int m0, float* dst) {
+  constexpr int CPAD = BN + 8, CPR = BN / 8, RL = 256 / CPR;
+  static_assert(256 % CPR == 0, "chunks per row");
+  const int tid = threadIdx.x, c = tid % CPR, rl = tid / CPR;
+  const int N = p.N, n = n0 + 8 * c;
+  const bool nok = n < N;
+  const int g = m0 / p.bnb_rpg;
+  const float slope = p.bnb_act == ACT_LRELU ? p.bnb_leak : 0.f;
+  float mu[8], rs[8], s[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = nok ? p.bnb_mean[g * N + n + i] : 0.f;
+    rs[i] = nok ? p.bnb_rstd[g * N + n + i] : 0.f;
+    s[i] = 0.f;
+    s2[i] = 0.f;
+  }
+  elem_t* C = reinterpret_cast<elem_t*>(p.C);
+  for (int r = rl; r < BM; r += RL) {
+    const int off = rowoff[r];
+    if (off < 0 || !nok) continue;
+    const size_t o = (size_t)off + p.cofs + n;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ctile + r * CPAD + 8 * c);
+    *reinterpret_cast<u32x4*>(C + o) = v;
+    const elem8 dv = __builtin_bit_cast(elem8, v);
+    const elem8 yv = *reinterpret_cast<const elem8*>(p.bnb_y + o);
+    const elem8 xv = *reinterpret_cast<const elem8*>(p.bnb_x + o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float gv = (float)dv[i] * ((float)yv[i] > 0.f ? 1.f : slope);
+      s[i] += gv;
+      s2[i] += gv * ((float)xv[i] - mu[i]) * rs[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red2[(rl * BN + 8 * c + i) * 2 + 0] = s[i];
+    red2[(rl * BN + 8 * c + i) * 2 + 1] = s2[i];
+  }
+  __syncthreads();
+  for (int nl = tid; nl < BN; nl += 256) {
+    if (n0 + nl >= N) continue;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < RL; ++l) {
+      a += red2[(l * BN + nl) * 2 + 0];
+      b += red2[(l * BN + nl) * 2 + 1];
+    }
+    dst[n0 + nl] = a;
+    dst[N + n0 + nl] = b;
+  }
 }
 
 }  // namespace dcg

@@ -235,7 +235,18 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const bool do_stats = p.stats != nullptr;
   // vector store path: elem_t output, whole 8-channel groups, aligned destination
   const bool vec = !p.out_f32 && (BN % 8 == 0) && (N % 8 == 0) && (p.ldc % 8 == 0) && (p.cofs % 8 == 0);
-  frag_epilogue_dispatch<FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats, vec);
+  frag_epilogue_dispatch<FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats, vec, m0);
+  if (p.bnb_x) {  // BN-backward statistics fused into the store pass (epilogue.h)
+    constexpr bool kFits = (BM + 2 * WM * BN) * 4 + BM * CPAD * 2 + 16384 <= 2 * STAGE * 16;
+    if constexpr (kFits) {
+      __syncthreads();
+      float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + BM * CPAD * 2);
+      vec_store_bnb<BM, BN>(p, rowoff, ctile, red2, n0, m0, p.stats + (size_t)(blockIdx.x * p.nphases + phase) * 2 * N);
+    } else {
+      __builtin_trap();  // the host only requests fused statistics on tiles with the LDS for them
+    }
+    return;
+  }
   if (do_stats || vec) __syncthreads();
   if (vec) {
     constexpr int CPR = BN / 8;  // 16-byte chunks per row

@@ -42,6 +42,15 @@ struct IGemmArgs {
   int ablate;               // timing-only builds: bit0 drops A loads, bit1 drops B loads (0 = normal)
   unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime at 4 points (nullptr = off)
   IGemmPhaseK phk[4];       // igemm3: the phase table by value
+  // fused BN-backward statistics (epilogue of the data-gradient GEMM that produces dL/da for a
+  // BN + activation layer): stats become (sum g, sum g*xhat), g = da * act'(y), xhat = (x-mean)*rstd,
+  // instead of (sum v, sum v^2). x / y share C's layout. Tile group = tile row0 / bnb_rpg.
+  const elem_t* bnb_x;
+  const elem_t* bnb_y;
+  const float* bnb_mean;    // [groups][N]
+  const float* bnb_rstd;
+  int bnb_rpg, bnb_act;
+  float bnb_leak;
 };
 
 struct WGradArgs {

@@ -196,16 +196,50 @@ class HipEngine:
 
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
-               cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None, bkn=False, kb_valid=-1):
+               cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None, bkn=False, kb_valid=-1, bnb=None):
         """One conv-shaped GEMM. Bw is a bf16 weight-mirror view; bkn=True reads it as
-        [tap][K][N] (D forward, G dgrad, im2col'd layers), else as [tap][N][K]."""
+        [tap][K][N] (D forward, G dgrad, im2col'd layers), else as [tap][N][K]. bnb = (x, y,
+        mean, rstd, rows_per_group, act): the epilogue also emits the BN-backward partial sums of
+        the layer whose dL/da this GEMM produces (see _dgrad_bnb)."""
         plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn)
         if plan is None:
             raise RuntimeError("no igemm tile for %s (mode %d, N %d, bkn %d)" % (name, mode, N, bkn))
         cfg, splits = plan
+        bx = by = bm = br = 0
+        brpg = bact = 0
+        if bnb is not None:
+            bx, by, bm, br = _p(bnb[0]), _p(bnb[1]), _p(bnb[2]), _p(bnb[3])
+            brpg, bact = bnb[4], bnb[5]
         prog.igemm_ex(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
-                      ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0, int(bkn), kb_valid, splits)
+                      ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0, int(bkn), kb_valid, splits,
+                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak)
         return cfg
+
+    def _dgrad_bnb(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, bn_name, x, y, groups, act, group_offset=0):
+        """Fused BN-backward statistics for the data-gradient GEMM that writes dL/da of BN layer
+        ``bn_name`` (x = its pre-BN input, y = its activation output, same layout as the GEMM
+        output). Returns (igemm kwargs, partials, partials per group) or None when no tile keeps
+        the real/fake groups apart (odd sizes) -- the BN backward then runs its own stats pass."""
+        if os.environ.get("DCGAN_NO_FUSED_BNB") == "1":
+            return None
+        if mode == 1:
+            hq, wq, phases = -(-Hout // 2), -(-Wout // 2), 4
+            if Hout % 2 or Wout % 2:
+                return None
+            M = Bn * hq * wq
+        else:
+            M, phases = Bn * Hout * Wout, 1
+        rpg = M // groups
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rpg, bkn)
+        if plan is None or N % 8 or not H.bnb_fits(plan[0]):
+            return None
+        bm, _ = H.tile_of(plan[0])
+        P = -(-M // bm) * phases
+        part = self._stats_buf(bn_name + ".bwd", P, N)
+        st = self.bn[bn_name]
+        mean, rstd = st["mean"][group_offset:], st["rstd"][group_offset:]
+        kw = dict(stats=part, rows_per_group=rpg, bnb=(x, y, mean, rstd, rpg, act))
+        return kw, part, P // groups
 
     def _deconv_out(self, prog, name, x, w, y, B, L, pad, bias, act):
         """G's output layer: the direct narrow kernel for RGB / gray outputs, else the igemm."""
@@ -335,6 +369,7 @@ class HipEngine:
                         cfg.d_lin_in, 16, _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), 0)
         prog.head_dgrad("d_head.dgrad", _p(self.dl_d), _p(Pd[lin + "/Matrix"]), _p(self.d_da[last.name]), B2,
                         cfg.d_lin_in, 0)
+        fused_next = None  # BN-backward partials emitted by the previous (upper) layer's dgrad GEMM
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
             rows = B2 * L.out_hw ** 2
@@ -342,7 +377,7 @@ class HipEngine:
             dx = self.d_dx[L.name]
             if L.bn:
                 self._bn_bwd(prog, L.bn, self.d_x[L.name], da, a, dx, rows, L.cout, 2, LRELU, Pd, gD,
-                             self.coef[L.bn], write_param_grads=True)
+                             self.coef[L.bn], write_param_grads=True, fused=fused_next)
             else:
                 prog.act_bwd(L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
                 # live bias (no BN after it): db = sum over rows of dx
@@ -357,11 +392,18 @@ class HipEngine:
                 self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
                             gD[L.name + "/w"])
             # data gradient into the previous activation (not needed below layer 0)
+            fused_next = None
             if i > 0:
                 nat = self.wbf_d[L.name + "/w"]
                 P_ = self.dl[i - 1]
+                kw = {}
+                if P_.bn:
+                    r = self._dgrad_bnb(1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.bn,
+                                        self.d_x[P_.name], self.d_a[P_.name], 2, LRELU)
+                    if r is not None:
+                        kw, fused_next = r[0], (r[1], r[2])
                 self._igemm(prog, L.name + ".dgrad", 1, dx, nat, self.d_da[P_.name], B2, L.out_hw, L.out_hw, L.cout,
-                            L.in_hw, L.in_hw, L.cin, pad)
+                            L.in_hw, L.in_hw, L.cin, pad, **kw)
 
     def _colsum(self, prog, name, x, rows, C, dst):
         if C % 8 == 0:
@@ -411,18 +453,24 @@ class HipEngine:
             self._side_open = False
 
     def _bn_bwd(self, prog, name, x, dy, y, dx, rows, C, groups, act, P, grads, coef, write_param_grads,
-                stats_key=None, row_offset_groups=None):
+                stats_key=None, row_offset_groups=None, fused=None):
+        """BN + activation backward. fused = (partials, partials per group) when the producing
+        data-gradient GEMM already emitted the statistics (else a column-stats pass here)."""
         st = self.bn[name]
         mean, rstd = st["mean"], st["rstd"]
         if row_offset_groups is not None:  # fake-half only (group 1)
             mean = mean[row_offset_groups:row_offset_groups + 1]
             rstd = rstd[row_offset_groups:row_offset_groups + 1]
         rpg = rows // groups
-        rpb = self._rows_per_block(rpg, C)
-        Pn = rows // rpb
-        part = self._stats_buf(name + ".bwd", Pn, C)
-        prog.colstats(name + ".bwd_stats", 1, _p(x), _p(dy), _p(y), _p(mean), _p(rstd), act, self.cfg.lrelu_leak,
-                      rows, C, rpb, rpg, _p(part), 0)
+        if fused is not None:
+            part, ppg = fused
+            Pn = ppg * groups
+        else:
+            rpb = self._rows_per_block(rpg, C)
+            Pn = rows // rpb
+            part = self._stats_buf(name + ".bwd", Pn, C)
+            prog.colstats(name + ".bwd_stats", 1, _p(x), _p(dy), _p(y), _p(mean), _p(rstd), act,
+                          self.cfg.lrelu_leak, rows, C, rpb, rpg, _p(part), 0)
         dg = grads[name + "/gamma"] if write_param_grads else None
         db = grads[name + "/beta"] if write_param_grads else None
         prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg), _p(P[name + "/gamma"]),
@@ -439,21 +487,29 @@ class HipEngine:
         half = lambda t: t[B:]  # noqa: E731  fake half of a [2B, ...] buffer
         prog.head_dgrad("g.d_head.dgrad", _p(self.dl_g), _p(Pd[lin + "/Matrix"]), _p(half(self.d_da[last.name])), B,
                         cfg.d_lin_in, 0)
+        fused_next = None
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
             rows = B * L.out_hw ** 2
             da, a, dx = half(self.d_da[L.name]), half(self.d_a[L.name]), half(self.d_dx[L.name])
             if L.bn:
                 self._bn_bwd(prog, L.bn, half(self.d_x[L.name]), da, a, dx, rows, L.cout, 1, LRELU, Pd, None,
-                             self.coef_g[L.bn], write_param_grads=False, row_offset_groups=1)
+                             self.coef_g[L.bn], write_param_grads=False, row_offset_groups=1, fused=fused_next)
             else:
                 prog.act_bwd("g." + L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
             nat = self.wbf_d[L.name + "/w"]
             pad = same_pads(L.in_hw)[0]
+            fused_next = None
             if i > 0:
                 P_ = self.dl[i - 1]
+                kw = {}
+                if P_.bn:
+                    r = self._dgrad_bnb(1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.bn,
+                                        half(self.d_x[P_.name]), half(self.d_a[P_.name]), 1, LRELU, group_offset=1)
+                    if r is not None:
+                        kw, fused_next = r[0], (r[1], r[2])
                 self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, half(self.d_da[P_.name]), B, L.out_hw,
-                            L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
+                            L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, **kw)
             else:
                 if L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
                     prog.narrow_deconv("g." + L.name + ".dgrad_img", _p(dx), _p(nat), 0, _p(self.img_grad), B,
@@ -469,6 +525,8 @@ class HipEngine:
         self._colsum(prog, Lg.name + ".dbias", self.img_g, B * Lg.out_hw ** 2, Lg.cout, gG[Lg.name + "/biases"])
         a_prev = self.g_a[self.gl[-2].name] if n > 1 else self.g_h0
         da_prev = self.g_da[self.gl[-2].name] if n > 1 else self.g_da0
+        x_prev = self.g_x[self.gl[-2].name] if n > 1 else self.g_h0_pre
+        bn_prev = self.gl[-2].bn if n > 1 else "g_bn0"
         padL = same_pads(Lg.out_hw)[0]
         wL = self.wbf_g[Lg.name + "/w"]  # [5,5,co,ci] read as [tap][K=co][N=ci]
         if Lg.cout % 8 != 0:
@@ -476,31 +534,51 @@ class HipEngine:
                            Lg.in_hw, Lg.in_hw, padL, padL, self.kp_g, 0)
             self._wgrad(prog, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
                         0, gG[Lg.name + "/w"])
+            r = self._dgrad_bnb(2, B, 1, 1, self.kp_g, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev, a_prev, 1,
+                                RELU)
+            fused_next = None
+            kw = {}
+            if r is not None:
+                kw, fused_next = r[0], (r[1], r[2])
             self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, wL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
-                        Lg.in_hw, Lg.cin, 0, bkn=True, kb_valid=25 * Lg.cout)
+                        Lg.in_hw, Lg.cin, 0, bkn=True, kb_valid=25 * Lg.cout, **kw)
         else:
             self._wgrad(prog, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
                         Lg.cin, padL, gG[Lg.name + "/w"])
+            r = self._dgrad_bnb(0, B, Lg.out_hw, Lg.out_hw, Lg.cout, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev,
+                                a_prev, 1, RELU)
+            fused_next = None
+            kw = {}
+            if r is not None:
+                kw, fused_next = r[0], (r[1], r[2])
             self._igemm(prog, Lg.name + ".dgrad", 0, self.img_g, wL, da_prev, B, Lg.out_hw, Lg.out_hw, Lg.cout,
-                        Lg.in_hw, Lg.in_hw, Lg.cin, padL, bkn=True)
+                        Lg.in_hw, Lg.in_hw, Lg.cin, padL, bkn=True, **kw)
         for j in range(n - 2, -1, -1):
             L = self.gl[j]
             rows = B * L.out_hw ** 2
             x, a, da, dx = self.g_x[L.name], self.g_a[L.name], self.g_da[L.name], self.g_dx[L.name]
             self._bn_bwd(prog, L.bn, x, da, a, dx, rows, L.cout, 1, RELU, Pg, gG, self.coef[L.bn],
-                         write_param_grads=True)
+                         write_param_grads=True, fused=fused_next)
             src = self.g_a[self.gl[j - 1].name] if j > 0 else self.g_h0
             dsrc = self.g_da[self.gl[j - 1].name] if j > 0 else self.g_da0
+            xsrc = self.g_x[self.gl[j - 1].name] if j > 0 else self.g_h0_pre
+            bsrc = self.gl[j - 1].bn if j > 0 else "g_bn0"
             pad = same_pads(L.out_hw)[0]
             self._wgrad(prog, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
                         gG[L.name + "/w"])
+            r = self._dgrad_bnb(0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc, src, 1,
+                                RELU)
+            fused_next = None
+            kw = {}
+            if r is not None:
+                kw, fused_next = r[0], (r[1], r[2])
             self._igemm(prog, L.name + ".dgrad", 0, dx, self.wbf_g[L.name + "/w"], dsrc, B, L.out_hw, L.out_hw,
-                        L.cout, L.in_hw, L.in_hw, L.cin, pad, bkn=True)
+                        L.cout, L.in_hw, L.in_hw, L.cin, pad, bkn=True, **kw)
         # g_bn0 backward + projection gradients
         C0 = cfg.g_base_ch
         rows0 = B * cfg.g_base_hw ** 2
         self._bn_bwd(prog, "g_bn0", self.g_h0_pre, self.g_da0, self.g_h0, self.g_dx0, rows0, C0, 1, RELU, Pg, gG,
-                     self.coef["g_bn0"], write_param_grads=True)
+                     self.coef["g_bn0"], write_param_grads=True, fused=fused_next)
         prog.linear_wgrad("g_h0_lin.wgrad", _p(self.z), _p(self.g_dx0), _p(gG["g_h0_lin/Matrix"]),
                           _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
 

@@ -78,6 +78,13 @@ def tile_of(cfg: int) -> Tuple[int, int]:
     return IGEMM_CFGS[cfg % 100]
 
 
+def bnb_fits(cfg: int) -> bool:
+    """True when the tile's LDS can hold the fused BN-backward statistics scratch (epilogue.h)."""
+    bm, bn = tile_of(cfg)
+    ns = (3 if cfg < 210 else 2) if cfg >= 200 else 2
+    return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= ns * (bm + bn) * 128
+
+
 WGRAD_CFGS = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64), 4: (32, 64), 5: (64, 32), 6: (32, 32)}
 CU_COUNT = 256
 
