@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <functional>
 #include <memory>
@@ -289,11 +290,34 @@ class Program {
   int bn_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, double count, uintptr_t gamma,
                   uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
                   uintptr_t ema_mean, uintptr_t ema_var, float decay, int stream) {
+    int PS = split_slices(ppg);
+    if (PS > 1) {  // many partial rows: sliced reduction + last-arrival finalize
+      double* ws = nullptr;
+      unsigned* ctr = nullptr;
+      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)groups * ((C + 15) / 16));
+      return add(name, stream, [=](hipStream_t s) {
+        return KF(dcg_bn_finalize_split)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+                                         P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
+                                         P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, ws, ctr, PS, s);
+      });
+    }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_finalize)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                              P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
                              P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, s);
     });
+  }
+  static int split_slices(int ppg) { return ppg > 64 ? std::min(32, (ppg + 63) / 64) : 1; }
+  void alloc_split(double** ws, unsigned** ctr, size_t ws_elems, size_t counters) {
+    void* w = nullptr;
+    void* c = nullptr;
+    HIPCHECK(hipMalloc(&w, ws_elems * sizeof(double)));
+    HIPCHECK(hipMalloc(&c, counters * sizeof(unsigned)));
+    HIPCHECK(hipMemset(c, 0, counters * sizeof(unsigned)));
+    dev_allocs_.push_back(w);
+    dev_allocs_.push_back(c);
+    *ws = reinterpret_cast<double*>(w);
+    *ctr = reinterpret_cast<unsigned*>(c);
   }
   int bn_coef_eval(std::string name, int C, uintptr_t gamma, uintptr_t beta, float eps, uintptr_t mean,
                    uintptr_t var, float debias, uintptr_t scale, uintptr_t shift, int stream) {
@@ -312,6 +336,17 @@ class Program {
   int bn_bwd_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, float count, uintptr_t gamma,
                       uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
                       int stream) {
+    int PS = split_slices(ppg);
+    if (PS > 1) {
+      double* ws = nullptr;
+      unsigned* ctr = nullptr;
+      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)((C + 15) / 16));
+      return add(name, stream, [=](hipStream_t s) {
+        return KF(dcg_bn_bwd_finalize_split)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+                                             P<const float>(mean), P<const float>(rstd), P<float>(dgamma),
+                                             P<float>(dbeta), P<float>(coef), ws, ctr, PS, s);
+      });
+    }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_bwd_finalize)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                                  P<const float>(mean), P<const float>(rstd), P<float>(dgamma), P<float>(dbeta),

@@ -277,6 +277,119 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const elem_t* __restr
   }
 }
 
+// ---------------------------------------------------------------- split finalizes
+// The partial arrays come from the conv epilogues: one row per output tile, up to ~2k rows for
+// a 64-channel layer. A handful of workgroups walking them serially was latency-bound (up to
+// 40 us); here grid.z = PS slices each reduce ~64 rows of 16 channels, write their (double)
+// sums with `sc1` stores, and the workgroup that arrives last (agent-scope counter, reset for
+// the next launch / graph replay) combines the PS slices in slice order -- deterministic -- and
+// runs the finalize. ws: [groups][PS][2][C] doubles; counters: zero-initialised.
+__device__ __forceinline__ void st_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 16);
+}
+__device__ __forceinline__ double ld_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+}
+
+// returns true in the last-arriving workgroup of `expected`; every thread of the block agrees
+__device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned expected, int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = old == expected - 1;
+    if (*flag_lds) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return *flag_lds != 0;
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_split_kernel(
+    const float* __restrict__ part, int ppg, int groups, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    float* __restrict__ scale_out, float* __restrict__ shift_out, float* __restrict__ ema_mean,
+    float* __restrict__ ema_var, float decay, double* ws, unsigned* counters, int PS) {
+  __shared__ int flag;
+  const int cg = blockIdx.x, g = blockIdx.y, ps = blockIdx.z;
+  const int c = cg * 16 + (threadIdx.x & 15);
+  const bool cok = c < C;
+  const int chunk = (ppg + PS - 1) / PS;
+  const int p0 = g * ppg + ps * chunk, p1 = min(g * ppg + ppg, p0 + chunk);
+  double s1, s2;
+  reduce_rows2<double>(part, p0, max(p0, p1), (size_t)2 * C, c, cok, C, s1, s2);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ws, (uint32_t)((size_t)groups * PS * 2 * C * 8));
+  if (threadIdx.x < 16 && cok) {
+    st_sc1_f64(rw, (uint32_t)((((size_t)g * PS + ps) * 2 + 0) * C + c) * 8u, s1);
+    st_sc1_f64(rw, (uint32_t)((((size_t)g * PS + ps) * 2 + 1) * C + c) * 8u, s2);
+  }
+  if (!last_arrival(counters + g * gridDim.x + cg, (unsigned)PS, &flag)) return;
+  if (threadIdx.x >= 16 || !cok) return;
+  double a = 0.0, b = 0.0;
+  for (int q = 0; q < PS; ++q) {
+    a += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 0) * C + c) * 8u);
+    b += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 1) * C + c) * 8u);
+  }
+  const int idx = g * C + c;
+  const double m = a / count;
+  double v = b / count - m * m;
+  if (v < 0.0) v = 0.0;
+  const float mf = (float)m, vf = (float)v;
+  const float r = rsqrtf(vf + eps);
+  mean_out[idx] = mf;
+  rstd_out[idx] = r;
+  const float sc = gamma[c] * r;
+  scale_out[idx] = sc;
+  shift_out[idx] = beta[c] - mf * sc;
+  if (ema_mean) {
+    const float al = 1.f - decay;
+    ema_mean[idx] -= al * (ema_mean[idx] - mf);
+    ema_var[idx] -= al * (ema_var[idx] - vf);
+  }
+}
+
+// backward: slices over (group, rows); the last arrival per 16-channel group (over all groups x
+// slices) forms each group's coefficients and the group-summed dgamma / dbeta.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_split_kernel(
+    const float* __restrict__ part, int ppg, int groups, int C, float count, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ coef, double* ws, unsigned* counters, int PS) {
+  __shared__ int flag;
+  const int cg = blockIdx.x, g = blockIdx.y, ps = blockIdx.z;
+  const int c = cg * 16 + (threadIdx.x & 15);
+  const bool cok = c < C;
+  const int chunk = (ppg + PS - 1) / PS;
+  const int p0 = g * ppg + ps * chunk, p1 = min(g * ppg + ppg, p0 + chunk);
+  double s1, s2;
+  reduce_rows2<double>(part, p0, max(p0, p1), (size_t)2 * C, c, cok, C, s1, s2);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ws, (uint32_t)((size_t)groups * PS * 2 * C * 8));
+  if (threadIdx.x < 16 && cok) {
+    st_sc1_f64(rw, (uint32_t)((((size_t)g * PS + ps) * 2 + 0) * C + c) * 8u, s1);
+    st_sc1_f64(rw, (uint32_t)((((size_t)g * PS + ps) * 2 + 1) * C + c) * 8u, s2);
+  }
+  if (!last_arrival(counters + cg, (unsigned)(PS * groups), &flag)) return;
+  if (threadIdx.x >= 16 || !cok) return;
+  float dg = 0.f, db = 0.f;
+  for (int gg = 0; gg < groups; ++gg) {
+    double a = 0.0, b = 0.0;
+    for (int q = 0; q < PS; ++q) {
+      a += ld_sc1_f64(rw, (uint32_t)((((size_t)gg * PS + q) * 2 + 0) * C + c) * 8u);
+      b += ld_sc1_f64(rw, (uint32_t)((((size_t)gg * PS + q) * 2 + 1) * C + c) * 8u);
+    }
+    const float sg1 = (float)a, sg2 = (float)b;
+    dg += sg2;
+    db += sg1;
+    const float r = rstd[gg * C + c], mu = mean[gg * C + c];
+    const float A = gamma[c] * r;
+    const float c2 = -A * sg2 / count;
+    const float bb = -A * sg1 / count;
+    coef[(gg * 3 + 0) * C + c] = A;
+    coef[(gg * 3 + 1) * C + c] = c2 * r;
+    coef[(gg * 3 + 2) * C + c] = bb - c2 * mu * r;
+  }
+  if (dgamma) dgamma[c] = dg;
+  if (dbeta) dbeta[c] = db;
+}
+
 // ---------------------------------------------------------------- activation backward (no BN)
 // dx = dy * act'(y); 8 per thread + scalar tail
 __global__ __launch_bounds__(256) void act_bwd_kernel(const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
@@ -399,5 +512,23 @@ extern "C" int DCG_API(dcg_sum_partials)(const float* part, int P, int stride, i
 extern "C" int DCG_API(dcg_colsum_small)(const elem_t* x, int R, int C, float* part, int blocks, hipStream_t s) {
   if (C > 16) return -2;
   hipLaunchKernelGGL(colsum_small_kernel, dim3(blocks), dim3(256), 0, s, x, R, C, part);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_bn_finalize_split)(const float* part, int ppg, int groups, int C, double count,
+                                              const float* gamma, const float* beta, float eps, float* mean,
+                                              float* rstd, float* scale, float* shift, float* ema_mean, float* ema_var,
+                                              float decay, double* ws, unsigned* counters, int PS, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_split_kernel, dim3((C + 15) / 16, groups, PS), dim3(256), 0, s, part, ppg, groups, C,
+                     count, gamma, beta, eps, mean, rstd, scale, shift, ema_mean, ema_var, decay, ws, counters, PS);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_bn_bwd_finalize_split)(const float* part, int ppg, int groups, int C, float count,
+                                                  const float* gamma, const float* mean, const float* rstd,
+                                                  float* dgamma, float* dbeta, float* coef, double* ws,
+                                                  unsigned* counters, int PS, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_split_kernel, dim3((C + 15) / 16, groups, PS), dim3(256), 0, s, part, ppg,
+                     groups, C, count, gamma, mean, rstd, dgamma, dbeta, coef, ws, counters, PS);
   return (int)hipGetLastError();
 }

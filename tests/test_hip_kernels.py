@@ -386,3 +386,47 @@ def test_narrow_deconv(B, Hi, Ho, C, N, dtype):
     yc = R.conv2d_same(xg, w.float())
     (gx,) = torch.autograd.grad(yc, xg, x.float())
     close(h.narrow_deconv(x, w, (Ho, Ho)), gx, 1e-2, "narrow as conv dgrad")
+
+
+@pytest.mark.parametrize("P,groups,C", [(2048, 2, 80), (700, 1, 512), (96, 2, 64)])
+def test_bn_finalize_split_paths(P, groups, C):
+    """Many partial rows -> the sliced finalize with a last-arrival combine (counters reset, so a
+    second launch of the same op gives the same bits); compared with float64 sums."""
+    h = H()
+    ext = h.ext()
+    _p = h._p
+    g = torch.Generator().manual_seed(70)
+    part = (torch.randn(P, 2, C, generator=g, dtype=torch.float64) * 3 + 1).abs()
+    part_d = part.float().to(dev)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = (torch.rand(C, generator=g) - 0.5).to(dev)
+    cnt = 1000.0
+    outs = [torch.zeros(groups, C, device=dev) for _ in range(4)]
+    ema_m, ema_v = torch.zeros(groups, C, device=dev), torch.zeros(groups, C, device=dev)
+    pr = ext.Program()
+    pr.bn_finalize("fin", _p(part_d), P // groups, groups, C, cnt, _p(gamma), _p(beta), 1e-5, _p(outs[0]), _p(outs[1]),
+                   _p(outs[2]), _p(outs[3]), _p(ema_m), _p(ema_v), 0.9, 0)
+    h.run(pr)
+    first = [o.clone() for o in outs]
+    h.run(pr)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(first, outs)), "second launch differs (counter reset)"
+    pg = part.reshape(groups, P // groups, 2, C).sum(1)
+    m = pg[:, 0] / cnt
+    v = (pg[:, 1] / cnt - m * m).clamp_min(0)
+    close(outs[0].cpu(), m, 1e-5, "mean")
+    close(outs[1].cpu(), (v + 1e-5).rsqrt(), 1e-4, "rstd")
+    # backward coefficients + group-summed dgamma / dbeta
+    mean, rstd = outs[0], outs[1]
+    dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    coef = torch.zeros(groups, 3, C, device=dev)
+    pr2 = ext.Program()
+    pr2.bn_bwd_finalize("bfin", _p(part_d), P // groups, groups, C, cnt, _p(gamma), _p(mean), _p(rstd), _p(dg), _p(db),
+                        _p(coef), 0)
+    h.run(pr2)
+    torch.cuda.synchronize()
+    close(db.cpu(), pg[:, 0].sum(0), 1e-5, "dbeta")
+    close(dg.cpu(), pg[:, 1].sum(0), 1e-5, "dgamma")
+    A = gamma.double().cpu() * rstd.double().cpu()
+    close(coef[:, 0].cpu(), A, 1e-5, "coef A")
+    close(coef[:, 1].cpu(), -A * pg[:, 1] / cnt * rstd.double().cpu(), 1e-4, "coef x")
