@@ -64,6 +64,19 @@ struct WGradArgs {
   int Hd, Wd;
 };
 
+struct WGrad3Args {                 // wgrad3.hip: 25-tap gather GEMM, in-kernel split-K
+  const elem_t* G; int Hg, Wg, Mc;     // gathered operand [B][Hg][Wg][Mc]
+  const elem_t* Dm; int Nc;            // direct operand [K][Nc]
+  int K, pl, splits, kt_per_split;
+  uint32_t g_bytes, d_bytes;
+  FastDiv fd_hw, fd_w;                 // of Hd*Wd, Wd (pixel decode of k)
+  int Hd, Wd;
+  float* out;                          // final fp32 gradient [25][Mc][Nc] (TF layout), scaled
+  float scale;
+  float* ws;                           // [tiles][splits][BM*BN] fp32 slabs (splits > 1)
+  unsigned* counters;                  // [tiles] arrival counters, zero between launches
+};
+
 }  // namespace dcg
 
 extern "C" {
