@@ -278,6 +278,42 @@ class Program {
     });
   }
 
+  // weight gradient v3 (wgrad3.hip): the 25-tap gather GEMM with the split-K reduction in-kernel,
+  // written scaled straight into the fp32 gradient dst [25][Mc][Nc] -- one launch, no slabs pass
+  int wgrad3(std::string name, uintptr_t G, int Hg, int Wg, int Mc, uintptr_t Dm, int Bn, int Hd, int Wd, int Nc,
+             int pad, int cfg, int splits, uintptr_t dst, float scale, int stream) {
+    int bm = 0, bn = 0, ns = 0;
+    if (dcg_wgrad3_tile(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
+    if (Mc % 8 || Nc % 8) throw std::runtime_error("wgrad3 needs Mc % 8 == 0 and Nc % 8 == 0 (16-byte DMA chunks)");
+    if (splits < 1) throw std::runtime_error("splits must be >= 1");
+    WGrad3Args a{};
+    a.G = P<const elem_t>(G); a.Hg = Hg; a.Wg = Wg; a.Mc = Mc;
+    a.Dm = P<const elem_t>(Dm); a.Nc = Nc;
+    a.K = Bn * Hd * Wd; a.pl = pad; a.splits = splits;
+    const int KT = (a.K + 63) / 64;
+    a.kt_per_split = (KT + splits - 1) / splits;
+    const size_t g_elems = (size_t)Bn * Hg * Wg * Mc, d_elems = (size_t)a.K * Nc;
+    if (g_elems * 2 >= OOB || d_elems * 2 >= OOB)
+      throw std::runtime_error("wgrad3 operand exceeds the 3.875 GiB buffer-descriptor range");
+    a.g_bytes = (uint32_t)(g_elems * 2); a.d_bytes = (uint32_t)(d_elems * 2);
+    a.fd_hw = fastdiv_make(Hd * Wd); a.fd_w = fastdiv_make(Wd); a.Hd = Hd; a.Wd = Wd;
+    a.out = P<float>(dst); a.scale = scale;
+    const size_t tiles = (size_t)((Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * 25;
+    if (splits > 1) {
+      if ((size_t)splits * bm * bn * 4 >= OOB) throw std::runtime_error("wgrad3: split slabs too large");
+      void* ws = nullptr;
+      void* ctr = nullptr;
+      HIPCHECK(hipMalloc(&ws, tiles * splits * (size_t)bm * bn * sizeof(float)));
+      HIPCHECK(hipMalloc(&ctr, tiles * sizeof(unsigned)));
+      HIPCHECK(hipMemset(ctr, 0, tiles * sizeof(unsigned)));
+      dev_allocs_.push_back(ws);
+      dev_allocs_.push_back(ctr);
+      a.ws = reinterpret_cast<float*>(ws);
+      a.counters = reinterpret_cast<unsigned*>(ctr);
+    }
+    return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad3_launch)(&a, cfg, s); });
+  }
+
   // ------------------------------------------------------------------ BN / activations
   int colstats(std::string name, int mode, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                int act, float leak, int R, int C, int rows_per_block, int rows_per_group, uintptr_t part,
@@ -503,7 +539,11 @@ static py::tuple igemm_tile(int cfg) {
   return py::make_tuple(bm, bn);
 }
 static py::tuple wgrad_tile(int cfg) {
-  int bm = 0, bn = 0;
+  int bm = 0, bn = 0, ns = 0;
+  if (cfg >= 300) {
+    if (dcg_wgrad3_tile(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad cfg");
+    return py::make_tuple(bm, bn);
+  }
   if (dcg_wgrad_tile(cfg, &bm, &bn)) throw std::runtime_error("bad cfg");
   return py::make_tuple(bm, bn);
 }
@@ -544,6 +584,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)
+      .def("wgrad3", &Program::wgrad3)
       .def("colstats", &Program::colstats)
       .def("bn_finalize", &Program::bn_finalize)
       .def("bn_coef_eval", &Program::bn_coef_eval)

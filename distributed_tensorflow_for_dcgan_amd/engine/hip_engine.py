@@ -5,15 +5,22 @@ native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buf
 replayed every step -- optionally captured into hipGraphs so a step is a handful of graph
 launches:
 
-  segment A  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
-             2B batch [real | fake] with per-half BN statistics (= the reference's two
-             D calls) -> fused 3-loss BCE -> D backward of d_loss (both halves; D grads final)
-  [DDP]      D-gradient all-reduce starts on the comm stream ...
-  segment B  ... while the g_loss chain runs back through D(fake) (pre-update D weights) into
-             G's backward (G grads final)
-  [DDP]      G-gradient all-reduce
-  segment C  TF-Adam(D), TF-Adam(G) (device beta powers, 1/W folded in), step counter,
-             bf16 re-pack of the updated conv weights for the next step's kernels
+  segment A   z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
+              2B batch [real | fake] with per-half BN statistics (= the reference's two
+              D calls) -> fused 3-loss BCE -> the g_loss chain back through D(fake)
+              (pre-update D weights) into G's backward (G grads final)
+  [DDP]       G-gradient all-reduce starts on the comm stream ...
+  segment B1  ... while D's backward of d_loss runs (both halves): head + top conv layer
+              first, i.e. 76 % of D's gradient bytes (d_h3_conv/w at 64x64) ...
+  [DDP]       ... whose all-reduce overlaps ...
+  segment B2  ... the rest of D's backward (D grads final); small last all-reduce
+  segment C   TF-Adam(G) (its all-reduce is long done), TF-Adam(D), step counter (device
+              beta powers, 1/W folded in); each Adam also writes the bf16/fp16 weight mirror
+              that the next step's kernels read
+
+G's backward finalises its largest gradient (g_h1/w) LAST and D's backward finalises its
+largest FIRST, so running G's backward before D's leaves only a few MB of the 37.8 MB fp32
+exchange exposed -- on xGMI rings the bytes, not the number of calls, set the cost.
 
 Layouts: activations NHWC bf16; master weights fp32 in TF layout inside the flat
 ``ParamSet`` buffers (what the checkpoint writes and DDP reduces); each conv weight also
@@ -419,12 +426,18 @@ class HipEngine:
     def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst):
         K = Bn * Hd * Wd
         taps = 1 if mode == 2 else 25
-        cfg, splits = H.pick_wgrad(Mc, Nc, K, taps)
-        slabs = self._t(splits, taps, Mc, Nc, dtype=torch.float32)
-        self._keep.append(slabs)
         # weight gradients may run on a side stream, concurrently with the data-gradient chain
         # on the main stream (both only read dx / the layer input); see _fork
         self._fork(prog)
+        if mode == 0:  # 25-tap layers: LDS-DMA pipelined kernel, split-K reduced in-kernel
+            plan = H.wgrad3_cfg_for(Mc, Nc, Bn, Hd, Wd, Hg)
+            if plan is not None:
+                prog.wgrad3(name + ".wgrad", _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, plan[0], plan[1],
+                            _p(dst), 1.0, self.SIDE)
+                return
+        cfg, splits = H.pick_wgrad(Mc, Nc, K, taps)
+        slabs = self._t(splits, taps, Mc, Nc, dtype=torch.float32)
+        self._keep.append(slabs)
         prog.wgrad(name + ".wgrad", mode, _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(slabs),
                    _p(dst), dst.numel(), 1.0, self.SIDE)
 

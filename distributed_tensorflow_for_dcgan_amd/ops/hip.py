@@ -206,6 +206,44 @@ def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_
     return cfg, splits
 
 
+WGRAD3_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64)}
+
+
+def pick_wgrad3(Mc: int, Nc: int, K: int, target_blocks: int = 2 * CU_COUNT) -> Optional[Tuple[int, int]]:
+    """(cfg, splits) heuristic for wgrad3.hip (25-tap gather GEMM, in-kernel split-K): the
+    largest tile not wider than the operands, split-K until ~target_blocks workgroups while
+    every split keeps >= 8 k-tiles of 64 pixels. None -> wgrad.hip."""
+    if Mc % 8 or Nc % 8 or Mc < 64 or Nc < 64:
+        return None
+    kt = -(-K // 64)
+    for tid in (0, 1, 2, 3):
+        bm, bn = WGRAD3_TILES[tid]
+        if bm > Mc or bn > Nc:
+            continue
+        tiles = -(-Mc // bm) * -(-Nc // bn) * 25
+        sp = 1
+        while tiles * sp < target_blocks and kt // (2 * sp) >= 8 and sp < 16:
+            sp *= 2
+        return 300 + tid, sp
+    return None
+
+
+def wgrad3_key(Mc: int, Nc: int, Bn: int, Hd: int, Wd: int, Hg: int) -> str:
+    return "w3,%d,%d,%d,%d,%d,%d" % (Mc, Nc, Bn, Hd, Wd, Hg)
+
+
+def wgrad3_cfg_for(Mc: int, Nc: int, Bn: int, Hd: int, Wd: int, Hg: int) -> Optional[Tuple[int, int]]:
+    """(cfg, splits) for a 25-tap weight gradient on wgrad3.hip, or None to keep wgrad.hip:
+    the tuned entry (benchmarks/bench_wgrad.py --write; cfg 0 = wgrad.hip measured faster),
+    else the heuristic."""
+    if os.environ.get("DCGAN_NO_WGRAD3") == "1":
+        return None
+    ent = tuned_table().get(wgrad3_key(Mc, Nc, Bn, Hd, Wd, Hg))
+    if ent is not None:
+        return None if ent[0] == 0 else ent
+    return pick_wgrad3(Mc, Nc, Bn * Hd * Wd)
+
+
 # --------------------------------------------------------------------------- one-shot wrappers
 def _check_bf16(*ts):
     for t in ts:
@@ -344,6 +382,25 @@ def conv_wgrad(g_src: torch.Tensor, dm: torch.Tensor, pad: int, mode: int = 0, c
                out.numel(), 1.0, 0)
     run(prog)
     return out if mode != 2 else out[0]
+
+
+def conv_wgrad3(g_src: torch.Tensor, dm: torch.Tensor, pad: int, cfg: Optional[int] = None,
+                splits: Optional[int] = None, scale: float = 1.0) -> torch.Tensor:
+    """wgrad3.hip: out[25][Mc][Nc] = scale * sum_k G[b,2y+ky-pad,2x+kx-pad,m] * Dm[b,y,x,n] (fp32)."""
+    _check_bf16(g_src, dm)
+    Bn, Hg, Wg, Mc = g_src.shape
+    _, Hd, Wd, Nc = dm.shape
+    if cfg is None or splits is None:
+        plan = pick_wgrad3(Mc, Nc, Bn * Hd * Wd)
+        if plan is None:
+            raise ValueError("no wgrad3 tile for Mc=%d Nc=%d" % (Mc, Nc))
+        cfg = plan[0] if cfg is None else cfg
+        splits = plan[1] if splits is None else splits
+    out = torch.empty(25, Mc, Nc, device=dm.device, dtype=torch.float32)
+    prog = ext().Program(g_src.dtype == torch.float16)
+    prog.wgrad3("wgrad3", _p(g_src), Hg, Wg, Mc, _p(dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(out), scale, 0)
+    run(prog)
+    return out
 
 
 def im2col_s2(x: torch.Tensor, kpad: int) -> torch.Tensor:

@@ -201,6 +201,43 @@ def test_wgrad_conv_and_deconv():
     close(outd.reshape(5, 5, Co, Ci), gwd, 2e-3, "deconv wgrad")
 
 
+@pytest.mark.parametrize("B,Hs,Ci,Co", [(4, 16, 64, 128), (2, 8, 128, 256), (3, 7, 64, 64), (2, 14, 256, 128)])
+def test_wgrad3_conv_and_deconv_all_tiles(B, Hs, Ci, Co):
+    """wgrad3.hip (LDS-DMA pipeline, in-kernel split-K) vs autograd: every tile x LDS-stage
+    config, split-K 1/3/4 (uneven splits, empty-tail splits), conv and deconv operand roles,
+    odd spatial sizes; a second launch of the same recorded op gives the same bits."""
+    h = H()
+    Ho = -(-Hs // 2)
+    pad = (max((Ho - 1) * 2 + 5 - Hs, 0)) // 2
+    x = bf(rnd(B, Hs, Hs, Ci, seed=80))
+    w = rnd(5, 5, Ci, Co, scale=0.05, seed=81).requires_grad_(True)
+    dy = bf(rnd(B, Ho, Ho, Co, seed=82))
+    (gw,) = torch.autograd.grad(R.conv2d_same(x.float(), w), w, dy.float())
+    for cfg in (300, 301, 302, 303, 310, 311, 312, 313):
+        bm, bn = h.WGRAD3_TILES[cfg % 10]
+        for sp in (1, 3, 4):
+            out = h.conv_wgrad3(x, dy, pad, cfg=cfg, splits=sp, scale=0.5)
+            close(out.reshape(5, 5, Ci, Co), 0.5 * gw, 2e-3, "conv wgrad3 cfg%d sp%d" % (cfg, sp))
+    # deconv: Y = deconv(X) [B,Hs,Hs,Co] from X [B,Ho,Ho,Ci]; G-operand = dY (gathered), Dm = X
+    Xd = bf(rnd(B, Ho, Ho, Ci, seed=83))
+    wd = rnd(5, 5, Co, Ci, scale=0.05, seed=84).requires_grad_(True)
+    yd = R.conv2d_transpose_same(Xd.float(), wd, (Hs, Hs))
+    dyd = bf(rnd(B, Hs, Hs, Co, seed=85))
+    (gwd,) = torch.autograd.grad(yd, wd, dyd.float())
+    for cfg in (300, 313):
+        outd = h.conv_wgrad3(dyd, Xd, pad, cfg=cfg, splits=4)
+        close(outd.reshape(5, 5, Co, Ci), gwd, 2e-3, "deconv wgrad3 cfg%d" % cfg)
+    # replay determinism (split-K counters re-armed by the kernel)
+    prog = h.ext().Program()
+    out = torch.empty(25, Ci, Co, device=dev)
+    prog.wgrad3("w3", h._p(x), Hs, Hs, Ci, h._p(dy), B, Ho, Ho, Co, pad, 300, 4, h._p(out), 1.0, 0)
+    h.run(prog)
+    first = out.clone()
+    h.run(prog)
+    torch.cuda.synchronize()
+    assert torch.equal(first, out)
+
+
 def test_wgrad_plain_im2col():
     h = H()
     B, Hs, C, Co = 4, 32, 3, 64
