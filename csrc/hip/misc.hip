@@ -324,34 +324,39 @@ __global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__
 }
 
 // ---------------------------------------------------------------- im2col (stride 2, TF SAME)
-// src elem_t [B][H][W][C] -> dst elem_t [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad
-__global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict__ src, elem_t* __restrict__ dst, int B,
-                                                        int H, int W, int C, int Ho, int Wo, int pl_y, int pl_x,
-                                                        int Kpad) {
-  const int kv = Kpad / 8;
-  const size_t n = (size_t)B * Ho * Wo * kv;
-  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const int v = (int)(i % kv);
-    const size_t row = i / kv;
-    const int ox = (int)(row % Wo);
-    const size_t t1 = row / Wo;
-    const int oy = (int)(t1 % Ho), b = (int)(t1 / Ho);
-    elem8 o;
+// src elem_t [B][H][W][C] -> dst elem_t [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad.
+// One thread per 16-byte output chunk (consecutive threads -> consecutive chunks: fully coalesced
+// stores; the 5x5xC patch reads hit L1/L2). 32-bit index math only, channel count fixed at compile
+// time (CC > 0) so k -> (ky, kx, c) is multiply-shift arithmetic; (b, oy, ox) via FastDiv.
+template <int CC>
+__global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict__ src, elem_t* __restrict__ dst,
+                                                        uint32_t n_chunks, int Crt, int H, int W, FastDiv fd_kv,
+                                                        FastDiv fd_wo, FastDiv fd_ho, int pl_y, int pl_x, int Kpad) {
+  const int C = CC > 0 ? CC : Crt;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n_chunks) return;
+  const uint32_t row = fdiv(i, fd_kv);
+  const int v = (int)(i - row * fd_kv.d);
+  const uint32_t t1 = fdiv(row, fd_wo);
+  const int ox = (int)(row - t1 * fd_wo.d);
+  const uint32_t b = fdiv(t1, fd_ho);
+  const int oy = (int)(t1 - b * fd_ho.d);
+  const elem_t* img = src + (size_t)b * H * W * C;
+  const int iy0 = 2 * oy - pl_y, ix0 = 2 * ox - pl_x;
+  elem8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = v * 8 + j;
-      float val = 0.f;
-      if (k < 25 * C) {
-        const int tap = k / C, c = k - tap * C;
-        const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-        const int iy = 2 * oy + ky - pl_y, ix = 2 * ox + kx - pl_x;
-        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-          val = (float)src[(((size_t)b * H + iy) * W + ix) * C + c];
-      }
-      o[j] = (elem_t)val;
+  for (int j = 0; j < 8; ++j) {
+    const int k = v * 8 + j;
+    elem_t val = (elem_t)0.f;
+    if (k < 25 * C) {
+      const int tap = k / C, c = k - tap * C;
+      const int ky = tap / 5, kx = tap - 5 * ky;
+      const int iy = iy0 + ky, ix = ix0 + kx;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) val = img[(iy * W + ix) * C + c];
     }
-    *reinterpret_cast<u32x4*>(dst + row * Kpad + v * 8) = __builtin_bit_cast(u32x4, o);
+    o[j] = val;
   }
+  *reinterpret_cast<u32x4*>(dst + (size_t)i * 8) = __builtin_bit_cast(u32x4, o);
 }
 
 // ---------------------------------------------------------------- casts
@@ -467,9 +472,20 @@ extern "C" int DCG_API(dcg_philox_uniform)(float* out, size_t n, uint64_t seed, 
 
 extern "C" int DCG_API(dcg_im2col_s2)(const elem_t* src, elem_t* dst, int B, int H, int W, int C, int Ho, int Wo, int pl_y,
                              int pl_x, int Kpad, hipStream_t s) {
-  if (Kpad % 8) return -2;
-  hipLaunchKernelGGL(im2col_s2_kernel, dim3(grid_for((size_t)B * Ho * Wo * (Kpad / 8))), dim3(256), 0, s, src, dst,
-                     B, H, W, C, Ho, Wo, pl_y, pl_x, Kpad);
+  if (Kpad % 8 || Kpad < 25 * C) return -2;
+  const size_t n = (size_t)B * Ho * Wo * (Kpad / 8);
+  if (n >= 0x7fffff00u) return -2;  // 32-bit chunk index
+  const dim3 grid((unsigned)((n + 255) / 256));
+  const dcg::FastDiv fkv = fastdiv_make(Kpad / 8), fwo = fastdiv_make(Wo), fho = fastdiv_make(Ho);
+  if (C == 3)
+    hipLaunchKernelGGL(im2col_s2_kernel<3>, grid, dim3(256), 0, s, src, dst, (uint32_t)n, C, H, W, fkv, fwo, fho, pl_y,
+                       pl_x, Kpad);
+  else if (C == 1)
+    hipLaunchKernelGGL(im2col_s2_kernel<1>, grid, dim3(256), 0, s, src, dst, (uint32_t)n, C, H, W, fkv, fwo, fho, pl_y,
+                       pl_x, Kpad);
+  else
+    hipLaunchKernelGGL(im2col_s2_kernel<0>, grid, dim3(256), 0, s, src, dst, (uint32_t)n, C, H, W, fkv, fwo, fho, pl_y,
+                       pl_x, Kpad);
   return (int)hipGetLastError();
 }
 

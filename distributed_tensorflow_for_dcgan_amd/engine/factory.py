@@ -115,7 +115,7 @@ class ReferenceEngine:
 def build_engine(cfg: DCGANConfig, batch_size: int, device: torch.device, engine: str = "auto",
                  dtype: str = "bf16", seed: int = 0, rank: int = 0, world: int = 1, graph: bool = True,
                  allreduce_dtype: str = "fp32", lr: float = 2e-4, beta1: float = 0.5,
-                 zero_debias: bool = False, bucket_mb: float = 8.0):
+                 zero_debias: bool = False, bucket_mb: float = 32.0):
     if engine == "auto":
         engine = "hip" if device.type == "cuda" and dtype in ("bf16", "fp16") else "reference"
     if engine == "reference":

@@ -60,7 +60,7 @@ class HipEngine:
 
     def __init__(self, cfg: DCGANConfig, batch_size: int, device: torch.device, dtype: str = "bf16",
                  seed: int = 0, lr: float = 2e-4, beta1: float = 0.5, zero_debias: bool = False, rank: int = 0,
-                 world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 8.0,
+                 world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 32.0,
                  rank_seeded_z: bool = True, **_):
         if dtype not in ("bf16", "fp16"):
             raise ValueError("the HIP engine computes in bf16 or fp16 (fp32 master weights / statistics / "
@@ -188,13 +188,16 @@ class HipEngine:
         self.progB = ext.Program(self.f16)
         self.progC = ext.Program(self.f16)
         self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
-        self._build_d_backward_dloss(self.progA)
+        self._build_gloss_and_g_backward(self.progA)
         self._join(self.progA)
-        self._build_gloss_and_g_backward(self.progB)
+        self._build_d_backward_dloss(self.progB)  # sets self._b_split (top layer done)
         self._join(self.progB)
-        self._build_update(self.progC, "d")
+        self._build_update(self.progC, first=True)
         self._c_split = self.progC.size()
-        self._build_update(self.progC, "g")
+        self._build_update(self.progC, first=False)
+        # D-gradient slice final after segment B1: the top conv layer (+ its BN) and the head,
+        # which the ParamSet lays out last
+        self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
         self.progCast = ext.Program(self.f16)  # fp32 masters -> bf16/fp16 mirrors (init / checkpoint load)
         for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
             self.progCast.cast_to_bf16("mirror", _p(ps.flat), 0, _p(pb.flat), ps.flat.numel(), 1.0, 0.0, 0)
@@ -398,6 +401,11 @@ class HipEngine:
             else:
                 self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
                             gD[L.name + "/w"])
+            if i == len(self.dl) - 1:
+                # head + top layer gradients final: DDP splits the segment here so their
+                # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
+                self._join(prog)
+                self._b_split = prog.size()
             # data gradient into the previous activation (not needed below layer 0)
             fused_next = None
             if i > 0:
@@ -596,27 +604,27 @@ class HipEngine:
                           _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
 
     # ---- optimiser (+ bf16 weight mirrors)
-    def _build_update(self, prog, which="dg"):
-        """TF-Adam for D and/or G; each Adam also writes the bf16/fp16 mirror the conv GEMMs
-        read. bf16: the D half comes first so that under DDP it overlaps with the G-gradient
-        all-reduce. fp16: one overflow check over both (all-reduced) gradients gates both
-        Adams, so everything runs in the G half (after the last all-reduce)."""
+    def _build_update(self, prog, first: bool):
+        """TF-Adam for G (first part) and D + the step counter (last part); each Adam also
+        writes the bf16/fp16 mirror the conv GEMMs read. Under DDP the G all-reduce completes
+        first (it was issued before D's backward), so Adam(G) runs while D's last bucket is
+        still on the wire. fp16: one overflow check over both (all-reduced) gradients gates
+        both Adams, so everything runs in the last part."""
         gs = 1.0 / self.world
         od, og = self.opt_d, self.opt_g
         ls = _p(self.loss_scale)
-        if self.f16:
-            if "g" not in which:
-                return
+        do_g = (first and not self.f16) or (not first and self.f16)
+        do_d = not first
+        if self.f16 and do_d:
             prog.nonfinite_check("ls.check_d", _p(self.grad_d.flat), self.grad_d.flat.numel(), ls, 0)
             prog.nonfinite_check("ls.check_g", _p(self.grad_g.flat), self.grad_g.flat.numel(), ls, 0)
-            which = "dg"
-        if "d" in which:
-            prog.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
-                         _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
-                         gs, 0, ls)
-        if "g" in which:
+        if do_g:
             prog.adam_bf("adam_g", _p(self.model.g.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
                          _p(og.v.flat), _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
+                         gs, 0, ls)
+        if do_d:
+            prog.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
+                         _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
                          gs, 0, ls)
             prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
                           _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
@@ -633,29 +641,32 @@ class HipEngine:
 
     def _segments(self):
         """The step as (program, begin, end) segments. Single process: one segment. DDP: the
-        collectives sit between segments -- D-grad all-reduce overlaps G backward (B), the
-        G-grad all-reduce overlaps D's Adam + repack (C[:split])."""
+        collectives sit between segments -- G-grad all-reduce overlaps D's backward (B1, B2),
+        the all-reduce of D's top layer + head overlaps the rest of D's backward (B2), Adam(G)
+        overlaps the last (small) D all-reduce."""
         if self.world == 1 and not self._timing:
             return [[(self.progA, 0, -1), (self.progB, 0, -1), (self.progC, 0, -1)]]
-        return [[(self.progA, 0, -1)], [(self.progB, 0, -1)], [(self.progC, 0, self._c_split)],
-                [(self.progC, self._c_split, -1)]]
+        return [[(self.progA, 0, -1)], [(self.progB, 0, self._b_split)], [(self.progB, self._b_split, -1)],
+                [(self.progC, 0, self._c_split)], [(self.progC, self._c_split, -1)]]
+
+    PHASES = ("fwd+G_bwd", "D_bwd_top", "D_bwd_rest", "wait_allreduce_G", "adam_G", "wait_allreduce_D",
+              "adam_D")
 
     def enable_timing(self) -> None:
-        """Per-phase GPU timers: the step runs as 4 segments with events
+        """Per-phase GPU timers: the step runs as 5 segments with events
         between them. Call before the first train_step (graphs are captured per segment)."""
         if self._graphs:
             raise RuntimeError("enable_timing() must precede the first train_step")
         self._timing = True
-        self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
+        self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self.PHASES) + 1)]
 
     def phase_times(self) -> Dict[str, float]:
         """Milliseconds of the last step's phases (synchronises on its last event)."""
         if not self._timing:
             return {}
         ev = self._ev
-        ev[6].synchronize()
-        names = ("fwd+D_bwd", "G_bwd", "wait_allreduce_D", "adam_D", "wait_allreduce_G", "adam_G")
-        return {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(names)}
+        ev[-1].synchronize()
+        return {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(self.PHASES)}
 
     def _run_segment(self, i, st):
         if self.graph_enabled:
@@ -674,28 +685,36 @@ class HipEngine:
         tick = (lambda i: self._ev[i].record(cs)) if self._timing else (lambda i: None)
         ddp = self.world > 1
         tick(0)
-        self._run_segment(0, st)          # fwd + D backward -> grad_d final
+        self._run_segment(0, st)          # fwd, g_loss chain through D(fake), G backward -> grad_g final
         tick(1)
         if ddp:
-            self._ar_d.launch()
-        self._run_segment(1, st)          # G backward (overlaps the D all-reduce)
+            self._ar_g.launch()
+        self._run_segment(1, st)          # D backward: head + top layer (overlaps the G all-reduce)
         tick(2)
         if ddp:
-            self._ar_g.launch()
-            self._ar_d.wait(scale_in_place=False)
+            self._ar_dtop.launch()
+        self._run_segment(2, st)          # rest of D's backward -> grad_d final
         tick(3)
-        self._run_segment(2, st)          # Adam D -> D bf16 mirror (overlaps the G all-reduce)
-        tick(4)
         if ddp:
+            self._ar_drest.launch()
             self._ar_g.wait(scale_in_place=False)
+        tick(4)
+        self._run_segment(3, st)          # Adam G -> G mirror (overlaps the last D all-reduce)
         tick(5)
-        self._run_segment(3, st)          # Adam G, step counter, G bf16 mirror
+        if ddp:
+            self._ar_dtop.wait(scale_in_place=False)
+            self._ar_drest.wait(scale_in_place=False)
         tick(6)
+        self._run_segment(4, st)          # Adam D, step counter, D mirror
+        tick(7)
 
     def _ensure_comm(self):
-        if self.world > 1 and not hasattr(self, "_ar_d"):
-            self._ar_d = D.GradAllReducer(self.grad_d.flat, self.bucket_mb, self.allreduce_dtype)
-            self._ar_g = D.GradAllReducer(self.grad_g.flat, self.bucket_mb, self.allreduce_dtype)
+        if self.world > 1 and not hasattr(self, "_ar_g"):
+            o = self._d_top_off
+            cs, mb, wd = self.comm_stream, self.bucket_mb, self.allreduce_dtype
+            self._ar_g = D.GradAllReducer(self.grad_g.flat, mb, wd, stream=cs)
+            self._ar_dtop = D.GradAllReducer(self.grad_d.flat[o:], mb, wd, stream=cs)
+            self._ar_drest = D.GradAllReducer(self.grad_d.flat[:o], mb, wd, stream=cs)
 
     def _capture(self):
         """Capture each step segment into its own hipGraph (collectives stay outside, issued

@@ -155,7 +155,7 @@ class GradAllReducer:
     """
 
     def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 8.0, wire_dtype: str = "fp32",
-                 reverse: bool = True):
+                 reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None):
         self.flat = flat_grad
         self.world = world_size()
         esize = 2 if wire_dtype == "bf16" else 4
@@ -163,7 +163,9 @@ class GradAllReducer:
         if reverse:  # gradients of the last layers are final first
             self.buckets = self.buckets[::-1]
         self.wire_dtype = wire_dtype
-        self.stream = torch.cuda.Stream(device=flat_grad.device) if flat_grad.is_cuda else None
+        # reducers of one engine share a comm stream: their collectives run in issue order
+        self.stream = stream if stream is not None else (
+            torch.cuda.Stream(device=flat_grad.device) if flat_grad.is_cuda else None)
         self.wire = (torch.empty(flat_grad.numel(), dtype=torch.bfloat16, device=flat_grad.device)
                      if wire_dtype == "bf16" else None)
         self._works = []

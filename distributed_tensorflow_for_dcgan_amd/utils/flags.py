@@ -59,7 +59,7 @@ EXTRA_FLAGS: List[Tuple[str, str, Any, str]] = [
     ("sample_every", "int", 100, "sample when global_step %% sample_every == 1 (reference: 100)"),
     ("engine", "str", "auto", "auto | hip | reference : which training step implementation"),
     ("graph", "bool", True, "capture the HIP training step into a hipGraph"),
-    ("bucket_mb", "float", 8.0, "gradient all-reduce bucket size in MiB"),
+    ("bucket_mb", "float", 32.0, "gradient all-reduce bucket size in MiB (HIP engine: one call per overlap window)"),
     ("allreduce_dtype", "str", "fp32", "gradient all-reduce wire dtype: fp32 | bf16"),
     ("shard_data", "bool", True, "give every rank a disjoint shard of the input files"),
     ("shuffle_buffer", "int", 10776, "shuffle-buffer min_after_dequeue (reference: 10% of 107,766)"),

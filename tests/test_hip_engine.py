@@ -77,33 +77,13 @@ def test_engine_stagewise(size, c_dim, B, dtype):
     real = (torch.rand(B, size, size, c_dim, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     eng.set_batch(real)
     st = eng._streams()  # main + side stream (weight gradients run concurrently)
-    H.run(eng.progA, st)          # forward + d_loss backward (D grads final)
+    H.run(eng.progA, st)          # forward, g_loss chain through D(fake), G backward (G grads final)
     torch.cuda.synchronize()
     Pd, Pg, gD, gG = eng.model.d, eng.model.g, eng.grad_d, eng.grad_g
     rep = {}
     dl, gl = cfg.d_layers(), cfg.g_layers()
     lin = cfg.d_lin_name
     B2 = 2 * B
-    # head
-    a_last = d64(eng.d_a[dl[-1].name]).reshape(B2, -1)
-    rep["d head dW"] = rel(gD[lin + "/Matrix"].flatten(), a_last.t() @ d64(eng.dl_d))
-    rep["d head da"] = rel(eng.d_da[dl[-1].name].reshape(B2, -1), d64(eng.dl_d)[:, None] * d64(Pd[lin + "/Matrix"]).t())
-    for i in range(len(dl) - 1, -1, -1):
-        L = dl[i]
-        if L.bn:
-            gx, dgam, dbet = bn_act_bwd64(eng.d_x[L.name], eng.d_da[L.name], Pd[L.bn + "/gamma"], Pd[L.bn + "/beta"],
-                                          "lrelu", groups=2)
-            rep["d %s bn dx" % L.name] = rel(eng.d_dx[L.name], gx)
-            rep["d %s dgamma" % L.bn] = rel(gD[L.bn + "/gamma"], dgam)
-            rep["d %s dbeta" % L.bn] = rel(gD[L.bn + "/beta"], dbet)
-        src = eng.d_in if i == 0 else eng.d_a[dl[i - 1].name]
-        gx, gw = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name], "conv", edt=edt)
-        rep["d %s dW" % L.name] = rel(gD[L.name + "/w"], gw)
-        if i > 0:
-            rep["d %s dgrad" % L.name] = rel(eng.d_da[dl[i - 1].name], gx)
-    rep["d h0 dbias"] = rel(gD[dl[0].name + "/biases"], d64(eng.d_dx[dl[0].name]).reshape(-1, dl[0].cout).sum(0))
-    H.run(eng.progB, st)          # g_loss chain + G backward
-    torch.cuda.synchronize()
     for i in range(len(dl) - 1, -1, -1):
         L = dl[i]
         if L.bn:
@@ -138,6 +118,26 @@ def test_engine_stagewise(size, c_dim, B, dtype):
     rep["G bn0 dx"] = rel(eng.g_dx0.reshape(gx.shape), gx)
     rep["G lin dW"] = rel(gG["g_h0_lin/Matrix"], d64(eng.z).t() @ d64(eng.g_dx0))
     rep["G lin db"] = rel(gG["g_h0_lin/bias"], d64(eng.g_dx0).sum(0))
+    H.run(eng.progB, st)          # D backward of d_loss (overwrites the fake halves of d_da / d_dx)
+    torch.cuda.synchronize()
+    # head
+    a_last = d64(eng.d_a[dl[-1].name]).reshape(B2, -1)
+    rep["d head dW"] = rel(gD[lin + "/Matrix"].flatten(), a_last.t() @ d64(eng.dl_d))
+    rep["d head da"] = rel(eng.d_da[dl[-1].name].reshape(B2, -1), d64(eng.dl_d)[:, None] * d64(Pd[lin + "/Matrix"]).t())
+    for i in range(len(dl) - 1, -1, -1):
+        L = dl[i]
+        if L.bn:
+            gx, dgam, dbet = bn_act_bwd64(eng.d_x[L.name], eng.d_da[L.name], Pd[L.bn + "/gamma"], Pd[L.bn + "/beta"],
+                                          "lrelu", groups=2)
+            rep["d %s bn dx" % L.name] = rel(eng.d_dx[L.name], gx)
+            rep["d %s dgamma" % L.bn] = rel(gD[L.bn + "/gamma"], dgam)
+            rep["d %s dbeta" % L.bn] = rel(gD[L.bn + "/beta"], dbet)
+        src = eng.d_in if i == 0 else eng.d_a[dl[i - 1].name]
+        gx, gw = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name], "conv", edt=edt)
+        rep["d %s dW" % L.name] = rel(gD[L.name + "/w"], gw)
+        if i > 0:
+            rep["d %s dgrad" % L.name] = rel(eng.d_da[dl[i - 1].name], gx)
+    rep["d h0 dbias"] = rel(gD[dl[0].name + "/biases"], d64(eng.d_dx[dl[0].name]).reshape(-1, dl[0].cout).sum(0))
     print("\nstagewise relative errors (%dx%dx%d, B=%d, %s):" % (size, size, c_dim, B, dtype))
     for k, v in rep.items():
         print("  %-28s %.5f" % (k, v))

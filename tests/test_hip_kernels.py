@@ -115,6 +115,24 @@ def test_im2col_and_plain_gemm_3ch():
     close(y, ref, 2e-3, "im2col conv")
 
 
+@pytest.mark.parametrize("B,Hs,C,kpad", [(3, 64, 3, 80), (2, 28, 1, 32), (2, 14, 4, 112), (5, 7, 3, 96)])
+def test_im2col_exact(B, Hs, C, kpad):
+    """im2col_s2 is a pure copy: bit-exact against an unfold of the TF-SAME padded input
+    (compile-time C = 3 / 1 paths and the generic one, odd sizes, extra K padding)."""
+    import torch.nn.functional as F
+    h = H()
+    x = bf(rnd(B, Hs, Hs, C, seed=17))
+    col = h.im2col_s2(x, kpad)
+    Ho = -(-Hs // 2)
+    tot = max((Ho - 1) * 2 + 5 - Hs, 0)
+    pl = tot // 2
+    xp = F.pad(x.permute(0, 3, 1, 2).float(), (pl, tot - pl, pl, tot - pl))
+    u = F.unfold(xp, 5, stride=2)  # [B, C*25, Ho*Wo], k = c*25 + tap
+    ref = u.reshape(B, C, 25, Ho * Ho).permute(0, 3, 2, 1).reshape(B * Ho * Ho, 25 * C)
+    assert torch.equal(col[:, :25 * C].float(), ref)
+    assert not col[:, 25 * C:].float().any()
+
+
 IG3 = [200, 201, 202, 203, 204, 205, 210, 211, 212, 213, 214, 215]
 
 
