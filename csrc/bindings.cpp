@@ -120,7 +120,7 @@ class Program {
                int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
                uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
-               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f) {
+               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
     int bm = 0, bn = 0, ns = 0;
     const bool v3 = cfg >= 200;
     if (v3 ? dcg_igemm3_tile(cfg, &bm, &bn, &ns) : dcg_igemm_tile(cfg, &bm, &bn))
@@ -211,13 +211,19 @@ class Program {
       const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 16384 > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
-      if (!stats || bnb_rpg <= 0 || !bnb_y || !bnb_mean || !bnb_rstd)
-        throw std::runtime_error("igemm bnb: needs stats, rows-per-group, y, mean, rstd");
-      for (auto& q : ph)  // tiles must not straddle a BN group (a phase's rows are (b, qy, qx))
-        if (bnb_rpg % bm || q.M % bnb_rpg) throw std::runtime_error("igemm bnb: tile rows must divide the group");
-      a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
-      a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
-      a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
+      if (bnb_store_g) {  // activation backward only (no BN): x, mean, rstd and groups unused
+        if (!stats || !bnb_y) throw std::runtime_error("igemm act-backward store: needs stats and y");
+        a.bnb_x = P<const elem_t>(bnb_y); a.bnb_y = P<const elem_t>(bnb_y);
+        a.bnb_rpg = 1 << 30; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak; a.bnb_store_g = 1;
+      } else {
+        if (!stats || bnb_rpg <= 0 || !bnb_y || !bnb_mean || !bnb_rstd)
+          throw std::runtime_error("igemm bnb: needs stats, rows-per-group, y, mean, rstd");
+        for (auto& q : ph)  // tiles must not straddle a BN group (a phase's rows are (b, qy, qx))
+          if (bnb_rpg % bm || q.M % bnb_rpg) throw std::runtime_error("igemm bnb: tile rows must divide the group");
+        a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
+        a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
+        a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
+      }
     }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
     if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
@@ -326,6 +332,18 @@ class Program {
   int bn_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, double count, uintptr_t gamma,
                   uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
                   uintptr_t ema_mean, uintptr_t ema_var, float decay, int stream) {
+    if (use_rows_fin()) {
+      const int PS = rows_slices(ppg, C);
+      double* ws = nullptr;
+      unsigned* ctr = nullptr;
+      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)groups);
+      return add(name, stream, [=](hipStream_t s) {
+        return KF(dcg_bn_finalize_rows)(0, P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
+                                        P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
+                                        P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, nullptr,
+                                        nullptr, nullptr, ws, ctr, PS, s);
+      });
+    }
     int PS = split_slices(ppg);
     if (PS > 1) {  // many partial rows: sliced reduction + last-arrival finalize
       double* ws = nullptr;
@@ -344,6 +362,16 @@ class Program {
     });
   }
   static int split_slices(int ppg) { return ppg > 64 ? std::min(32, (ppg + 63) / 64) : 1; }
+  // row-wide finalize (bn_finalize_rows_kernel): ~8 partial rows per row lane per slice
+  // measured slower than the 16-channel split finalize on the 64x64 step (+85 us): opt-in only
+  static bool use_rows_fin() {
+    const char* e = getenv("DCGAN_BN_FIN_V2");
+    return e && e[0] == '1';
+  }
+  static int rows_slices(int ppg, int C) {
+    const int lanes = C <= 512 ? std::max(1, 512 / C) : 1;
+    return std::max(1, std::min(64, (ppg + lanes * 8 - 1) / (lanes * 8)));
+  }
   void alloc_split(double** ws, unsigned** ctr, size_t ws_elems, size_t counters) {
     void* w = nullptr;
     void* c = nullptr;
@@ -372,6 +400,18 @@ class Program {
   int bn_bwd_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, float count, uintptr_t gamma,
                       uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
                       int stream) {
+    if (use_rows_fin()) {
+      const int PS = rows_slices(ppg, C);
+      double* ws = nullptr;
+      unsigned* ctr = nullptr;
+      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, 1);
+      return add(name, stream, [=](hipStream_t s) {
+        return KF(dcg_bn_finalize_rows)(1, P<const float>(part), ppg, groups, C, (double)count, P<const float>(gamma),
+                                        nullptr, 0.f, P<float>(mean), P<float>(rstd), nullptr, nullptr, nullptr,
+                                        nullptr, 0.f, P<float>(dgamma), P<float>(dbeta), P<float>(coef), ws, ctr, PS,
+                                        s);
+      });
+    }
     int PS = split_slices(ppg);
     if (PS > 1) {
       double* ws = nullptr;
@@ -401,6 +441,33 @@ class Program {
       return KF(dcg_act_bwd)(P<const elem_t>(dy), P<const elem_t>(y), P<elem_t>(dx), n, act, leak, s);
     });
   }
+  // dx = dy * act'(y) and db = column sums of dx in one launch (last-arrival reduction)
+  int act_bwd_dbias(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, int R, int C, int act, float leak,
+                    uintptr_t db, int stream) {
+    const int max_blocks = 1024;
+    void* part = nullptr;
+    void* ctr = nullptr;
+    HIPCHECK(hipMalloc(&part, (size_t)max_blocks * C * sizeof(float)));
+    HIPCHECK(hipMalloc(&ctr, sizeof(unsigned)));
+    HIPCHECK(hipMemset(ctr, 0, sizeof(unsigned)));
+    dev_allocs_.push_back(part);
+    dev_allocs_.push_back(ctr);
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_act_bwd_dbias)(P<const elem_t>(dy), P<const elem_t>(y), P<elem_t>(dx), R, C, act, leak,
+                                   reinterpret_cast<float*>(part), max_blocks, reinterpret_cast<unsigned*>(ctr),
+                                   P<float>(db), s);
+    });
+  }
+
+  // D head backward (weight + bias + data gradient) in one launch
+  int head_bwd(std::string name, uintptr_t x, uintptr_t dl, uintptr_t w, uintptr_t dx, uintptr_t dW, uintptr_t db,
+               int R, int K, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_head_bwd)(P<const elem_t>(x), P<const float>(dl), P<const float>(w), P<elem_t>(dx), P<float>(dW),
+                              P<float>(db), R, K, s);
+    });
+  }
+
   int sum_partials(std::string name, uintptr_t part, int Pn, int stride, int C, uintptr_t dst, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_sum_partials)(P<const float>(part), Pn, stride, C, P<float>(dst), s);
@@ -420,10 +487,13 @@ class Program {
                           P<float>(prob), P<const float>(ls), s);
     });
   }
+  // stats (optional): BN partial statistics of the output, channel = column % C ->
+  // [(B / 8) * (N / C)][2][C] partial rows (the row block of the kernel is 8)
   int linear_fwd(std::string name, uintptr_t z, uintptr_t W, uintptr_t b, uintptr_t out, int B, int K, int N,
-                 int stream) {
+                 int stream, uintptr_t stats = 0, int C = 0) {
     return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_linear_fwd)(P<const float>(z), P<const float>(W), P<const float>(b), P<elem_t>(out), B, K, N, s);
+      return KF(dcg_linear_fwd)(P<const float>(z), P<const float>(W), P<const float>(b), P<elem_t>(out), B, K, N,
+                                P<float>(stats), C, s);
     });
   }
   int linear_wgrad(std::string name, uintptr_t z, uintptr_t dh, uintptr_t dW, uintptr_t db, int B, int K, int N,
@@ -580,7 +650,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("bias"), py::arg("act"), py::arg("leak"), py::arg("stats"), py::arg("stream"), py::arg("bkn"),
            py::arg("kb_valid"), py::arg("splits"), py::arg("bnb_x") = 0, py::arg("bnb_y") = 0,
            py::arg("bnb_mean") = 0, py::arg("bnb_rstd") = 0, py::arg("bnb_rpg") = 0, py::arg("bnb_act") = 0,
-           py::arg("bnb_leak") = 0.f)
+           py::arg("bnb_leak") = 0.f, py::arg("bnb_store_g") = 0)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)
@@ -593,10 +663,14 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("bn_bwd_apply", &Program::bn_bwd_apply)
       .def("act_bwd", &Program::act_bwd)
       .def("sum_partials", &Program::sum_partials)
+      .def("act_bwd_dbias", &Program::act_bwd_dbias)
+      .def("head_bwd", &Program::head_bwd)
       .def("colsum_small", &Program::colsum_small)
       .def("gan_loss", &Program::gan_loss, py::arg("name"), py::arg("logits"), py::arg("B"), py::arg("out"),
            py::arg("dl_d"), py::arg("dl_g"), py::arg("prob"), py::arg("stream"), py::arg("ls") = 0)
-      .def("linear_fwd", &Program::linear_fwd)
+      .def("linear_fwd", &Program::linear_fwd, py::arg("name"), py::arg("z"), py::arg("W"), py::arg("b"),
+           py::arg("out"), py::arg("B"), py::arg("K"), py::arg("N"), py::arg("stream"), py::arg("stats") = 0,
+           py::arg("C") = 0)
       .def("linear_wgrad", &Program::linear_wgrad)
       .def("gemv_head", &Program::gemv_head)
       .def("head_dgrad", &Program::head_dgrad)

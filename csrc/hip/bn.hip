@@ -95,9 +95,17 @@ __global__ __launch_bounds__(256) void colstats_kernel(int mode, const elem_t* _
     }
   }
   __syncthreads();
+  int nl = lanes;
+  if ((lanes & (lanes - 1)) == 0) {  // pairwise tree over the row lanes (fixed order)
+    for (int h = lanes / 2; h > 0; h >>= 1) {
+      for (int q = threadIdx.x; q < h * C * 2; q += 256) red[q] += red[q + h * C * 2];
+      __syncthreads();
+    }
+    nl = 1;
+  }
   for (int c = threadIdx.x; c < C; c += 256) {
     float a = 0.f, b = 0.f;
-    for (int l = 0; l < lanes; ++l) { a += red[(l * C + c) * 2]; b += red[(l * C + c) * 2 + 1]; }
+    for (int l = 0; l < nl; ++l) { a += red[(l * C + c) * 2]; b += red[(l * C + c) * 2 + 1]; }
     part[(size_t)blockIdx.x * 2 * C + c] = a;
     part[(size_t)blockIdx.x * 2 * C + C + c] = b;
   }
@@ -290,6 +298,12 @@ __device__ __forceinline__ void st_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t of
 __device__ __forceinline__ double ld_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
 }
+__device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 16);
+}
+__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
 
 // returns true in the last-arriving workgroup of `expected`; every thread of the block agrees
 __device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned expected, int* flag_lds) {
@@ -390,6 +404,132 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_split_kernel(
   if (dbeta) dbeta[c] = db;
 }
 
+// ---------------------------------------------------------------- row-wide finalizes (v2)
+// Same math as the split finalizes above, different reduction layout: a workgroup owns a slice
+// of partial ROWS and all 2C columns of them (16-byte loads along the row; 256 / (C/2) rows in
+// flight per pass), instead of 16 channels x a slice (64-byte row segments). Per-thread double
+// accumulators, a fixed-order LDS tree over the row lanes, one double row per slice in ws
+// (`sc1` stores); the last-arriving slice (agent counter, re-armed) combines the slices in
+// slice order and runs the finalize for every channel. grid = (PS, groups).
+//   MODE 0: BN forward  -- mean / rstd / scale / shift (+ EMA) per group; counter per group.
+//   MODE 1: BN backward -- per-group coefficients + dgamma / dbeta summed over the groups;
+//           one counter for all (PS x groups) workgroups.
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_finalize_rows_kernel(
+    const float* __restrict__ part, int ppg, int groups, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ mean_io, float* __restrict__ rstd_io,
+    float* __restrict__ scale_out, float* __restrict__ shift_out, float* __restrict__ ema_mean,
+    float* __restrict__ ema_var, float decay, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ coef, double* ws, unsigned* counters) {
+  __shared__ double red[1024];
+  __shared__ int flag;
+  const int PS = gridDim.x, ps = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const int V4 = C >> 1;  // float4 columns of a partial row [2][C]
+  const int chunk = (ppg + PS - 1) / PS;
+  const int p0 = g * ppg + ps * chunk, p1 = min(g * ppg + ppg, p0 + chunk);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ws, (uint32_t)((size_t)groups * PS * 2 * C * 8));
+  const size_t wrow = ((size_t)g * PS + ps) * 2 * C;
+  if (V4 <= 256) {
+    const int lanes = 256 / V4, c4 = tid % V4, ln = tid / V4;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if (ln < lanes) {
+      int p = p0 + ln;
+      for (; p + 3 * lanes < p1; p += 4 * lanes) {  // 4 rows in flight
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(part + (size_t)(p + u * lanes) * 2 * C + 4 * c4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
+      }
+      for (; p < p1; p += lanes) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(part + (size_t)p * 2 * C + 4 * c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[ln * 2 * C + 4 * c4 + e] = a[e];
+    }
+    __syncthreads();
+    int nl = lanes;
+    if ((lanes & (lanes - 1)) == 0) {
+      for (int h = lanes / 2; h > 0; h >>= 1) {
+        for (int q = tid; q < h * 2 * C; q += 256) red[q] += red[q + h * 2 * C];
+        __syncthreads();
+      }
+      nl = 1;
+    }
+    for (int col = tid; col < 2 * C; col += 256) {
+      double t = 0.0;
+      for (int l = 0; l < nl; ++l) t += red[l * 2 * C + col];
+      st_sc1_f64(rw, (uint32_t)((wrow + col) * 8), t);
+    }
+  } else {  // wide rows (C > 512): one row lane, 256-column passes
+    for (int c4 = tid; c4 < V4; c4 += 256) {
+      double a[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int p = p0; p < p1; ++p) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(part + (size_t)p * 2 * C + 4 * c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st_sc1_f64(rw, (uint32_t)((wrow + 4 * c4 + e) * 8), a[e]);
+    }
+  }
+  if (MODE == 0) {
+    if (!last_arrival(counters + g, (unsigned)PS, &flag)) return;
+    for (int c = tid; c < C; c += 256) {
+      double a = 0.0, b = 0.0;
+      for (int q = 0; q < PS; ++q) {
+        a += ld_sc1_f64(rw, (uint32_t)(((((size_t)g * PS + q) * 2 + 0) * C + c) * 8));
+        b += ld_sc1_f64(rw, (uint32_t)(((((size_t)g * PS + q) * 2 + 1) * C + c) * 8));
+      }
+      const int idx = g * C + c;
+      const double m = a / count;
+      double v = b / count - m * m;
+      if (v < 0.0) v = 0.0;
+      const float mf = (float)m, vf = (float)v;
+      const float r = rsqrtf(vf + eps);
+      mean_io[idx] = mf;
+      rstd_io[idx] = r;
+      const float sc = gamma[c] * r;
+      scale_out[idx] = sc;
+      shift_out[idx] = beta[c] - mf * sc;
+      if (ema_mean) {  // TF ExponentialMovingAverage: shadow -= (1 - decay) * (shadow - value)
+        const float al = 1.f - decay;
+        ema_mean[idx] -= al * (ema_mean[idx] - mf);
+        ema_var[idx] -= al * (ema_var[idx] - vf);
+      }
+    }
+  } else {
+    if (!last_arrival(counters, (unsigned)(PS * groups), &flag)) return;
+    const float cnt = (float)count;
+    for (int c = tid; c < C; c += 256) {
+      float dg = 0.f, db = 0.f;
+      for (int gg = 0; gg < groups; ++gg) {
+        double a = 0.0, b = 0.0;
+        for (int q = 0; q < PS; ++q) {
+          a += ld_sc1_f64(rw, (uint32_t)(((((size_t)gg * PS + q) * 2 + 0) * C + c) * 8));
+          b += ld_sc1_f64(rw, (uint32_t)(((((size_t)gg * PS + q) * 2 + 1) * C + c) * 8));
+        }
+        const float sg1 = (float)a, sg2 = (float)b;
+        dg += sg2;
+        db += sg1;
+        const float r = rstd_io[gg * C + c], mu = mean_io[gg * C + c];
+        const float A = gamma[c] * r;
+        const float c2 = -A * sg2 / cnt;
+        const float bb = -A * sg1 / cnt;
+        coef[(gg * 3 + 0) * C + c] = A;
+        coef[(gg * 3 + 1) * C + c] = c2 * r;
+        coef[(gg * 3 + 2) * C + c] = bb - c2 * mu * r;
+      }
+      if (dgamma) dgamma[c] = dg;
+      if (dbeta) dbeta[c] = db;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- activation backward (no BN)
 // dx = dy * act'(y); 8 per thread + scalar tail
 __global__ __launch_bounds__(256) void act_bwd_kernel(const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
@@ -432,6 +572,139 @@ __global__ __launch_bounds__(256) void colsum_small_kernel(const elem_t* __restr
     for (int t = 0; t < 256; ++t) a += red[t][threadIdx.x];
     part[blockIdx.x * C + threadIdx.x] = a;
   }
+}
+
+// ---------------------------------------------------------------- activation backward + bias gradient
+// dx = dy * act'(y) over [R][C] and db[c] = sum_r dx[r][c] (of the stored, rounded dx) in ONE
+// launch, replacing act_bwd + a column-sum pass + a partials pass: every block writes its
+// partial column sums, the last block to arrive (counter) reduces them in block order
+// (deterministic) and re-arms the counter for the next replay.
+//   CC = 0: C % 8 == 0; thread = (row lane, 8-channel chunk), 16-byte loads / stores.
+//   CC = 1 / 3: image tensors; thread = 8 consecutive elements, channel = element index % CC.
+template <int CC>
+__global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __restrict__ dy,
+                                                            const elem_t* __restrict__ y, elem_t* __restrict__ dx,
+                                                            int R, int C, int per_block, int act, float leak,
+                                                            float* __restrict__ part, unsigned* __restrict__ counter,
+                                                            float* __restrict__ db) {
+  __shared__ float red[2048];
+  const int tid = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t prs = make_rsrc(part, (uint32_t)(gridDim.x * C * 4));
+  if constexpr (CC == 0) {
+    const int C8 = C >> 3, RL = 256 / C8, c = tid % C8, rl = tid / C8;
+    const int r0 = blockIdx.x * per_block, r1 = min(R, r0 + per_block);
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    if (rl < RL) {
+      // 4 rows per iteration, all loads issued before any use (memory-level parallelism)
+      for (int rb = r0 + rl; rb < r1; rb += 4 * RL) {
+        u32x4 dvv[4], yvv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rb + u * RL;
+          const size_t o = (size_t)(r < r1 ? r : r0) * C + 8 * c;
+          dvv[u] = *reinterpret_cast<const u32x4*>(dy + o);
+          yvv[u] = *reinterpret_cast<const u32x4*>(y + o);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rb + u * RL;
+          if (r >= r1) break;
+          const elem8 dv = __builtin_bit_cast(elem8, dvv[u]), yv = __builtin_bit_cast(elem8, yvv[u]);
+          elem8 out;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            out[i] = f2bf((float)dv[i] * act_grad_from_out((float)yv[i], act, leak));
+            s[i] += (float)out[i];
+          }
+          *reinterpret_cast<u32x4*>(dx + (size_t)r * C + 8 * c) = __builtin_bit_cast(u32x4, out);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[rl * C + 8 * c + i] = s[i];
+    }
+    __syncthreads();
+    // pairwise tree over the RL row lanes (fixed order, log2(RL) LDS rounds)
+    for (int h = RL / 2; h > 0; h >>= 1) {
+      for (int q = tid; q < h * C; q += 256) red[q] += red[q + h * C];
+      __syncthreads();
+    }
+    for (int cc = tid; cc < C; cc += 256) st_sc1_f32(prs, (uint32_t)(blockIdx.x * C + cc) * 4u, red[cc]);
+  } else {
+    const size_t n = (size_t)R * CC;
+    const size_t e0 = (size_t)blockIdx.x * per_block, e1 = min(n, e0 + per_block);  // per_block % 8 == 0
+    float s[CC];
+#pragma unroll
+    for (int i = 0; i < CC; ++i) s[i] = 0.f;
+    // full 8-element chunks: 2 per iteration, loads first; the scalar tail after
+    const uint32_t nfull = (uint32_t)((min(e1, n & ~(size_t)7) - min(e0, n & ~(size_t)7)) / 8);
+    for (uint32_t q0 = tid; q0 < nfull; q0 += 2 * 256) {
+      u32x4 dvv[2], yvv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t q = q0 + u * 256 < nfull ? q0 + u * 256 : q0;
+        dvv[u] = *reinterpret_cast<const u32x4*>(dy + e0 + 8 * (size_t)q);
+        yvv[u] = *reinterpret_cast<const u32x4*>(y + e0 + 8 * (size_t)q);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t q = q0 + u * 256;
+        if (q >= nfull) break;
+        const size_t e = e0 + 8 * (size_t)q;
+        int ch = (int)((uint32_t)(e % CC));
+        const elem8 dv = __builtin_bit_cast(elem8, dvv[u]), yv = __builtin_bit_cast(elem8, yvv[u]);
+        elem8 out;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          out[i] = f2bf((float)dv[i] * act_grad_from_out((float)yv[i], act, leak));
+          const float v = (float)out[i];
+#pragma unroll
+          for (int k = 0; k < CC; ++k) s[k] += ch == k ? v : 0.f;
+          ch = ch == CC - 1 ? 0 : ch + 1;
+        }
+        *reinterpret_cast<u32x4*>(dx + e) = __builtin_bit_cast(u32x4, out);
+      }
+    }
+    for (size_t e = e0 + 8 * (size_t)nfull + tid; e < e1; e += 256) {  // tail (< 8 elements)
+      const int ch = (int)(e % CC);
+      const elem_t o = f2bf((float)dy[e] * act_grad_from_out((float)y[e], act, leak));
+      dx[e] = o;
+#pragma unroll
+      for (int k = 0; k < CC; ++k) s[k] += ch == k ? (float)o : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < CC; ++q) {  // butterfly within each wave, then the 4 waves in order
+      const float w = wave_sum(s[q]);
+      if ((tid & 63) == 0) red[(tid >> 6) * CC + q] = w;
+    }
+    __syncthreads();
+    if (tid < CC)
+      st_sc1_f32(prs, (uint32_t)(blockIdx.x * CC + tid) * 4u, red[tid] + red[CC + tid] + red[2 * CC + tid] + red[3 * CC + tid]);
+  }
+  // ---- last-arrival reduction of the partials [gridDim.x][C]: the partials were written with
+  // plain stores; a device-scope __threadfence() here would write back the whole XCD L2 in
+  // every block (measured: 30 us for this kernel). Instead: vmcnt(0) + relaxed agent-scope
+  // counter (last_arrival) and the partials re-read with `sc1` loads that bypass the
+  // (non-coherent) L1 of this CU; the writers' L2 lines are written through by the sc1 store
+  // policy below (partials are stored with st_sc1 in the two paths above).
+  __shared__ int flag_s;
+  if (!last_arrival(counter, gridDim.x, &flag_s)) return;
+  const int nb = gridDim.x;
+  const int G = 256 / C;  // block groups summed in parallel, then combined in group order
+  const int c = tid % C, g = tid / C;
+  float a = 0.f;
+  if (g < G)
+    for (int b = g; b < nb; b += G) a += ld_sc1_f32(prs, (uint32_t)(b * C + c) * 4u);
+  __syncthreads();
+  if (g < G) red[tid] = a;
+  __syncthreads();
+  if (tid < C) {  // C <= 256 (launcher)
+    float t = 0.f;
+    for (int q = 0; q < G; ++q) t += red[q * C + tid];
+    db[tid] = t;
+  }
+  if (tid == 0) *counter = 0u;
 }
 
 }  // namespace dcg
@@ -530,5 +803,53 @@ extern "C" int DCG_API(dcg_bn_bwd_finalize_split)(const float* part, int ppg, in
                                                   unsigned* counters, int PS, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_split_kernel, dim3((C + 15) / 16, groups, PS), dim3(256), 0, s, part, ppg,
                      groups, C, count, gamma, mean, rstd, dgamma, dbeta, coef, ws, counters, PS);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_act_bwd_dbias)(const elem_t* dy, const elem_t* y, elem_t* dx, int R, int C, int act,
+                                          float leak, float* part, int max_blocks, unsigned* counter, float* db,
+                                          hipStream_t s) {
+  int per_block = 0, blocks = 0;
+  if (C % 8 == 0) {
+    if (C > 256 || 256 % (C / 8)) return -2;
+    const int RL = 256 / (C / 8);
+    per_block = RL * 16;  // 16 rows per thread
+    blocks = (R + per_block - 1) / per_block;
+    if (blocks > max_blocks) { per_block = (R + max_blocks - 1) / max_blocks; blocks = (R + per_block - 1) / per_block; }
+    hipLaunchKernelGGL(act_bwd_dbias_kernel<0>, dim3(blocks), dim3(256), 0, s, dy, y, dx, R, C, per_block, act, leak,
+                       part, counter, db);
+  } else if (C == 1 || C == 3) {
+    const size_t n = (size_t)R * C;
+    per_block = 8 * 256 * 2;  // 2 chunks of 8 per thread
+    blocks = (int)((n + per_block - 1) / per_block);
+    if (blocks > max_blocks) {
+      per_block = (int)(((n + max_blocks - 1) / max_blocks + 7) / 8 * 8);
+      blocks = (int)((n + per_block - 1) / per_block);
+    }
+    if (C == 1)
+      hipLaunchKernelGGL(act_bwd_dbias_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, y, dx, R, C, per_block, act,
+                         leak, part, counter, db);
+    else
+      hipLaunchKernelGGL(act_bwd_dbias_kernel<3>, dim3(blocks), dim3(256), 0, s, dy, y, dx, R, C, per_block, act,
+                         leak, part, counter, db);
+  } else {
+    return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_bn_finalize_rows)(int mode, const float* part, int ppg, int groups, int C, double count,
+                                             const float* gamma, const float* beta, float eps, float* mean, float* rstd,
+                                             float* scale, float* shift, float* ema_mean, float* ema_var, float decay,
+                                             float* dgamma, float* dbeta, float* coef, double* ws, unsigned* counters,
+                                             int PS, hipStream_t s) {
+  if (C % 2 || (C / 2 <= 256 && 2 * C * (256 / (C / 2)) > 1024)) return -2;
+  const dim3 grid(PS, groups);
+  if (mode == 0)
+    hipLaunchKernelGGL(bn_finalize_rows_kernel<0>, grid, dim3(256), 0, s, part, ppg, groups, C, count, gamma, beta, eps,
+                       mean, rstd, scale, shift, ema_mean, ema_var, decay, dgamma, dbeta, coef, ws, counters);
+  else
+    hipLaunchKernelGGL(bn_finalize_rows_kernel<1>, grid, dim3(256), 0, s, part, ppg, groups, C, count, gamma, beta, eps,
+                       mean, rstd, scale, shift, ema_mean, ema_var, decay, dgamma, dbeta, coef, ws, counters);
   return (int)hipGetLastError();
 }

@@ -111,6 +111,17 @@ __device__ __forceinline__ void frag_epilogue_dispatch(const f32x4 (&acc)[FM][FN
 #undef DCG_EPI
 }
 
+// Pairwise tree over the RL row lanes of red2[RL][BN][2] (fixed order: deterministic; log2(RL)
+// LDS rounds instead of an RL-long dependent chain of LDS reads). Result in red2[0][BN][2].
+template <int RL, int BN>
+__device__ __forceinline__ void lane_tree(float* red2) {
+#pragma unroll
+  for (int h = RL / 2; h > 0; h >>= 1) {
+    for (int q = threadIdx.x; q < h * BN * 2; q += 256) red2[q] += red2[q + h * BN * 2];
+    __syncthreads();
+  }
+}
+
 // Store pass of a data-gradient GEMM that feeds a BN + activation backward: 16-byte row stores
 // of the C tile (LDS) and, in the same pass, 16-byte loads of the layer's x and y at the same
 // offsets -> per-channel partial sums (sum g, sum g*xhat), g = dL/da * act'(y) -- the statistics
@@ -127,6 +138,37 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
   const bool nok = n < N;
   const int g = m0 / p.bnb_rpg;
   const float slope = p.bnb_act == ACT_LRELU ? p.bnb_leak : 0.f;
+  if (p.bnb_store_g) {  // activation backward only: store g, partial sums of the stored g
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    elem_t* C = reinterpret_cast<elem_t*>(p.C);
+    for (int r = rl; r < BM; r += RL) {
+      const int off = rowoff[r];
+      if (off < 0 || !nok) continue;
+      const size_t o = (size_t)off + p.cofs + n;
+      const elem8 dv = __builtin_bit_cast(elem8, *reinterpret_cast<const u32x4*>(ctile + r * CPAD + 8 * c));
+      const elem8 yv = *reinterpret_cast<const elem8*>(p.bnb_y + o);
+      elem8 gv;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float yy = (float)yv[i];
+        gv[i] = f2bf((float)dv[i] * (p.bnb_act == ACT_TANH ? 1.f - yy * yy : (yy > 0.f ? 1.f : slope)));
+        s[i] += (float)gv[i];
+      }
+      *reinterpret_cast<u32x4*>(C + o) = __builtin_bit_cast(u32x4, gv);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red2[(rl * BN + 8 * c + i) * 2 + 0] = s[i];
+    __syncthreads();
+    lane_tree<RL, BN>(red2);
+    for (int nl = tid; nl < BN; nl += 256) {
+      if (n0 + nl >= N) continue;
+      dst[n0 + nl] = red2[nl * 2 + 0];
+      dst[N + n0 + nl] = 0.f;
+    }
+    return;
+  }
   float mu[8], rs[8], s[8], s2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -158,15 +200,11 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
     red2[(rl * BN + 8 * c + i) * 2 + 1] = s2[i];
   }
   __syncthreads();
+  lane_tree<RL, BN>(red2);
   for (int nl = tid; nl < BN; nl += 256) {
     if (n0 + nl >= N) continue;
-    float a = 0.f, b = 0.f;
-    for (int l = 0; l < RL; ++l) {
-      a += red2[(l * BN + nl) * 2 + 0];
-      b += red2[(l * BN + nl) * 2 + 1];
-    }
-    dst[n0 + nl] = a;
-    dst[N + n0 + nl] = b;
+    dst[n0 + nl] = red2[nl * 2 + 0];
+    dst[N + n0 + nl] = red2[nl * 2 + 1];
   }
 }
 

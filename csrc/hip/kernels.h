@@ -51,6 +51,9 @@ struct IGemmArgs {
   const float* bnb_rstd;
   int bnb_rpg, bnb_act;
   float bnb_leak;
+  // activation-only backward (layer without BN): store g = dL/da * act'(y) instead of dL/da and
+  // emit (sum g, 0) per channel -- the bias gradient partials. bnb_x aliases y, mean/rstd unused.
+  int bnb_store_g;
 };
 
 struct WGradArgs {

@@ -53,11 +53,14 @@ __global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------- linear: out = z @ W + b
-// z fp32 [B][K], W fp32 [K][N], out elem_t [B][N]; block = 256 columns x RB rows
+// z fp32 [B][K], W fp32 [K][N], out elem_t [B][N]; block = 256 columns x RB rows.
+// Latency-bound (each thread walks K = 100 W rows): 20 independent W loads in flight.
+// stats != nullptr: also the BN partial statistics of the stored (rounded) output, channel =
+// column % C, one partial row per (row block, column / C) -> part[P][2][C] (no colstats pass).
 template <int RB>
 __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ z, const float* __restrict__ W,
                                                          const float* __restrict__ bias, elem_t* __restrict__ out,
-                                                         int B, int K, int N) {
+                                                         int B, int K, int N, float* __restrict__ stats, int C) {
   extern __shared__ float zs[];  // [RB][K]
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * RB;
@@ -70,14 +73,14 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
   float acc[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) acc[r] = 0.f;
-  // 8 independent W loads in flight per thread (the loop is latency-, not FLOP-bound)
+  constexpr int KU = 20;
   int k = 0;
-  for (; k + 8 <= K; k += 8) {
-    float w[8];
+  for (; k + KU <= K; k += KU) {
+    float w[KU];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = W[(size_t)(k + u) * N + n];
+    for (int u = 0; u < KU; ++u) w[u] = W[(size_t)(k + u) * N + n];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < KU; ++u)
 #pragma unroll
       for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k + u] * w[u];
   }
@@ -87,9 +90,22 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
     for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k] * w;
   }
   const float b = bias ? bias[n] : 0.f;
+  float s = 0.f, s2 = 0.f;
 #pragma unroll
   for (int r = 0; r < RB; ++r)
-    if (r0 + r < B) out[(size_t)(r0 + r) * N + n] = (elem_t)(acc[r] + b);
+    if (r0 + r < B) {
+      const elem_t o = (elem_t)(acc[r] + b);
+      out[(size_t)(r0 + r) * N + n] = o;
+      const float v = (float)o;
+      s += v;
+      s2 += v * v;
+    }
+  if (stats) {
+    const int sp = n / C, c = n - sp * C;
+    const size_t prow = (size_t)blockIdx.y * (N / C) + sp;
+    stats[(prow * 2 + 0) * C + c] = s;
+    stats[(prow * 2 + 1) * C + c] = s2;
+  }
 }
 
 // dW[K][N] = z^T @ dh (fp32 out), db[N] = sum_b dh; block = 256 columns x KC k-rows
@@ -189,6 +205,65 @@ __global__ void sum_vec_kernel(const float* __restrict__ v, int n, float* __rest
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// D head backward of d_loss in ONE launch (was: partial wgrad + split reduce + bias sum + dgrad):
+//   dW[k] = sum_r x[r][k] * dl[r],  db = sum_r dl[r],  dx[r][k] = dl[r] * w[k] (elem_t)
+// block = 64 columns (8 chunks of 8) x 32 row lanes; the row lanes reduce through LDS in a fixed
+// order (deterministic). Block 0's second wave also sums dl for the bias.
+__global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict__ x, const float* __restrict__ dl,
+                                                       const float* __restrict__ w, elem_t* __restrict__ dx,
+                                                       float* __restrict__ dW, float* __restrict__ db, int R, int K) {
+  __shared__ float red[32][65];
+  const int tid = threadIdx.x, c = tid & 7, rl = tid >> 3;
+  const int k = blockIdx.x * 64 + c * 8;
+  const bool kok = k < K;  // K % 8 == 0 (launcher)
+  float s[8], wv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s[i] = 0.f;
+    wv[i] = kok ? w[k + i] : 0.f;
+  }
+  if (kok) {
+    for (int rb = rl; rb < R; rb += 4 * 32) {  // 4 rows per iteration, loads first
+      u32x4 xv[4];
+      float gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 32 * u < R ? rb + 32 * u : rb;
+        xv[u] = *reinterpret_cast<const u32x4*>(x + (size_t)r * K + k);
+        gv[u] = dl[r];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 32 * u;
+        if (r >= R) break;
+        const elem8 xb = __builtin_bit_cast(elem8, xv[u]);
+        elem8 ob;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s[i] += (float)xb[i] * gv[u];
+          ob[i] = (elem_t)(gv[u] * wv[i]);
+        }
+        *reinterpret_cast<u32x4*>(dx + (size_t)r * K + k) = __builtin_bit_cast(u32x4, ob);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[rl][c * 8 + i] = s[i];
+  __syncthreads();
+  if (tid < 64 && blockIdx.x * 64 + tid < K) {
+    float a = 0.f;
+    for (int l = 0; l < 32; ++l) a += red[l][tid];
+    dW[blockIdx.x * 64 + tid] = a;
+  }
+  if (blockIdx.x == 0 && tid >= 64 && tid < 128) {
+    const int lane = tid - 64;
+    float a = 0.f;
+    for (int r = lane; r < R; r += 64) a += dl[r];
+    a = wave_sum(a);
+    if (lane == 0) db[0] = a;
+  }
 }
 
 // ---------------------------------------------------------------- TF Adam
@@ -325,38 +400,49 @@ __global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__
 
 // ---------------------------------------------------------------- im2col (stride 2, TF SAME)
 // src elem_t [B][H][W][C] -> dst elem_t [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad.
-// One thread per 16-byte output chunk (consecutive threads -> consecutive chunks: fully coalesced
-// stores; the 5x5xC patch reads hit L1/L2). 32-bit index math only, channel count fixed at compile
-// time (CC > 0) so k -> (ky, kx, c) is multiply-shift arithmetic; (b, oy, ox) via FastDiv.
+// One workgroup per output row (b, oy): the 5 input rows it reads (zero-padded to 2*Wo+3
+// columns) are staged in LDS with coalesced loads, then every thread writes 16-byte chunks of
+// the output row (consecutive threads -> consecutive chunks). Channel count fixed at compile
+// time (CC > 0) so k -> (ky, kx, c) is multiply-shift arithmetic.
 template <int CC>
 __global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict__ src, elem_t* __restrict__ dst,
-                                                        uint32_t n_chunks, int Crt, int H, int W, FastDiv fd_kv,
-                                                        FastDiv fd_wo, FastDiv fd_ho, int pl_y, int pl_x, int Kpad) {
+                                                        int Crt, int H, int W, int Ho, int Wo, int pl_y, int pl_x,
+                                                        int Kpad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  elem_t* band = reinterpret_cast<elem_t*>(smem);  // [5][Wp][C]
   const int C = CC > 0 ? CC : Crt;
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i >= n_chunks) return;
-  const uint32_t row = fdiv(i, fd_kv);
-  const int v = (int)(i - row * fd_kv.d);
-  const uint32_t t1 = fdiv(row, fd_wo);
-  const int ox = (int)(row - t1 * fd_wo.d);
-  const uint32_t b = fdiv(t1, fd_ho);
-  const int oy = (int)(t1 - b * fd_ho.d);
+  const int Wp = 2 * Wo + 3;
+  const int b = blockIdx.x / Ho, oy = blockIdx.x - b * Ho;
+  const int iy0 = 2 * oy - pl_y, ix0 = -pl_x;
   const elem_t* img = src + (size_t)b * H * W * C;
-  const int iy0 = 2 * oy - pl_y, ix0 = 2 * ox - pl_x;
-  elem8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = v * 8 + j;
-    elem_t val = (elem_t)0.f;
-    if (k < 25 * C) {
-      const int tap = k / C, c = k - tap * C;
-      const int ky = tap / 5, kx = tap - 5 * ky;
-      const int iy = iy0 + ky, ix = ix0 + kx;
-      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) val = img[(iy * W + ix) * C + c];
-    }
-    o[j] = val;
+  const int band_n = 5 * Wp * C;
+  for (int i = threadIdx.x; i < band_n; i += 256) {
+    const int row = i / (Wp * C), rem = i - row * (Wp * C);
+    const int col = rem / C, c = rem - col * C;
+    const int iy = iy0 + row, ix = ix0 + col;
+    elem_t v = (elem_t)0.f;
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = img[((size_t)iy * W + ix) * C + c];
+    band[i] = v;
   }
-  *reinterpret_cast<u32x4*>(dst + (size_t)i * 8) = __builtin_bit_cast(u32x4, o);
+  __syncthreads();
+  const int KV = Kpad >> 3;
+  elem_t* drow = dst + (size_t)blockIdx.x * Wo * Kpad;
+  for (int q = threadIdx.x; q < Wo * KV; q += 256) {
+    const int ox = q / KV, v = q - ox * KV;
+    elem8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = v * 8 + j;
+      elem_t val = (elem_t)0.f;
+      if (k < 25 * C) {
+        const int tap = k / C, c = k - tap * C;
+        const int ky = tap / 5, kx = tap - 5 * ky;
+        val = band[(ky * Wp + 2 * ox + kx) * C + c];
+      }
+      o[j] = val;
+    }
+    *reinterpret_cast<u32x4*>(drow + (size_t)q * 8) = __builtin_bit_cast(u32x4, o);
+  }
 }
 
 // ---------------------------------------------------------------- casts
@@ -392,10 +478,12 @@ extern "C" int DCG_API(dcg_gan_loss)(const float* logits, int B, float* out, flo
 }
 
 extern "C" int DCG_API(dcg_linear_fwd)(const float* z, const float* W, const float* b, elem_t* out, int B, int K, int N,
-                              hipStream_t s) {
+                              float* stats, int C, hipStream_t s) {
+  if (stats && (C <= 0 || N % C)) return -2;
   constexpr int RB = 8;  // (N/256) x (B/8) = 512 blocks for the 64x64 model at B=128
   dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
-  hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N);
+  hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N,
+                     stats, C);
   return (int)hipGetLastError();
 }
 
@@ -473,19 +561,15 @@ extern "C" int DCG_API(dcg_philox_uniform)(float* out, size_t n, uint64_t seed, 
 extern "C" int DCG_API(dcg_im2col_s2)(const elem_t* src, elem_t* dst, int B, int H, int W, int C, int Ho, int Wo, int pl_y,
                              int pl_x, int Kpad, hipStream_t s) {
   if (Kpad % 8 || Kpad < 25 * C) return -2;
-  const size_t n = (size_t)B * Ho * Wo * (Kpad / 8);
-  if (n >= 0x7fffff00u) return -2;  // 32-bit chunk index
-  const dim3 grid((unsigned)((n + 255) / 256));
-  const dcg::FastDiv fkv = fastdiv_make(Kpad / 8), fwo = fastdiv_make(Wo), fho = fastdiv_make(Ho);
+  const size_t shm = (size_t)5 * (2 * Wo + 3) * C * sizeof(elem_t);
+  if (shm > 64 * 1024) return -2;
+  const dim3 grid((unsigned)(B * Ho));
   if (C == 3)
-    hipLaunchKernelGGL(im2col_s2_kernel<3>, grid, dim3(256), 0, s, src, dst, (uint32_t)n, C, H, W, fkv, fwo, fho, pl_y,
-                       pl_x, Kpad);
+    hipLaunchKernelGGL(im2col_s2_kernel<3>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad);
   else if (C == 1)
-    hipLaunchKernelGGL(im2col_s2_kernel<1>, grid, dim3(256), 0, s, src, dst, (uint32_t)n, C, H, W, fkv, fwo, fho, pl_y,
-                       pl_x, Kpad);
+    hipLaunchKernelGGL(im2col_s2_kernel<1>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad);
   else
-    hipLaunchKernelGGL(im2col_s2_kernel<0>, grid, dim3(256), 0, s, src, dst, (uint32_t)n, C, H, W, fkv, fwo, fho, pl_y,
-                       pl_x, Kpad);
+    hipLaunchKernelGGL(im2col_s2_kernel<0>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad);
   return (int)hipGetLastError();
 }
 
@@ -506,5 +590,12 @@ extern "C" int DCG_API(dcg_cast_to_bf16)(const void* src, int src_dtype, elem_t*
 
 extern "C" int DCG_API(dcg_cast_bf16_f32)(const elem_t* src, float* dst, size_t n, hipStream_t s) {
   hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_head_bwd)(const elem_t* x, const float* dl, const float* w, elem_t* dx, float* dW, float* db,
+                                     int R, int K, hipStream_t s) {
+  if (K % 8) return -2;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((K + 63) / 64), dim3(256), 0, s, x, dl, w, dx, dW, db, R, K);
   return (int)hipGetLastError();
 }

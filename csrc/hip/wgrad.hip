@@ -187,8 +187,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* src, in
   const size_t n4 = n / 4;
   const size_t i = (size_t)blockIdx.x * COLS + col;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (i < n4)
-    for (int k = lane; k < splits; k += L) s += reinterpret_cast<const f32x4*>(src + (size_t)k * n)[i];
+  if (i < n4) {
+    auto slab = [&](int k) { return reinterpret_cast<const f32x4*>(src + (size_t)k * n)[i]; };
+    int k = lane;
+    for (; k + 3 * L < splits; k += 4 * L) {  // 4 slabs in flight per lane, summed in slab order
+      const f32x4 a = slab(k), b = slab(k + L), c = slab(k + 2 * L), d = slab(k + 3 * L);
+      s += a;
+      s += b;
+      s += c;
+      s += d;
+    }
+    for (; k < splits; k += L) s += slab(k);
+  }
   red[lane][col] = s;
   __syncthreads();
   if (lane == 0 && i < n4) {

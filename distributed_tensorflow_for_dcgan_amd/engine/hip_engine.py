@@ -216,13 +216,14 @@ class HipEngine:
             raise RuntimeError("no igemm tile for %s (mode %d, N %d, bkn %d)" % (name, mode, N, bkn))
         cfg, splits = plan
         bx = by = bm = br = 0
-        brpg = bact = 0
+        brpg = bact = bstore = 0
         if bnb is not None:
             bx, by, bm, br = _p(bnb[0]), _p(bnb[1]), _p(bnb[2]), _p(bnb[3])
             brpg, bact = bnb[4], bnb[5]
+            bstore = int(len(bnb) > 6 and bnb[6])
         prog.igemm_ex(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
                       ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), 0, int(bkn), kb_valid, splits,
-                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak)
+                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak, bstore)
         return cfg
 
     def _dgrad_bnb(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, bn_name, x, y, groups, act, group_offset=0):
@@ -250,6 +251,25 @@ class HipEngine:
         mean, rstd = st["mean"][group_offset:], st["rstd"][group_offset:]
         kw = dict(stats=part, rows_per_group=rpg, bnb=(x, y, mean, rstd, rpg, act))
         return kw, part, P // groups
+
+    def _dgrad_actb(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, name, y, act):
+        """Fused activation backward for the data-gradient GEMM that produces dL/da of a layer
+        WITHOUT BN: the GEMM stores dx = dL/da * act'(y) directly and emits per-tile partial
+        column sums of dx (the bias gradient). Returns (igemm kwargs, partials, #partials) or
+        None (no vectorizable tile; the caller runs the separate act backward)."""
+        if os.environ.get("DCGAN_NO_FUSED_ACTG") == "1":
+            return None
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, None, bkn)
+        if plan is None or N % 8 or not H.bnb_fits(plan[0]):
+            return None
+        bm, _ = H.tile_of(plan[0])
+        if mode == 1:
+            M, phases = Bn * (-(-Hout // 2)) * (-(-Wout // 2)), 4
+        else:
+            M, phases = Bn * Hout * Wout, 1
+        P = -(-M // bm) * phases
+        part = self._stats_buf(name + ".actb", P, N)
+        return dict(stats=part, bnb=(y, y, None, None, 0, act, True)), part, P
 
     def _deconv_out(self, prog, name, x, w, y, B, L, pad, bias, act):
         """G's output layer: the direct narrow kernel for RGB / gray outputs, else the igemm."""
@@ -302,14 +322,15 @@ class HipEngine:
             prog.philox_uniform("z", _p(z), z.numel(), self.seed * 1000003 + 17 + 7919 * self.rank * int(self.rank_seeded_z),
                                 _p(self.step_counter), 0, -1.0, 1.0, 0)
         # G projection + g_bn0 + relu
-        prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
-                        B, cfg.z_dim, cfg.g_lin_out, 0)
         C0 = cfg.g_base_ch
         rows0 = B * cfg.g_base_hw ** 2
-        rpb = self._rows_per_block(rows0, C0)
-        part0 = self._stats_buf("g_bn0", rows0 // rpb, C0)
-        prog.colstats("g_bn0.stats", 0, _p(self.g_h0_pre), 0, 0, 0, 0, 0, 0.0, rows0, C0, rpb, rows0, _p(part0), 0)
-        self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, rows0 // rpb, update_ema)
+        # g_bn0 partial statistics straight from the projection kernel: one partial row per
+        # (8-row block of z, spatial position) -- see linear_fwd_kernel
+        P0 = -(-B // 8) * (cfg.g_lin_out // C0)
+        part0 = self._stats_buf("g_bn0", P0, C0)
+        prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
+                        B, cfg.z_dim, cfg.g_lin_out, 0, _p(part0), C0)
+        self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, P0, update_ema)
         a_prev = self.g_h0
         Wg, Wd = self.wbf_g, self.wbf_d
         for L in self.gl:
@@ -375,10 +396,15 @@ class HipEngine:
         Pd, gD = self.model.d, self.grad_d
         lin = cfg.d_lin_name
         last = self.dl[-1]
-        prog.head_wgrad("d_head.wgrad", _p(self.d_a[last.name]), _p(self.dl_d), _p(self.d_head_part), B2,
-                        cfg.d_lin_in, 16, _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), 0)
-        prog.head_dgrad("d_head.dgrad", _p(self.dl_d), _p(Pd[lin + "/Matrix"]), _p(self.d_da[last.name]), B2,
-                        cfg.d_lin_in, 0)
+        if os.environ.get("DCGAN_NO_HEAD_BWD") == "1":  # A/B: the unfused head backward
+            prog.head_wgrad("d_head.wgrad", _p(self.d_a[last.name]), _p(self.dl_d), _p(self.d_head_part), B2,
+                            cfg.d_lin_in, 16, _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), 0)
+            prog.head_dgrad("d_head.dgrad", _p(self.dl_d), _p(Pd[lin + "/Matrix"]), _p(self.d_da[last.name]), B2,
+                            cfg.d_lin_in, 0)
+        else:
+            prog.head_bwd("d_head.bwd", _p(self.d_a[last.name]), _p(self.dl_d), _p(Pd[lin + "/Matrix"]),
+                          _p(self.d_da[last.name]), _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), B2,
+                          cfg.d_lin_in, 0)
         fused_next = None  # BN-backward partials emitted by the previous (upper) layer's dgrad GEMM
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
@@ -388,10 +414,11 @@ class HipEngine:
             if L.bn:
                 self._bn_bwd(prog, L.bn, self.d_x[L.name], da, a, dx, rows, L.cout, 2, LRELU, Pd, gD,
                              self.coef[L.bn], write_param_grads=True, fused=fused_next)
-            else:
-                prog.act_bwd(L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
-                # live bias (no BN after it): db = sum over rows of dx
-                self._colsum(prog, L.name + ".dbias", dx, rows, L.cout, gD[L.name + "/biases"])
+            elif fused_next is not None:  # dx already stored by the upper dgrad GEMM; db from its partials
+                part, Pn = fused_next
+                prog.sum_partials(L.name + ".dbias", _p(part), Pn, 2 * L.cout, L.cout, _p(gD[L.name + "/biases"]), 0)
+            else:  # live bias (no BN after it): db = sum over rows of dx, fused with the act backward
+                self._act_bwd_dbias(prog, L.name + ".act_bwd", da, a, dx, rows, L.cout, LRELU, gD[L.name + "/biases"])
             # weight gradient
             src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
             pad = same_pads(L.in_hw)[0]
@@ -412,13 +439,30 @@ class HipEngine:
                 nat = self.wbf_d[L.name + "/w"]
                 P_ = self.dl[i - 1]
                 kw = {}
+                out = self.d_da[P_.name]
                 if P_.bn:
                     r = self._dgrad_bnb(1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.bn,
                                         self.d_x[P_.name], self.d_a[P_.name], 2, LRELU)
                     if r is not None:
                         kw, fused_next = r[0], (r[1], r[2])
-                self._igemm(prog, L.name + ".dgrad", 1, dx, nat, self.d_da[P_.name], B2, L.out_hw, L.out_hw, L.cout,
+                else:
+                    r = self._dgrad_actb(1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.name,
+                                         self.d_a[P_.name], LRELU)
+                    if r is not None:
+                        kw, fused_next, out = r[0], (r[1], r[2]), self.d_dx[P_.name]
+                self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
                             L.in_hw, L.in_hw, L.cin, pad, **kw)
+
+    def _act_bwd_dbias(self, prog, name, dy, y, dx, rows, C, act, db):
+        """dx = dy * act'(y) and the bias gradient db = column sums of dx: one fused launch
+        when the channel count has a kernel variant, else act_bwd + a column-sum pass."""
+        leak = self.cfg.lrelu_leak if act == LRELU else 0.0
+        fused_ok = os.environ.get("DCGAN_NO_FUSED_ACTB") != "1"
+        if fused_ok and (C in (1, 3) or (C % 8 == 0 and C <= 256 and 256 % (C // 8) == 0)):
+            prog.act_bwd_dbias(name, _p(dy), _p(y), _p(dx), rows, C, act, leak, _p(db), 0)
+        else:
+            prog.act_bwd(name, _p(dy), _p(y), _p(dx), dx.numel(), act, leak, 0)
+            self._colsum(prog, name + ".dbias", dx, rows, C, db)
 
     def _colsum(self, prog, name, x, rows, C, dst):
         if C % 8 == 0:
@@ -516,7 +560,7 @@ class HipEngine:
             if L.bn:
                 self._bn_bwd(prog, L.bn, half(self.d_x[L.name]), da, a, dx, rows, L.cout, 1, LRELU, Pd, None,
                              self.coef_g[L.bn], write_param_grads=False, row_offset_groups=1, fused=fused_next)
-            else:
+            elif fused_next is None:  # (else dx was stored by the upper dgrad GEMM)
                 prog.act_bwd("g." + L.name + ".act_bwd", _p(da), _p(a), _p(dx), dx.numel(), LRELU, cfg.lrelu_leak, 0)
             nat = self.wbf_d[L.name + "/w"]
             pad = same_pads(L.in_hw)[0]
@@ -524,12 +568,18 @@ class HipEngine:
             if i > 0:
                 P_ = self.dl[i - 1]
                 kw = {}
+                out = half(self.d_da[P_.name])
                 if P_.bn:
                     r = self._dgrad_bnb(1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.bn,
                                         half(self.d_x[P_.name]), half(self.d_a[P_.name]), 1, LRELU, group_offset=1)
                     if r is not None:
                         kw, fused_next = r[0], (r[1], r[2])
-                self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, half(self.d_da[P_.name]), B, L.out_hw,
+                else:
+                    r = self._dgrad_actb(1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                                         "g." + P_.name, half(self.d_a[P_.name]), LRELU)
+                    if r is not None:
+                        kw, fused_next, out = r[0], (r[1], r[2]), half(self.d_dx[P_.name])
+                self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, out, B, L.out_hw,
                             L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, **kw)
             else:
                 if L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
@@ -541,9 +591,8 @@ class HipEngine:
         # ---------------- G backward
         n = len(self.gl)
         Lg = self.gl[-1]
-        prog.act_bwd("g_out.tanh_bwd", _p(self.img_grad), _p(self.fake), _p(self.img_g), self.img_g.numel(), TANH,
-                     0.0, 0)
-        self._colsum(prog, Lg.name + ".dbias", self.img_g, B * Lg.out_hw ** 2, Lg.cout, gG[Lg.name + "/biases"])
+        self._act_bwd_dbias(prog, "g_out.tanh_bwd", self.img_grad, self.fake, self.img_g, B * Lg.out_hw ** 2,
+                            Lg.cout, TANH, gG[Lg.name + "/biases"])
         a_prev = self.g_a[self.gl[-2].name] if n > 1 else self.g_h0
         da_prev = self.g_da[self.gl[-2].name] if n > 1 else self.g_da0
         x_prev = self.g_x[self.gl[-2].name] if n > 1 else self.g_h0_pre

@@ -202,7 +202,10 @@ def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_
     bm, bn = WGRAD_CFGS[cfg]
     tiles = -(-Mc // bm) * -(-Nc // bn) * taps
     kt = -(-K // 64)
-    splits = max(1, min(-(-target_blocks // tiles), max(1, kt // 4)))
+    # plain (im2col'd, 1-tap) layers reduce over up to 2^18 pixels into a tiny 80 x 64 matrix:
+    # >= 16 k-tiles per split keeps the slab traffic (splits x Mc x Nc fp32) and the reduce short
+    min_kt = 16 if taps == 1 else 4
+    splits = max(1, min(-(-target_blocks // tiles), max(1, kt // min_kt)))
     return cfg, splits
 
 
@@ -401,6 +404,32 @@ def conv_wgrad3(g_src: torch.Tensor, dm: torch.Tensor, pad: int, cfg: Optional[i
     prog.wgrad3("wgrad3", _p(g_src), Hg, Wg, Mc, _p(dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(out), scale, 0)
     run(prog)
     return out
+
+
+def act_bwd_dbias(dy: torch.Tensor, y: torch.Tensor, act: int, leak: float = 0.2):
+    """(dx, db): dx = dy * act'(y) (elem dtype), db[c] = sum over rows of dx (fp32) -- one launch."""
+    _check_bf16(dy, y)
+    C = dy.shape[-1]
+    R = dy.numel() // C
+    dx = torch.empty_like(dy)
+    db = torch.empty(C, device=dy.device, dtype=torch.float32)
+    prog = ext().Program(dy.dtype == torch.float16)
+    prog.act_bwd_dbias("abd", _p(dy), _p(y), _p(dx), R, C, act, leak, _p(db), 0)
+    run(prog)
+    return dx, db
+
+
+def head_bwd(x: torch.Tensor, dl: torch.Tensor, w: torch.Tensor):
+    """(dx, dW, db) of logits = x @ w + b: dW = x^T dl, db = sum dl, dx = dl w^T (elem dtype)."""
+    _check_bf16(x)
+    R, K = x.shape
+    dx = torch.empty_like(x)
+    dW = torch.empty(K, device=x.device, dtype=torch.float32)
+    db = torch.empty(1, device=x.device, dtype=torch.float32)
+    prog = ext().Program(x.dtype == torch.float16)
+    prog.head_bwd("hb", _p(x), _p(dl), _p(w), _p(dx), _p(dW), _p(db), R, K, 0)
+    run(prog)
+    return dx, dW, db
 
 
 def im2col_s2(x: torch.Tensor, kpad: int) -> torch.Tensor:

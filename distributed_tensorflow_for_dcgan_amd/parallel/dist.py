@@ -12,7 +12,9 @@ Replaces the reference's asynchronous gRPC parameter server (all variables pinne
 * backend ``nccl`` (= RCCL over xGMI on ROCm) for GPUs, ``gloo`` for CPU tests.
 
 RCCL's ring over the 8-GPU xGMI full mesh is per-link bound (~153 GB/s per link), so
-buckets are kept large (default 8 MiB): the whole 37.8 MB fp32 gradient is 5 buckets.
+buckets are kept large: the HIP engine overlaps at graph-segment granularity (G grads
+during D's backward, D's top layer during the rest of D's backward), so each overlap
+window is ONE collective (32 MiB buckets) -- extra calls would only add latency.
 """
 from __future__ import annotations
 
@@ -154,7 +156,7 @@ class GradAllReducer:
     converted to bf16 for the wire (half the xGMI bytes) and back to fp32.
     """
 
-    def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 8.0, wire_dtype: str = "fp32",
+    def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 32.0, wire_dtype: str = "fp32",
                  reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None):
         self.flat = flat_grad
         self.world = world_size()

@@ -386,6 +386,19 @@ def test_linear_and_head():
     close(out, z @ W + b, 1e-2, "linear fwd")
     close(dW, z.t() @ dh.float(), 1e-3, "linear wgrad")
     close(db, dh.float().sum(0), 1e-3, "linear bias grad")
+    # fused BN partial statistics (channel = column % C; partial row = (8-row block, column // C))
+    C = 512
+    part = torch.full((-(-B // 8) * (N // C), 2, C), float("nan"), device=dev)
+    out2 = torch.empty_like(out)
+    pr = _prog()
+    pr.linear_fwd("lin", _p(z), _p(W), _p(b), _p(out2), B, K, N, 0, _p(part), C)
+    h.run(pr)
+    assert torch.equal(out2, out)
+    o = out.float().reshape(B, N // C, C)
+    close(part[:, 0].sum(0), o.sum((0, 1)), 1e-5, "linear stats sum")
+    close(part[:, 1].sum(0), (o * o).sum((0, 1)), 1e-5, "linear stats sumsq")
+    ob = torch.nn.functional.pad(o, (0, 0, 0, 0, 0, 40 - B)).reshape(5, 8, N // C, C).sum(1).reshape(-1, C)
+    close(part[:, 0], ob, 1e-5, "linear stats per block")
     # D head
     R_, Kh = 2 * B, 8192
     x = bf(rnd(R_, Kh, seed=37))
@@ -485,3 +498,47 @@ def test_bn_finalize_split_paths(P, groups, C):
     A = gamma.double().cpu() * rstd.double().cpu()
     close(coef[:, 0].cpu(), A, 1e-5, "coef A")
     close(coef[:, 1].cpu(), -A * pg[:, 1] / cnt * rstd.double().cpu(), 1e-4, "coef x")
+
+
+@pytest.mark.parametrize("R,C,act", [(256 * 1024, 64, 2), (1000, 64, 1), (128 * 64 * 64, 3, 3), (777, 3, 3),
+                                     (4099, 1, 2), (3 * 129, 256, 2), (50, 128, 0)])
+def test_act_bwd_dbias(R, C, act):
+    """Fused dx = dy * act'(y) + bias gradient (last-arrival reduction): dx bit-exact vs the
+    separate act_bwd formula, db vs an fp64 column sum of the stored dx; replay gives the same bits."""
+    h = H()
+    dy = bf(rnd(R, C, seed=90))
+    y = rnd(R, C, seed=91)
+    if act == 3:
+        y = torch.tanh(y * 2)
+    y = bf(y)
+    dx, db = h.act_bwd_dbias(dy, y, act, 0.2)
+    yf = y.float()
+    if act == 1:
+        d = (yf > 0).float()
+    elif act == 2:
+        d = torch.where(yf > 0, torch.ones_like(yf), torch.full_like(yf, 0.2))
+    elif act == 3:
+        d = 1 - yf * yf
+    else:
+        d = torch.ones_like(yf)
+    ref_dx = (dy.float() * d).to(torch.bfloat16)
+    if act == 3:  # 1 - y*y may be contracted into an fma on the GPU: one bf16 ulp
+        close(dx, ref_dx, 8e-3, "tanh dx")
+    else:
+        assert torch.equal(dx, ref_dx)
+    ref_db = dx.double().sum(0)
+    assert (db.double() - ref_db).abs().max().item() <= 1e-5 * (dx.double().abs().sum(0).max().item() + 1)
+    dx2, db2 = h.act_bwd_dbias(dy, y, act, 0.2)
+    assert torch.equal(db, db2) and torch.equal(dx, dx2)
+
+
+@pytest.mark.parametrize("R,K", [(256, 8192), (64, 4096), (10, 200)])
+def test_head_bwd_fused(R, K):
+    h = H()
+    x = bf(rnd(R, K, seed=92))
+    dl = rnd(R, seed=93)
+    w = rnd(K, scale=0.02, seed=94)
+    dx, dW, db = h.head_bwd(x, dl, w)
+    close(dW, x.float().t() @ dl, 1e-4, "head dW")
+    close(db, dl.sum(0, keepdim=True), 1e-5, "head db")
+    assert torch.equal(dx, (dl[:, None] * w[None, :]).to(torch.bfloat16))
