@@ -318,6 +318,30 @@ __device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned expecte
   return *flag_lds != 0;
 }
 
+// sum of the PS slice rows of group g, column c (and C + c), in slice order; 8 slices' loads in
+// flight at a time (a plain loop waited on every `sc1` load: ~60 dependent L2 round trips)
+__device__ __forceinline__ void slice_sums(__amdgpu_buffer_rsrc_t rw, int g, int PS, int C, int c, double& a,
+                                           double& b) {
+  int q = 0;
+  for (; q + 8 <= PS; q += 8) {
+    double va[8], vb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      va[u] = ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q + u) * 2 + 0) * C + c) * 8u);
+      vb[u] = ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q + u) * 2 + 1) * C + c) * 8u);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a += va[u];
+      b += vb[u];
+    }
+  }
+  for (; q < PS; ++q) {
+    a += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 0) * C + c) * 8u);
+    b += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 1) * C + c) * 8u);
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_split_kernel(
     const float* __restrict__ part, int ppg, int groups, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -339,10 +363,7 @@ __global__ __launch_bounds__(256) void bn_finalize_split_kernel(
   if (!last_arrival(counters + g * gridDim.x + cg, (unsigned)PS, &flag)) return;
   if (threadIdx.x >= 16 || !cok) return;
   double a = 0.0, b = 0.0;
-  for (int q = 0; q < PS; ++q) {
-    a += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 0) * C + c) * 8u);
-    b += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 1) * C + c) * 8u);
-  }
+  slice_sums(rw, g, PS, C, c, a, b);
   const int idx = g * C + c;
   const double m = a / count;
   double v = b / count - m * m;
@@ -385,10 +406,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_split_kernel(
   float dg = 0.f, db = 0.f;
   for (int gg = 0; gg < groups; ++gg) {
     double a = 0.0, b = 0.0;
-    for (int q = 0; q < PS; ++q) {
-      a += ld_sc1_f64(rw, (uint32_t)((((size_t)gg * PS + q) * 2 + 0) * C + c) * 8u);
-      b += ld_sc1_f64(rw, (uint32_t)((((size_t)gg * PS + q) * 2 + 1) * C + c) * 8u);
-    }
+    slice_sums(rw, gg, PS, C, c, a, b);
     const float sg1 = (float)a, sg2 = (float)b;
     dg += sg2;
     db += sg1;

@@ -61,7 +61,7 @@ template <int RB>
 __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ z, const float* __restrict__ W,
                                                          const float* __restrict__ bias, elem_t* __restrict__ out,
                                                          int B, int K, int N, float* __restrict__ stats, int C) {
-  extern __shared__ float zs[];  // [RB][K]
+  extern __shared__ __attribute__((aligned(16))) float zs[];  // [RB][K]
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * RB;
   for (int i = threadIdx.x; i < RB * K; i += 256) {
@@ -73,16 +73,24 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
   float acc[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) acc[r] = 0.f;
+  // z is read from LDS as float4 (4 k per ds_read_b128, broadcast): with scalar reads the loop
+  // was LDS-instruction bound (8 rows x 100 k reads per thread)
   constexpr int KU = 20;
   int k = 0;
-  for (; k + KU <= K; k += KU) {
-    float w[KU];
+  if ((K & 3) == 0) {
+    for (; k + KU <= K; k += KU) {
+      float w[KU];
 #pragma unroll
-    for (int u = 0; u < KU; ++u) w[u] = W[(size_t)(k + u) * N + n];
+      for (int u = 0; u < KU; ++u) w[u] = W[(size_t)(k + u) * N + n];
 #pragma unroll
-    for (int u = 0; u < KU; ++u)
+      for (int r = 0; r < RB; ++r)
 #pragma unroll
-      for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k + u] * w[u];
+        for (int u4 = 0; u4 < KU / 4; ++u4) {
+          const f32x4 zv = *reinterpret_cast<const f32x4*>(zs + r * K + k + 4 * u4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[r] += zv[e] * w[4 * u4 + e];
+        }
+    }
   }
   for (; k < K; ++k) {
     const float w = W[(size_t)k * N + n];
@@ -109,11 +117,11 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
 }
 
 // dW[K][N] = z^T @ dh (fp32 out), db[N] = sum_b dh; block = 256 columns x KC k-rows
-template <int KC>
+template <int KC>  // KC % 4 == 0
 __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ z, const elem_t* __restrict__ dh,
                                                            float* __restrict__ dW, float* __restrict__ db, int B,
                                                            int K, int N) {
-  extern __shared__ float zs[];  // [B][KC]
+  extern __shared__ __attribute__((aligned(16))) float zs[];  // [B][KC]
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int k0 = blockIdx.y * KC;
   for (int i = threadIdx.x; i < B * KC; i += 256) {
@@ -126,7 +134,23 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
   float sb = 0.f;
 #pragma unroll
   for (int k = 0; k < KC; ++k) acc[k] = 0.f;
-  for (int b = 0; b < B; ++b) {
+  int b = 0;
+  for (; b + 8 <= B; b += 8) {  // 8 dh loads in flight, z rows as float4 LDS reads
+    float g[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) g[u] = (float)dh[(size_t)(b + u) * N + n];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      sb += g[u];
+#pragma unroll
+      for (int k4 = 0; k4 < KC / 4; ++k4) {
+        const f32x4 zv = *reinterpret_cast<const f32x4*>(zs + (b + u) * KC + 4 * k4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[4 * k4 + e] += zv[e] * g[u];
+      }
+    }
+  }
+  for (; b < B; ++b) {
     const float g = (float)dh[(size_t)b * N + n];
     sb += g;
 #pragma unroll
@@ -400,24 +424,27 @@ __global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__
 
 // ---------------------------------------------------------------- im2col (stride 2, TF SAME)
 // src elem_t [B][H][W][C] -> dst elem_t [B*Ho*Wo][Kpad], k = tap*C + c (tap = ky*5 + kx), zero pad.
-// One workgroup per output row (b, oy): the 5 input rows it reads (zero-padded to 2*Wo+3
-// columns) are staged in LDS with coalesced loads, then every thread writes 16-byte chunks of
-// the output row (consecutive threads -> consecutive chunks). Channel count fixed at compile
-// time (CC > 0) so k -> (ky, kx, c) is multiply-shift arithmetic.
+// One workgroup per IM_ROWS output rows of one image: the 2*IM_ROWS+3 input rows they read
+// (zero-padded to 2*Wo+3 columns) are staged in LDS once (no 5/2x re-read of shared rows; ~9
+// independent loads per thread), then every thread writes several 16-byte chunks of the output
+// rows (consecutive threads -> consecutive chunks). Channel count fixed at compile time (CC > 0)
+// so k -> (ky, kx, c) is multiply-shift arithmetic.
+constexpr int IM_ROWS = 4;
 template <int CC>
 __global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict__ src, elem_t* __restrict__ dst,
                                                         int Crt, int H, int W, int Ho, int Wo, int pl_y, int pl_x,
-                                                        int Kpad) {
+                                                        int Kpad, int row_blocks) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  elem_t* band = reinterpret_cast<elem_t*>(smem);  // [5][Wp][C]
+  elem_t* band = reinterpret_cast<elem_t*>(smem);  // [2*IM_ROWS+3][Wp][C]
   const int C = CC > 0 ? CC : Crt;
-  const int Wp = 2 * Wo + 3;
-  const int b = blockIdx.x / Ho, oy = blockIdx.x - b * Ho;
-  const int iy0 = 2 * oy - pl_y, ix0 = -pl_x;
+  const int Wp = 2 * Wo + 3, WpC = Wp * C;
+  const int b = blockIdx.x / row_blocks, oy0 = (blockIdx.x - b * row_blocks) * IM_ROWS;
+  const int nrows = min(IM_ROWS, Ho - oy0);
+  const int iy0 = 2 * oy0 - pl_y, ix0 = -pl_x;
   const elem_t* img = src + (size_t)b * H * W * C;
-  const int band_n = 5 * Wp * C;
+  const int band_n = (2 * nrows + 3) * WpC;
   for (int i = threadIdx.x; i < band_n; i += 256) {
-    const int row = i / (Wp * C), rem = i - row * (Wp * C);
+    const int row = i / WpC, rem = i - row * WpC;
     const int col = rem / C, c = rem - col * C;
     const int iy = iy0 + row, ix = ix0 + col;
     elem_t v = (elem_t)0.f;
@@ -426,9 +453,12 @@ __global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict
   }
   __syncthreads();
   const int KV = Kpad >> 3;
-  elem_t* drow = dst + (size_t)blockIdx.x * Wo * Kpad;
-  for (int q = threadIdx.x; q < Wo * KV; q += 256) {
-    const int ox = q / KV, v = q - ox * KV;
+  const int per_row = Wo * KV;
+  elem_t* drow = dst + ((size_t)b * Ho + oy0) * Wo * Kpad;
+  for (int q = threadIdx.x; q < nrows * per_row; q += 256) {
+    const int r = q / per_row, qq = q - r * per_row;
+    const int ox = qq / KV, v = qq - ox * KV;
+    const elem_t* bp = band + (2 * r * Wp + 2 * ox) * C;
     elem8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -437,7 +467,7 @@ __global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict
       if (k < 25 * C) {
         const int tap = k / C, c = k - tap * C;
         const int ky = tap / 5, kx = tap - 5 * ky;
-        val = band[(ky * Wp + 2 * ox + kx) * C + c];
+        val = bp[(ky * Wp + kx) * C + c];
       }
       o[j] = val;
     }
@@ -489,7 +519,7 @@ extern "C" int DCG_API(dcg_linear_fwd)(const float* z, const float* W, const flo
 
 extern "C" int DCG_API(dcg_linear_wgrad)(const float* z, const elem_t* dh, float* dW, float* db, int B, int K, int N,
                                 hipStream_t s) {
-  constexpr int KC = 4;  // 4 k-rows per block: (N/256) x (K/4) = 800 blocks for the 64x64 model
+  constexpr int KC = 8;  // 8 k-rows per block: (N/256) x (K/8) = 416 blocks for the 64x64 model
   if ((size_t)B * KC * sizeof(float) > 65536) return -2;
   dim3 grid((N + 255) / 256, (K + KC - 1) / KC);
   hipLaunchKernelGGL((linear_wgrad_kernel<KC>), grid, dim3(256), B * KC * sizeof(float), s, z, dh, dW, db, B, K, N);
@@ -561,15 +591,19 @@ extern "C" int DCG_API(dcg_philox_uniform)(float* out, size_t n, uint64_t seed, 
 extern "C" int DCG_API(dcg_im2col_s2)(const elem_t* src, elem_t* dst, int B, int H, int W, int C, int Ho, int Wo, int pl_y,
                              int pl_x, int Kpad, hipStream_t s) {
   if (Kpad % 8 || Kpad < 25 * C) return -2;
-  const size_t shm = (size_t)5 * (2 * Wo + 3) * C * sizeof(elem_t);
+  const size_t shm = (size_t)(2 * dcg::IM_ROWS + 3) * (2 * Wo + 3) * C * sizeof(elem_t);
   if (shm > 64 * 1024) return -2;
-  const dim3 grid((unsigned)(B * Ho));
+  const int row_blocks = (Ho + dcg::IM_ROWS - 1) / dcg::IM_ROWS;
+  const dim3 grid((unsigned)(B * row_blocks));
   if (C == 3)
-    hipLaunchKernelGGL(im2col_s2_kernel<3>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad);
+    hipLaunchKernelGGL(im2col_s2_kernel<3>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad,
+                       row_blocks);
   else if (C == 1)
-    hipLaunchKernelGGL(im2col_s2_kernel<1>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad);
+    hipLaunchKernelGGL(im2col_s2_kernel<1>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad,
+                       row_blocks);
   else
-    hipLaunchKernelGGL(im2col_s2_kernel<0>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad);
+    hipLaunchKernelGGL(im2col_s2_kernel<0>, grid, dim3(256), shm, s, src, dst, C, H, W, Ho, Wo, pl_y, pl_x, Kpad,
+                       row_blocks);
   return (int)hipGetLastError();
 }
 

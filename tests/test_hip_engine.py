@@ -70,9 +70,12 @@ def _lrelu_d(a):
 
 @pytest.mark.parametrize("size,c_dim,B,dtype", [(64, 3, 16, "bf16"), (28, 1, 8, "bf16"), (128, 3, 4, "bf16"),
                                                 (256, 3, 4, "bf16"), (64, 3, 16, "fp16"), (256, 3, 4, "fp16")])
-def test_engine_stagewise(size, c_dim, B, dtype):
+def test_engine_stagewise(size, c_dim, B, dtype, monkeypatch):
     """fp16 runs with the dynamic loss scale in the gradient seeds: every stage is compared
-    against a recomputation from the engine's own (scaled) inputs, so the scale cancels."""
+    against a recomputation from the engine's own (scaled) inputs, so the scale cancels.
+    Adam(G) stays out of program A (no DCGAN_CONCURRENT_ADAM): the G stages are recomputed
+    from the pre-update G weights."""
+    monkeypatch.delenv("DCGAN_CONCURRENT_ADAM", raising=False)
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     from distributed_tensorflow_for_dcgan_amd.ops import hip as H
     dev = torch.device("cuda", 0)
