@@ -149,9 +149,10 @@ def tuned_table() -> dict:
     global _TUNED
     if _TUNED is None:
         _TUNED = {}
-        if os.environ.get("DCGAN_NO_TUNED") != "1" and os.path.exists(TUNED_PATH):
+        path = os.environ.get("DCGAN_TUNED_PATH", TUNED_PATH)  # A/B of tile tables
+        if os.environ.get("DCGAN_NO_TUNED") != "1" and os.path.exists(path):
             import json
-            with open(TUNED_PATH) as f:
+            with open(path) as f:
                 for k, v in json.load(f).items():
                     c, _, sp = str(v).partition(":")
                     _TUNED[k] = (int(c), int(sp or 1))
