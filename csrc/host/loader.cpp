@@ -1,224 +1,13 @@
-// Multi-threaded shuffling image loader (native replacement of the reference's input queues:
-// string_input_producer -> 16 QueueRunner threads -> RandomShuffleQueue, image_input.py:77-115).
-//
-// * reader threads pull file names from an epoch-shuffled list (infinite epochs when `loop`),
-//   read TFRecords (CRC-checked), extract the `image_raw` bytes feature, decode raw float64 /
-//   float32 / uint8 pixels and convert them ONCE into the output dtype (fp32 or bf16, uint8
-//   rescaled by scale/shift) into a slot of a fixed-capacity example pool;
-// * next_batch() waits until min_after_dequeue + batch examples are pooled (RandomShuffleQueue
-//   semantics), then draws `batch` uniformly random slots into the caller's buffer (typically a
-//   pinned host tensor, followed by an async H2D copy on a side stream), with the GIL released.
-// With threads == 1 the order is a deterministic function of the seed.
+// Python bindings of the host runtime: TFRecord / tf.train.Example I/O and the threaded
+// shuffling loader (loader.h). next_batch() releases the GIL while it waits / copies.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <algorithm>
-#include <atomic>
-#include <condition_variable>
-#include <cstring>
-#include <mutex>
-#include <random>
-#include <stdexcept>
-#include <string>
-#include <thread>
-#include <vector>
-
+#include "loader.h"
 #include "tfrecord.h"
 
 namespace py = pybind11;
 using namespace dcgh;
-
-static inline uint16_t f2bf(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);  // NaN
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-class Loader {
- public:
-  Loader(std::vector<std::string> files, std::string feature, int H, int W, int C, int batch, int capacity,
-         int min_after_dequeue, int threads, uint64_t seed, std::string out_dtype, std::string src_dtype, bool loop,
-         bool verify_crc, float u8_scale, float u8_shift)
-      : files_(std::move(files)), feature_(std::move(feature)), elems_((size_t)H * W * C), batch_(batch),
-        min_after_(std::max(0, min_after_dequeue)), loop_(loop), verify_(verify_crc), u8_scale_(u8_scale),
-        u8_shift_(u8_shift), rng_(seed), file_rng_(seed ^ 0x9E3779B97F4A7C15ull) {
-    if (files_.empty()) throw std::runtime_error("Loader: no input files");
-    if (out_dtype == "f32") out_bytes_ = 4;
-    else if (out_dtype == "bf16") out_bytes_ = 2;
-    else throw std::runtime_error("out_dtype must be f32 or bf16");
-    src_ = src_dtype;
-    capacity_ = std::max(capacity, min_after_ + batch_);
-    pool_.resize((size_t)capacity_ * elems_ * out_bytes_);
-    free_.reserve(capacity_);
-    for (int i = capacity_ - 1; i >= 0; --i) free_.push_back(i);
-    threads = std::max(1, threads);
-    for (int t = 0; t < threads; ++t) workers_.emplace_back([this] { work(); });
-  }
-
-  ~Loader() { stop(); }
-
-  void stop() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : workers_)
-      if (t.joinable()) t.join();
-    workers_.clear();
-  }
-
-  // fill `batch` examples at dst; returns number filled (< batch only at the end of a non-looping
-  // dataset, 0 when exhausted)
-  int next_batch(uintptr_t dst_ptr) {
-    uint8_t* dst = reinterpret_cast<uint8_t*>(dst_ptr);
-    py::gil_scoped_release nogil;
-    std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [this] {
-      return stop_ || !error_.empty() || (int)filled_.size() >= min_after_ + batch_ ||
-             (done_workers_ == (int)workers_.size() && !filled_.empty()) ||
-             (done_workers_ == (int)workers_.size());
-    });
-    if (!error_.empty()) throw std::runtime_error(error_);
-    int n = 0;
-    const size_t ebytes = elems_ * out_bytes_;
-    while (n < batch_ && !filled_.empty()) {
-      std::uniform_int_distribution<size_t> dist(0, filled_.size() - 1);
-      const size_t k = dist(rng_);
-      const int slot = filled_[k];
-      filled_[k] = filled_.back();
-      filled_.pop_back();
-      std::memcpy(dst + (size_t)n * ebytes, pool_.data() + (size_t)slot * ebytes, ebytes);
-      free_.push_back(slot);
-      ++n;
-    }
-    dequeued_ += n;
-    lk.unlock();
-    cv_.notify_all();
-    return n;
-  }
-
-  py::dict stats() {
-    std::lock_guard<std::mutex> g(mu_);
-    py::dict d;
-    d["records"] = records_.load();
-    d["pooled"] = (int)filled_.size();
-    d["capacity"] = capacity_;
-    d["dequeued"] = dequeued_;
-    d["epochs"] = epochs_;
-    d["fraction_of_capacity_full"] = (double)filled_.size() / capacity_;
-    return d;
-  }
-
- private:
-  bool take_file(std::string* f) {
-    std::lock_guard<std::mutex> g(mu_);
-    if (next_file_ >= order_.size()) {
-      if (epochs_ > 0 && !loop_) return false;
-      order_.resize(files_.size());
-      for (size_t i = 0; i < files_.size(); ++i) order_[i] = i;
-      std::shuffle(order_.begin(), order_.end(), file_rng_);
-      next_file_ = 0;
-      ++epochs_;
-    }
-    *f = files_[order_[next_file_++]];
-    return true;
-  }
-
-  void decode_into(const uint8_t* raw, size_t len, uint8_t* dst) {
-    std::string src = src_;
-    if (src == "auto") {
-      if (len == elems_ * 8) src = "f64";
-      else if (len == elems_ * 4) src = "f32";
-      else if (len == elems_) src = "u8";
-      else throw std::runtime_error("image_raw has " + std::to_string(len) + " bytes, expected " +
-                                    std::to_string(elems_) + " x {1,4,8}");
-    }
-    for (size_t i = 0; i < elems_; ++i) {
-      float v;
-      if (src == "f64") {
-        double d;
-        std::memcpy(&d, raw + 8 * i, 8);
-        v = (float)d;
-      } else if (src == "f32") {
-        std::memcpy(&v, raw + 4 * i, 4);
-      } else {
-        v = raw[i] * u8_scale_ + u8_shift_;
-      }
-      if (out_bytes_ == 4) std::memcpy(dst + 4 * i, &v, 4);
-      else {
-        const uint16_t b = f2bf(v);
-        std::memcpy(dst + 2 * i, &b, 2);
-      }
-    }
-  }
-
-  void work() {
-    std::string fname, rec;
-    std::vector<uint8_t> tmp(elems_ * out_bytes_);
-    try {
-      while (take_file(&fname)) {
-        RecordReader rr(fname, verify_);
-        while (rr.next(&rec)) {
-          const uint8_t* p = nullptr;
-          size_t len = 0;
-          if (!example_bytes_feature(reinterpret_cast<const uint8_t*>(rec.data()), rec.size(), feature_, &p, &len))
-            throw std::runtime_error("record without bytes feature '" + feature_ + "' in " + fname);
-          decode_into(p, len, tmp.data());
-          std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [this] { return stop_ || !free_.empty(); });
-          if (stop_) {
-            lk.unlock();
-            return finish();
-          }
-          const int slot = free_.back();
-          free_.pop_back();
-          std::memcpy(pool_.data() + (size_t)slot * tmp.size(), tmp.data(), tmp.size());
-          filled_.push_back(slot);
-          ++records_;
-          lk.unlock();
-          cv_.notify_all();
-        }
-      }
-    } catch (const std::exception& e) {
-      std::lock_guard<std::mutex> g(mu_);
-      if (error_.empty()) error_ = e.what();
-    }
-    finish();
-  }
-
-  void finish() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      ++done_workers_;
-    }
-    cv_.notify_all();
-  }
-
-  std::vector<std::string> files_;
-  std::string feature_, src_;
-  size_t elems_;
-  int batch_, min_after_, capacity_;
-  bool loop_, verify_;
-  float u8_scale_, u8_shift_;
-  size_t out_bytes_ = 4;
-  std::vector<uint8_t> pool_;
-  std::vector<int> free_, filled_;
-  std::vector<size_t> order_;
-  size_t next_file_ = 0;
-  int epochs_ = 0;
-  uint64_t dequeued_ = 0;
-  std::atomic<uint64_t> records_{0};
-  std::mt19937_64 rng_, file_rng_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stop_ = false;
-  int done_workers_ = 0;
-  std::string error_;
-  std::vector<std::thread> workers_;
-};
 
 // ---------------------------------------------------------------- module
 static uint32_t py_crc32c(py::bytes b, uint32_t crc) {
@@ -273,7 +62,22 @@ PYBIND11_MODULE(_dcgan_host, m) {
            py::arg("capacity"), py::arg("min_after_dequeue"), py::arg("threads"), py::arg("seed"),
            py::arg("out_dtype") = "f32", py::arg("src_dtype") = "auto", py::arg("loop") = true,
            py::arg("verify_crc") = true, py::arg("u8_scale") = 1.0f / 127.5f, py::arg("u8_shift") = -1.0f)
-      .def("next_batch", &Loader::next_batch)
-      .def("stats", &Loader::stats)
+      .def("next_batch",
+           [](Loader& l, uintptr_t dst) {
+             py::gil_scoped_release nogil;
+             return l.next_batch(reinterpret_cast<uint8_t*>(dst));
+           })
+      .def("stats",
+           [](Loader& l) {
+             const LoaderStats st = l.stats();
+             py::dict d;
+             d["records"] = st.records;
+             d["pooled"] = st.pooled;
+             d["capacity"] = st.capacity;
+             d["dequeued"] = st.dequeued;
+             d["epochs"] = st.epochs;
+             d["fraction_of_capacity_full"] = (double)st.pooled / st.capacity;
+             return d;
+           })
       .def("stop", &Loader::stop);
 }

@@ -179,4 +179,30 @@ bool example_bytes_feature(const uint8_t* ex, size_t n, const std::string& key, 
   return found;
 }
 
+// ---------------------------------------------------------------- Example writer
+static void put_varint(std::string* o, uint64_t v) {
+  while (v >= 0x80) {
+    o->push_back((char)(uint8_t)(v | 0x80));
+    v >>= 7;
+  }
+  o->push_back((char)(uint8_t)v);
+}
+
+static void put_len_field(std::string* o, uint8_t tag, const std::string& payload) {
+  o->push_back((char)tag);
+  put_varint(o, payload.size());
+  o->append(payload);
+}
+
+std::string make_bytes_example(const std::string& key, const uint8_t* data, size_t n) {
+  std::string bl, feat, entry, feats, ex;
+  put_len_field(&bl, 0x0A, std::string(reinterpret_cast<const char*>(data), n));  // BytesList.value
+  put_len_field(&feat, 0x0A, bl);                                                   // Feature.bytes_list
+  put_len_field(&entry, 0x0A, key);                                                 // map entry key
+  put_len_field(&entry, 0x12, feat);                                                // map entry value
+  put_len_field(&feats, 0x0A, entry);                                               // Features.feature
+  put_len_field(&ex, 0x0A, feats);                                                  // Example.features
+  return ex;
+}
+
 }  // namespace dcgh

@@ -43,4 +43,8 @@ class RecordWriter {
 bool example_bytes_feature(const uint8_t* ex, size_t n, const std::string& key, const uint8_t** ptr,
                            size_t* len);
 
+// Serialize tf.train.Example{features{feature{key: bytes_list{value: [data]}}}} (the record
+// layout the reference's image_input.py:42-48 parses). Used by the native self-test.
+std::string make_bytes_example(const std::string& key, const uint8_t* data, size_t n);
+
 }  // namespace dcgh
