@@ -469,6 +469,20 @@ class Program {
   }
 
   int sum_partials(std::string name, uintptr_t part, int Pn, int stride, int C, uintptr_t dst, int stream) {
+    const int PS = split_slices(Pn);
+    if (PS > 1) {  // many rows: sliced + last-arrival combine
+      void* ws = nullptr;
+      void* ctr = nullptr;
+      HIPCHECK(hipMalloc(&ws, (size_t)PS * C * sizeof(float)));
+      HIPCHECK(hipMalloc(&ctr, (size_t)((C + 15) / 16) * sizeof(unsigned)));
+      HIPCHECK(hipMemset(ctr, 0, (size_t)((C + 15) / 16) * sizeof(unsigned)));
+      dev_allocs_.push_back(ws);
+      dev_allocs_.push_back(ctr);
+      return add(name, stream, [=](hipStream_t s) {
+        return KF(dcg_sum_partials_split)(P<const float>(part), Pn, stride, C, P<float>(dst),
+                                          reinterpret_cast<float*>(ws), reinterpret_cast<unsigned*>(ctr), PS, s);
+      });
+    }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_sum_partials)(P<const float>(part), Pn, stride, C, P<float>(dst), s);
     });

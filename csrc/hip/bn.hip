@@ -422,6 +422,38 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_split_kernel(
   if (dbeta) dbeta[c] = db;
 }
 
+// ---------------------------------------------------------------- sliced partial-row sums
+// sum_partials over many rows (e.g. the bias-gradient partials of a dgrad GEMM's store pass:
+// ~2k tile rows): grid (ceil(C/16), PS) slices reduce ~64 rows each, `sc1`-store their sums,
+// the last slice per 16-channel group (agent counter, re-armed) adds the slices in slice order.
+__global__ __launch_bounds__(256) void sum_partials_split_kernel(const float* __restrict__ part, int P, int stride,
+                                                                 int C, float* __restrict__ dst, float* ws,
+                                                                 unsigned* counters) {
+  __shared__ int flag;
+  const int cg = blockIdx.x, ps = blockIdx.y, PS = gridDim.y;
+  const int c = cg * 16 + (threadIdx.x & 15);
+  const bool cok = c < C;
+  const int chunk = (P + PS - 1) / PS;
+  const int p0 = ps * chunk, p1 = min(P, p0 + chunk);
+  float s1, unused;
+  reduce_rows2<float>(part, p0, max(p0, p1), (size_t)stride, c, cok, -1, s1, unused);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ws, (uint32_t)((size_t)PS * C * 4));
+  if (threadIdx.x < 16 && cok) st_sc1_f32(rw, (uint32_t)(ps * C + c) * 4u, s1);
+  if (!last_arrival(counters + cg, (unsigned)PS, &flag)) return;
+  if (threadIdx.x >= 16 || !cok) return;
+  float a = 0.f;
+  int q = 0;
+  for (; q + 8 <= PS; q += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld_sc1_f32(rw, (uint32_t)((q + u) * C + c) * 4u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
+  }
+  for (; q < PS; ++q) a += ld_sc1_f32(rw, (uint32_t)(q * C + c) * 4u);
+  dst[c] = a;
+}
+
 // ---------------------------------------------------------------- row-wide finalizes (v2)
 // Same math as the split finalizes above, different reduction layout: a workgroup owns a slice
 // of partial ROWS and all 2C columns of them (16-byte loads along the row; 256 / (C/2) rows in
@@ -709,19 +741,29 @@ __global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __rest
   __shared__ int flag_s;
   if (!last_arrival(counter, gridDim.x, &flag_s)) return;
   const int nb = gridDim.x;
-  const int G = 256 / C;  // block groups summed in parallel, then combined in group order
+  int G = 1;  // power-of-two block groups summed in parallel, then a fixed-order tree
+  while (G * 2 * C <= 256) G *= 2;
   const int c = tid % C, g = tid / C;
   float a = 0.f;
-  if (g < G)
-    for (int b = g; b < nb; b += G) a += ld_sc1_f32(prs, (uint32_t)(b * C + c) * 4u);
-  __syncthreads();
-  if (g < G) red[tid] = a;
-  __syncthreads();
-  if (tid < C) {  // C <= 256 (launcher)
-    float t = 0.f;
-    for (int q = 0; q < G; ++q) t += red[q * C + tid];
-    db[tid] = t;
+  if (g < G) {
+    int b = g;
+    for (; b + 7 * G < nb; b += 8 * G) {  // 8 partial loads in flight
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld_sc1_f32(prs, (uint32_t)((b + u * G) * C + c) * 4u);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; b < nb; b += G) a += ld_sc1_f32(prs, (uint32_t)(b * C + c) * 4u);
   }
+  __syncthreads();
+  if (g < G) red[g * C + c] = a;
+  __syncthreads();
+  for (int h = G / 2; h > 0; h >>= 1) {
+    if (tid < h * C) red[tid] += red[tid + h * C];
+    __syncthreads();
+  }
+  if (tid < C) db[tid] = red[tid];
   if (tid == 0) *counter = 0u;
 }
 
@@ -869,5 +911,12 @@ extern "C" int DCG_API(dcg_bn_finalize_rows)(int mode, const float* part, int pp
   else
     hipLaunchKernelGGL(bn_finalize_rows_kernel<1>, grid, dim3(256), 0, s, part, ppg, groups, C, count, gamma, beta, eps,
                        mean, rstd, scale, shift, ema_mean, ema_var, decay, dgamma, dbeta, coef, ws, counters);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_sum_partials_split)(const float* part, int P, int stride, int C, float* dst, float* ws,
+                                               unsigned* counters, int PS, hipStream_t s) {
+  hipLaunchKernelGGL(sum_partials_split_kernel, dim3((C + 15) / 16, PS), dim3(256), 0, s, part, P, stride, C, dst, ws,
+                     counters);
   return (int)hipGetLastError();
 }

@@ -166,19 +166,36 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
 __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ b, float* __restrict__ out, int R,
                                                         int K) {
-  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (wave >= R) return;
+  // one workgroup per row, each of the 4 waves a quarter of K with all its loads issued up
+  // front (one wave per row walked K serially: latency-bound, 9 us for 256 x 8192)
+  __shared__ float part[4];
+  const int row = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kq = K / 4;  // K % 32 == 0 (launcher): 16-byte chunks per quarter
+  const elem_t* xr = x + (size_t)row * K + wave * kq;
+  const float* wr = w + wave * kq;
   float s = 0.f;
-  for (int k = lane * 8; k < K; k += 512) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)wave * K + k);
-    const elem8 xb = __builtin_bit_cast(elem8, v);
-    const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + k);
-    const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + k + 4);
-    s += (float)xb[0] * w0[0] + (float)xb[1] * w0[1] + (float)xb[2] * w0[2] + (float)xb[3] * w0[3] +
-         (float)xb[4] * w1[0] + (float)xb[5] * w1[1] + (float)xb[6] * w1[2] + (float)xb[7] * w1[3];
+  for (int k0 = lane * 8; k0 < kq; k0 += 4 * 512) {
+    u32x4 xv[4];
+    f32x4 w0[4], w1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * 512 < kq ? k0 + u * 512 : k0;
+      xv[u] = *reinterpret_cast<const u32x4*>(xr + k);
+      w0[u] = *reinterpret_cast<const f32x4*>(wr + k);
+      w1[u] = *reinterpret_cast<const f32x4*>(wr + k + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k0 + u * 512 >= kq) break;
+      const elem8 xb = __builtin_bit_cast(elem8, xv[u]);
+      s += (float)xb[0] * w0[u][0] + (float)xb[1] * w0[u][1] + (float)xb[2] * w0[u][2] + (float)xb[3] * w0[u][3] +
+           (float)xb[4] * w1[u][0] + (float)xb[5] * w1[u][1] + (float)xb[6] * w1[u][2] + (float)xb[7] * w1[u][3];
+    }
   }
   s = wave_sum(s);
-  if (lane == 0) out[wave] = s + b[0];
+  if (lane == 0) part[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[row] = ((part[0] + part[1]) + (part[2] + part[3])) + b[0];
 }
 
 // dx[r][k] = dl[r] * w[k] (elem_t), 8 per thread
@@ -527,8 +544,8 @@ extern "C" int DCG_API(dcg_linear_wgrad)(const float* z, const elem_t* dh, float
 }
 
 extern "C" int DCG_API(dcg_gemv_head)(const elem_t* x, const float* w, const float* b, float* out, int R, int K, hipStream_t s) {
-  if (K % 512) return -2;
-  hipLaunchKernelGGL(gemv_head_kernel, dim3((R + 3) / 4), dim3(256), 0, s, x, w, b, out, R, K);
+  if (K % 32) return -2;
+  hipLaunchKernelGGL(gemv_head_kernel, dim3(R), dim3(256), 0, s, x, w, b, out, R, K);
   return (int)hipGetLastError();
 }
 
