@@ -460,11 +460,15 @@ class Program {
   }
 
   // D head backward (weight + bias + data gradient) in one launch
+  // bx != 0: also the BN-backward partial statistics of the top BN layer -> part
+  // [groups * (K / C)][2][C] (see head_bwd_kernel); dW / db / x may be 0 (g_loss chain: dgrad only)
   int head_bwd(std::string name, uintptr_t x, uintptr_t dl, uintptr_t w, uintptr_t dx, uintptr_t dW, uintptr_t db,
-               int R, int K, int stream) {
+               int R, int K, int stream, uintptr_t bx, uintptr_t by, uintptr_t mean, uintptr_t rstd, int C, int rpg,
+               int act, float leak, uintptr_t part) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_head_bwd)(P<const elem_t>(x), P<const float>(dl), P<const float>(w), P<elem_t>(dx), P<float>(dW),
-                              P<float>(db), R, K, s);
+                              P<float>(db), R, K, P<const elem_t>(bx), P<const elem_t>(by), P<const float>(mean),
+                              P<const float>(rstd), C, rpg, act, leak, P<float>(part), s);
     });
   }
 
@@ -678,7 +682,10 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("act_bwd", &Program::act_bwd)
       .def("sum_partials", &Program::sum_partials)
       .def("act_bwd_dbias", &Program::act_bwd_dbias)
-      .def("head_bwd", &Program::head_bwd)
+      .def("head_bwd", &Program::head_bwd, py::arg("name"), py::arg("x"), py::arg("dl"), py::arg("w"), py::arg("dx"),
+           py::arg("dW"), py::arg("db"), py::arg("R"), py::arg("K"), py::arg("stream"), py::arg("bx") = 0,
+           py::arg("by") = 0, py::arg("mean") = 0, py::arg("rstd") = 0, py::arg("C") = 0, py::arg("rpg") = 0,
+           py::arg("act") = 0, py::arg("leak") = 0.f, py::arg("part") = 0)
       .def("colsum_small", &Program::colsum_small)
       .def("gan_loss", &Program::gan_loss, py::arg("name"), py::arg("logits"), py::arg("B"), py::arg("out"),
            py::arg("dl_d"), py::arg("dl_g"), py::arg("prob"), py::arg("stream"), py::arg("ls") = 0)

@@ -322,23 +322,19 @@ __device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned expecte
 // flight at a time (a plain loop waited on every `sc1` load: ~60 dependent L2 round trips)
 __device__ __forceinline__ void slice_sums(__amdgpu_buffer_rsrc_t rw, int g, int PS, int C, int c, double& a,
                                            double& b) {
-  int q = 0;
-  for (; q + 8 <= PS; q += 8) {
+  for (int q = 0; q < PS; q += 8) {  // guarded rounds of 8: no serial tail
     double va[8], vb[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      va[u] = ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q + u) * 2 + 0) * C + c) * 8u);
-      vb[u] = ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q + u) * 2 + 1) * C + c) * 8u);
+      const bool ok = q + u < PS;
+      va[u] = ok ? ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q + u) * 2 + 0) * C + c) * 8u) : 0.0;
+      vb[u] = ok ? ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q + u) * 2 + 1) * C + c) * 8u) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       a += va[u];
       b += vb[u];
     }
-  }
-  for (; q < PS; ++q) {
-    a += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 0) * C + c) * 8u);
-    b += ld_sc1_f64(rw, (uint32_t)((((size_t)g * PS + q) * 2 + 1) * C + c) * 8u);
   }
 }
 
@@ -442,15 +438,13 @@ __global__ __launch_bounds__(256) void sum_partials_split_kernel(const float* __
   if (!last_arrival(counters + cg, (unsigned)PS, &flag)) return;
   if (threadIdx.x >= 16 || !cok) return;
   float a = 0.f;
-  int q = 0;
-  for (; q + 8 <= PS; q += 8) {
+  for (int q = 0; q < PS; q += 8) {
     float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ld_sc1_f32(rw, (uint32_t)((q + u) * C + c) * 4u);
+    for (int u = 0; u < 8; ++u) v[u] = q + u < PS ? ld_sc1_f32(rw, (uint32_t)((q + u) * C + c) * 4u) : 0.f;
 #pragma unroll
     for (int u = 0; u < 8; ++u) a += v[u];
   }
-  for (; q < PS; ++q) a += ld_sc1_f32(rw, (uint32_t)(q * C + c) * 4u);
   dst[c] = a;
 }
 
@@ -746,15 +740,18 @@ __global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __rest
   const int c = tid % C, g = tid / C;
   float a = 0.f;
   if (g < G) {
-    int b = g;
-    for (; b + 7 * G < nb; b += 8 * G) {  // 8 partial loads in flight
+    // 8 partial loads in flight per round, guarded (no serial tail: every `sc1` load is a full
+    // memory round trip, ~1-2 us)
+    for (int b0 = g; b0 < nb; b0 += 8 * G) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld_sc1_f32(prs, (uint32_t)((b + u * G) * C + c) * 4u);
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * G;
+        v[u] = b < nb ? ld_sc1_f32(prs, (uint32_t)(b * C + c) * 4u) : 0.f;
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) a += v[u];
     }
-    for (; b < nb; b += G) a += ld_sc1_f32(prs, (uint32_t)(b * C + c) * 4u);
   }
   __syncthreads();
   if (g < G) red[g * C + c] = a;

@@ -248,57 +248,119 @@ __global__ void sum_vec_kernel(const float* __restrict__ v, int n, float* __rest
   if (threadIdx.x == 0) out[0] = red[0];
 }
 
-// D head backward of d_loss in ONE launch (was: partial wgrad + split reduce + bias sum + dgrad):
-//   dW[k] = sum_r x[r][k] * dl[r],  db = sum_r dl[r],  dx[r][k] = dl[r] * w[k] (elem_t)
-// block = 64 columns (8 chunks of 8) x 32 row lanes; the row lanes reduce through LDS in a fixed
-// order (deterministic). Block 0's second wave also sums dl for the bias.
-__global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict__ x, const float* __restrict__ dl,
+// D head backward in ONE launch (was: partial wgrad + split reduce + bias sum + dgrad + a
+// column-statistics pass of the BN backward below the head):
+//   dx[r][k] = dl[r] * w[k] (elem_t);  optional  dW[k] = sum_r xa[r][k] * dl[r], db = sum_r dl[r]
+//   optional BN-backward partial statistics of the top BN layer (x = its pre-BN input, y = its
+//   activation, both [R][K] = NHWC-flattened [R][K/C][C]): per group of rows_per_group rows and
+//   per spatial position s = k / C, part[g * (K/C) + s][0|1][c] = (sum g, sum g * xhat),
+//   g = dx * act'(y), xhat = (x - mean[g][c]) * rstd[g][c] -- of the STORED (rounded) dx.
+// block = 64 columns (8 chunks of 8, inside one spatial position) x 32 row lanes; row lanes
+// reduce through LDS in a fixed order (deterministic). Block 0's second wave sums dl for db.
+__global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict__ xa, const float* __restrict__ dl,
                                                        const float* __restrict__ w, elem_t* __restrict__ dx,
-                                                       float* __restrict__ dW, float* __restrict__ db, int R, int K) {
+                                                       float* __restrict__ dW, float* __restrict__ db, int R, int K,
+                                                       const elem_t* __restrict__ bx, const elem_t* __restrict__ by,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       int C, int rpg, int act, float leak, float* __restrict__ part) {
   __shared__ float red[32][65];
+  __shared__ float bred[2][2][32][65];  // [group][stat][lane][col]
   const int tid = threadIdx.x, c = tid & 7, rl = tid >> 3;
   const int k = blockIdx.x * 64 + c * 8;
-  const bool kok = k < K;  // K % 8 == 0 (launcher)
-  float s[8], wv[8];
+  const bool kok = k < K;  // K % 64 == 0 when stats are requested (launcher); K % 8 otherwise
+  const bool stats = bx != nullptr;
+  const int ch = stats ? k % C : 0;
+  float s[8], wv[8], mu[2][8], rs[2][8], t1[2][8], t2[2][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     s[i] = 0.f;
     wv[i] = kok ? w[k + i] : 0.f;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      mu[g][i] = (stats && kok && g * rpg < R) ? mean[g * C + ch + i] : 0.f;
+      rs[g][i] = (stats && kok && g * rpg < R) ? rstd[g * C + ch + i] : 0.f;
+      t1[g][i] = 0.f;
+      t2[g][i] = 0.f;
+    }
   }
+  const float slope = act == ACT_LRELU ? leak : 0.f;
   if (kok) {
     for (int rb = rl; rb < R; rb += 4 * 32) {  // 4 rows per iteration, loads first
-      u32x4 xv[4];
+      u32x4 xv[4], yv[4], xb[4];
       float gv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = rb + 32 * u < R ? rb + 32 * u : rb;
-        xv[u] = *reinterpret_cast<const u32x4*>(x + (size_t)r * K + k);
+        const size_t o = (size_t)r * K + k;
+        xv[u] = xa ? *reinterpret_cast<const u32x4*>(xa + o) : u32x4{0, 0, 0, 0};
+        if (stats) {
+          yv[u] = *reinterpret_cast<const u32x4*>(by + o);
+          xb[u] = *reinterpret_cast<const u32x4*>(bx + o);
+        }
         gv[u] = dl[r];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = rb + 32 * u;
         if (r >= R) break;
-        const elem8 xb = __builtin_bit_cast(elem8, xv[u]);
+        const int grp = r >= rpg ? 1 : 0;
+        const elem8 xe = __builtin_bit_cast(elem8, xv[u]);
         elem8 ob;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          s[i] += (float)xb[i] * gv[u];
+          s[i] += (float)xe[i] * gv[u];
           ob[i] = (elem_t)(gv[u] * wv[i]);
         }
         *reinterpret_cast<u32x4*>(dx + (size_t)r * K + k) = __builtin_bit_cast(u32x4, ob);
+        if (stats) {
+          const elem8 ye = __builtin_bit_cast(elem8, yv[u]), be = __builtin_bit_cast(elem8, xb[u]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float g = (float)ob[i] * ((float)ye[i] > 0.f ? 1.f : slope);
+            const float xh = ((float)be[i] - mu[grp][i]) * rs[grp][i];
+            t1[grp][i] += g;
+            t2[grp][i] += g * xh;
+          }
+        }
       }
     }
   }
+  if (dW) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) red[rl][c * 8 + i] = s[i];
+    for (int i = 0; i < 8; ++i) red[rl][c * 8 + i] = s[i];
+  }
+  if (stats) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bred[g][0][rl][c * 8 + i] = t1[g][i];
+        bred[g][1][rl][c * 8 + i] = t2[g][i];
+      }
+  }
   __syncthreads();
-  if (tid < 64 && blockIdx.x * 64 + tid < K) {
+  if (dW && tid < 64 && blockIdx.x * 64 + tid < K) {
     float a = 0.f;
     for (int l = 0; l < 32; ++l) a += red[l][tid];
     dW[blockIdx.x * 64 + tid] = a;
   }
-  if (blockIdx.x == 0 && tid >= 64 && tid < 128) {
+  if (stats) {
+    for (int h = 16; h > 0; h >>= 1) {  // fixed-order tree over the 32 row lanes
+      for (int q = tid; q < 2 * 2 * h * 64; q += 256) {
+        const int col = q & 63, l = (q >> 6) % h, gs = q / (64 * h);
+        float* base = &bred[gs >> 1][gs & 1][0][0];
+        base[l * 65 + col] += base[(l + h) * 65 + col];
+      }
+      __syncthreads();
+    }
+    const int groups = (R + rpg - 1) / rpg, S = K / C;
+    const int k0 = blockIdx.x * 64, sp = k0 / C, c0 = k0 % C;
+    for (int q = tid; q < groups * 2 * 64; q += 256) {
+      const int col = q & 63, st = (q >> 6) & 1, g = q >> 7;
+      part[((size_t)(g * S + sp) * 2 + st) * C + c0 + col] = bred[g][st][0][col];
+    }
+  }
+  if (db && blockIdx.x == 0 && tid >= 64 && tid < 128) {
     const int lane = tid - 64;
     float a = 0.f;
     for (int r = lane; r < R; r += 64) a += dl[r];
@@ -645,8 +707,13 @@ extern "C" int DCG_API(dcg_cast_bf16_f32)(const elem_t* src, float* dst, size_t 
 }
 
 extern "C" int DCG_API(dcg_head_bwd)(const elem_t* x, const float* dl, const float* w, elem_t* dx, float* dW, float* db,
-                                     int R, int K, hipStream_t s) {
+                                     int R, int K, const elem_t* bx, const elem_t* by, const float* mean,
+                                     const float* rstd, int C, int rpg, int act, float leak, float* part,
+                                     hipStream_t s) {
   if (K % 8) return -2;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3((K + 63) / 64), dim3(256), 0, s, x, dl, w, dx, dW, db, R, K);
+  if (bx && (C <= 0 || C % 64 || K % C || rpg <= 0 || (R + rpg - 1) / rpg > 2 || !by || !mean || !rstd || !part))
+    return -2;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((K + 63) / 64), dim3(256), 0, s, x, dl, w, dx, dW, db, R, K, bx, by, mean,
+                     rstd, C, rpg > 0 ? rpg : R, act, leak, part);
   return (int)hipGetLastError();
 }

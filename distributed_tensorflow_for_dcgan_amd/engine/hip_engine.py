@@ -415,11 +415,11 @@ class HipEngine:
                             cfg.d_lin_in, 16, _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), 0)
             prog.head_dgrad("d_head.dgrad", _p(self.dl_d), _p(Pd[lin + "/Matrix"]), _p(self.d_da[last.name]), B2,
                             cfg.d_lin_in, 0)
+            fused_next = None
         else:
-            prog.head_bwd("d_head.bwd", _p(self.d_a[last.name]), _p(self.dl_d), _p(Pd[lin + "/Matrix"]),
-                          _p(self.d_da[last.name]), _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), B2,
-                          cfg.d_lin_in, 0)
-        fused_next = None  # BN-backward partials emitted by the previous (upper) layer's dgrad GEMM
+            fused_next = self._head_bwd(prog, "d_head.bwd", self.d_a[last.name], self.dl_d, self.d_da[last.name],
+                                        gD[lin + "/Matrix"], gD[lin + "/bias"], B2, last, 2, 0)
+        # fused_next: BN-backward partials emitted by the layer above (head / dgrad GEMM store pass)
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
             rows = B2 * L.out_hw ** 2
@@ -477,6 +477,29 @@ class HipEngine:
         else:
             prog.act_bwd(name, _p(dy), _p(y), _p(dx), dx.numel(), act, leak, 0)
             self._colsum(prog, name + ".dbias", dx, rows, C, db)
+
+    def _head_bwd(self, prog, name, xa, dl, dx, dW, db, R, last, groups, group_offset):
+        """D head backward (dx, optional dW / db) with the top BN layer's backward statistics
+        fused in: returns (partials, partials per group) for _bn_bwd, or None when the layer
+        below the head has no BN / an unsupported channel count (then _bn_bwd runs its own
+        statistics pass). group_offset 1 = the fake half only (g_loss chain)."""
+        cfg = self.cfg
+        Pd = self.model.d
+        lin = cfg.d_lin_name
+        K = cfg.d_lin_in
+        C = last.cout
+        ok = bool(last.bn) and C % 64 == 0 and K % C == 0 and os.environ.get("DCGAN_NO_HEAD_STATS") != "1"
+        if not ok:
+            prog.head_bwd(name, _p(xa), _p(dl), _p(Pd[lin + "/Matrix"]), _p(dx), _p(dW), _p(db), R, K, 0)
+            return None
+        S = K // C
+        part = self._stats_buf(name + ".bnstats", groups * S, C)
+        st = self.bn[last.bn]
+        r0 = 0 if group_offset == 0 else self.B
+        prog.head_bwd(name, _p(xa), _p(dl), _p(Pd[lin + "/Matrix"]), _p(dx), _p(dW), _p(db), R, K, 0,
+                      _p(self.d_x[last.name][r0:]), _p(self.d_a[last.name][r0:]), _p(st["mean"][group_offset:]),
+                      _p(st["rstd"][group_offset:]), C, R // groups, LRELU, cfg.lrelu_leak, _p(part))
+        return part, S
 
     def _colsum(self, prog, name, x, rows, C, dst):
         if C % 8 == 0:
@@ -564,9 +587,8 @@ class HipEngine:
         lin = cfg.d_lin_name
         last = self.dl[-1]
         half = lambda t: t[B:]  # noqa: E731  fake half of a [2B, ...] buffer
-        prog.head_dgrad("g.d_head.dgrad", _p(self.dl_g), _p(Pd[lin + "/Matrix"]), _p(half(self.d_da[last.name])), B,
-                        cfg.d_lin_in, 0)
-        fused_next = None
+        fused_next = self._head_bwd(prog, "g.d_head.dgrad", None, self.dl_g, half(self.d_da[last.name]), None, None,
+                                    B, last, 1, 1)
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
             rows = B * L.out_hw ** 2

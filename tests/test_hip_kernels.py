@@ -542,3 +542,36 @@ def test_head_bwd_fused(R, K):
     close(dW, x.float().t() @ dl, 1e-4, "head dW")
     close(db, dl.sum(0, keepdim=True), 1e-5, "head db")
     assert torch.equal(dx, (dl[:, None] * w[None, :]).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("R,groups", [(256, 2), (128, 1)])
+def test_head_bwd_bn_stats(R, groups):
+    """Head backward with the top BN layer's backward statistics fused in: per (group, spatial
+    position) partial rows of (sum g, sum g * xhat), g = dx * lrelu'(y), from the stored dx."""
+    h = H()
+    K, C = 8192, 512
+    S = K // C
+    xa = bf(rnd(R, K, seed=95))
+    dl = rnd(R, seed=96)
+    w = rnd(K, scale=0.02, seed=97)
+    bx = bf(rnd(R, K, seed=98))
+    by = bf(rnd(R, K, seed=99))
+    mean = rnd(groups, C, scale=0.1, seed=100)
+    rstd = rnd(groups, C, seed=101).abs() + 0.5
+    dx = torch.empty_like(xa)
+    dW = torch.empty(K, device=dev)
+    db = torch.empty(1, device=dev)
+    part = torch.full((groups * S, 2, C), float("nan"), device=dev)
+    pr = _prog()
+    pr.head_bwd("hb", _p(xa), _p(dl), _p(w), _p(dx), _p(dW), _p(db), R, K, 0, _p(bx), _p(by), _p(mean), _p(rstd), C,
+                R // groups, 2, 0.2, _p(part))
+    h.run(pr)
+    assert torch.equal(dx, (dl[:, None] * w[None, :]).to(torch.bfloat16))
+    close(dW, xa.float().t() @ dl, 1e-4, "dW")
+    g = dx.float() * torch.where(by.float() > 0, 1.0, 0.2)
+    rpg = R // groups
+    for gi in range(groups):
+        gg = g[gi * rpg:(gi + 1) * rpg].reshape(rpg, S, C)
+        xh = (bx.float()[gi * rpg:(gi + 1) * rpg].reshape(rpg, S, C) - mean[gi]) * rstd[gi]
+        close(part[gi * S:(gi + 1) * S, 0], gg.sum(0), 1e-4, "sum g")
+        close(part[gi * S:(gi + 1) * S, 1], (gg * xh).sum(0), 1e-4, "sum g xhat")
