@@ -57,12 +57,17 @@ def main():
         kt = -(-K // 64)
         progs, outs = {}, {}
         c0, s0 = H.pick_wgrad(Mc, Nc, K, 25)
-        slabs = torch.empty(s0, 25, Mc, Nc, device=dev)
-        outs[(0, s0)] = torch.empty(25, Mc, Nc, device=dev)
-        p = ext.Program()
-        p.wgrad(name, 0, G.data_ptr(), Hg, Wg, Mc, Dm.data_ptr(), Bn, Hd, Wd, Nc, pad, c0, s0, slabs.data_ptr(),
-                outs[(0, s0)].data_ptr(), 25 * Mc * Nc, 1.0, 0)
-        progs[(0, s0)] = p
+        keep = []
+        for sw in sorted({s0, 4, 8, 12, 16, 24, 32}):  # wgrad.hip (+ its slab reduce) at several split counts
+            if sw > 1 and kt // sw < 4:
+                continue
+            slabs = torch.empty(sw, 25, Mc, Nc, device=dev)
+            keep.append(slabs)
+            outs[(0, sw)] = torch.empty(25, Mc, Nc, device=dev)
+            p = ext.Program()
+            p.wgrad(name, 0, G.data_ptr(), Hg, Wg, Mc, Dm.data_ptr(), Bn, Hd, Wd, Nc, pad, c0, sw, slabs.data_ptr(),
+                    outs[(0, sw)].data_ptr(), 25 * Mc * Nc, 1.0, 0)
+            progs[(0, sw)] = p
         for c3 in (300, 301, 302, 303, 310, 311, 312, 313):
             bm, bn = H.WGRAD3_TILES[c3 % 10]
             if bm > max(Mc, 64) or bn > max(Nc, 64):
@@ -98,7 +103,7 @@ def main():
         res.sort()
         good = [r for r in res if r[1] not in bad]
         best_t, (bc, bsp) = good[0]
-        old_t = [t for t, c in res if c[0] == 0][0]
+        old_t = [t for t, c in res if c == (0, s0)][0]
         print("%-14s Mc=%4d Nc=%4d K=%7d  wgrad.hip %7.1f us | best %3d:%-2d %7.1f us %6.0f TF/s | bad %s | %s" %
               (name, Mc, Nc, K, old_t, bc, bsp, best_t, fl / best_t / 1e6, sorted(bad) or "-",
                " ".join("%d:%d:%.0f" % (c[0], c[1], t) for t, c in good[:6])), flush=True)

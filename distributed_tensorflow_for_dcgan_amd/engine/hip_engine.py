@@ -525,6 +525,8 @@ class HipEngine:
                             _p(dst), 1.0, self.SIDE)
                 return
         cfg, splits = H.pick_wgrad(Mc, Nc, K, taps)
+        if mode == 0:
+            splits = H.wgrad_splits_for(Mc, Nc, Bn, Hd, Wd, Hg) or splits
         slabs = self._t(splits, taps, Mc, Nc, dtype=torch.float32)
         self._keep.append(slabs)
         prog.wgrad(name + ".wgrad", mode, _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(slabs),

@@ -236,6 +236,12 @@ def wgrad3_key(Mc: int, Nc: int, Bn: int, Hd: int, Wd: int, Hg: int) -> str:
     return "w3,%d,%d,%d,%d,%d,%d" % (Mc, Nc, Bn, Hd, Wd, Hg)
 
 
+def wgrad_splits_for(Mc: int, Nc: int, Bn: int, Hd: int, Wd: int, Hg: int) -> Optional[int]:
+    """Tuned split count for wgrad.hip on a 25-tap layer (entry "0:splits"), or None."""
+    ent = tuned_table().get(wgrad3_key(Mc, Nc, Bn, Hd, Wd, Hg))
+    return ent[1] if ent is not None and ent[0] == 0 and ent[1] >= 1 else None
+
+
 def wgrad3_cfg_for(Mc: int, Nc: int, Bn: int, Hd: int, Wd: int, Hg: int) -> Optional[Tuple[int, int]]:
     """(cfg, splits) for a 25-tap weight gradient on wgrad3.hip, or None to keep wgrad.hip:
     the tuned entry (benchmarks/bench_wgrad.py --write; cfg 0 = wgrad.hip measured faster),
