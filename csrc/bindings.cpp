@@ -507,11 +507,13 @@ class Program {
   }
   // stats (optional): BN partial statistics of the output, channel = column % C ->
   // [(B / 8) * (N / C)][2][C] partial rows (the row block of the kernel is 8)
+  // gen_step != 0: z ~ U(-1,1) generated in-kernel (Philox keyed by gen_seed and the device
+  // step counter, identical to philox_uniform) and written to z
   int linear_fwd(std::string name, uintptr_t z, uintptr_t W, uintptr_t b, uintptr_t out, int B, int K, int N,
-                 int stream, uintptr_t stats = 0, int C = 0) {
+                 int stream, uintptr_t stats = 0, int C = 0, uintptr_t gen_step = 0, uint64_t gen_seed = 0) {
     return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_linear_fwd)(P<const float>(z), P<const float>(W), P<const float>(b), P<elem_t>(out), B, K, N,
-                                P<float>(stats), C, s);
+      return KF(dcg_linear_fwd)(P<float>(z), P<const float>(W), P<const float>(b), P<elem_t>(out), B, K, N,
+                                P<float>(stats), C, P<const unsigned long long>(gen_step), gen_seed, s);
     });
   }
   int linear_wgrad(std::string name, uintptr_t z, uintptr_t dh, uintptr_t dW, uintptr_t db, int B, int K, int N,
@@ -691,7 +693,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("dl_d"), py::arg("dl_g"), py::arg("prob"), py::arg("stream"), py::arg("ls") = 0)
       .def("linear_fwd", &Program::linear_fwd, py::arg("name"), py::arg("z"), py::arg("W"), py::arg("b"),
            py::arg("out"), py::arg("B"), py::arg("K"), py::arg("N"), py::arg("stream"), py::arg("stats") = 0,
-           py::arg("C") = 0)
+           py::arg("C") = 0, py::arg("gen_step") = 0, py::arg("gen_seed") = 0)
       .def("linear_wgrad", &Program::linear_wgrad)
       .def("gemv_head", &Program::gemv_head)
       .def("head_dgrad", &Program::head_dgrad)

@@ -52,21 +52,64 @@ __global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- Philox z ~ U(-1, 1)
+__device__ __forceinline__ void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                             uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+  const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+  const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+  c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+}
+
+// 4 uniforms of counter i4 (Philox-4x32-10 keyed by seed, counter = (i4, step, stream)) in [lo, hi)
+__device__ __forceinline__ float philox_uniform_at(size_t idx, uint64_t seed, uint64_t st, uint64_t stream_id,
+                                                   float lo, float hi) {
+  const size_t i4 = idx >> 2;
+  uint32_t c0 = (uint32_t)i4, c1 = (uint32_t)(i4 >> 32), c2 = (uint32_t)st, c3 = (uint32_t)(st >> 32) ^ (uint32_t)stream_id;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c0, c1, c2, c3, k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const int j = (int)(idx & 3);
+  const uint32_t cj = j == 0 ? c0 : (j == 1 ? c1 : (j == 2 ? c2 : c3));
+  return lo + (hi - lo) * ((float)(cj >> 8) * (1.0f / 16777216.0f));
+}
+
 // ---------------------------------------------------------------- linear: out = z @ W + b
 // z fp32 [B][K], W fp32 [K][N], out elem_t [B][N]; block = 256 columns x RB rows.
 // Latency-bound (each thread walks K = 100 W rows): 20 independent W loads in flight.
 // stats != nullptr: also the BN partial statistics of the stored (rounded) output, channel =
 // column % C, one partial row per (row block, column / C) -> part[P][2][C] (no colstats pass).
+// gen_step != nullptr: z is not read but generated here -- z ~ U(-1,1) by Philox keyed by
+// (gen_seed, *gen_step), bit-identical to philox_uniform_kernel -- and written to z by the
+// column-0 blocks (the backward and the summaries read it): one launch less per step.
 template <int RB>
-__global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ z, const float* __restrict__ W,
+__global__ __launch_bounds__(256) void linear_fwd_kernel(float* __restrict__ z, const float* __restrict__ W,
                                                          const float* __restrict__ bias, elem_t* __restrict__ out,
-                                                         int B, int K, int N, float* __restrict__ stats, int C) {
+                                                         int B, int K, int N, float* __restrict__ stats, int C,
+                                                         const unsigned long long* __restrict__ gen_step,
+                                                         uint64_t gen_seed) {
   extern __shared__ __attribute__((aligned(16))) float zs[];  // [RB][K]
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * RB;
+  const uint64_t st = gen_step ? gen_step[0] : 0ull;
   for (int i = threadIdx.x; i < RB * K; i += 256) {
     const int r = i / K, k = i - r * K;
-    zs[i] = (r0 + r < B) ? z[(size_t)(r0 + r) * K + k] : 0.f;
+    float v = 0.f;
+    if (r0 + r < B) {
+      const size_t idx = (size_t)(r0 + r) * K + k;
+      if (gen_step) {
+        v = philox_uniform_at(idx, gen_seed, st, 0, -1.f, 1.f);
+        if (blockIdx.x == 0) z[idx] = v;
+      } else {
+        v = z[idx];
+      }
+    }
+    zs[i] = v;
   }
   __syncthreads();
   if (n >= N) return;
@@ -466,16 +509,6 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
   }
 }
 
-// ---------------------------------------------------------------- Philox z ~ U(-1, 1)
-__device__ __forceinline__ void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
-                                             uint32_t k1) {
-  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
-  const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
-  const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-  c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-}
-
 __global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__ out, size_t n, uint64_t seed,
                                                              const unsigned long long* __restrict__ step,
                                                              uint64_t stream_id, float lo, float hi) {
@@ -586,13 +619,14 @@ extern "C" int DCG_API(dcg_gan_loss)(const float* logits, int B, float* out, flo
   return (int)hipGetLastError();
 }
 
-extern "C" int DCG_API(dcg_linear_fwd)(const float* z, const float* W, const float* b, elem_t* out, int B, int K, int N,
-                              float* stats, int C, hipStream_t s) {
+extern "C" int DCG_API(dcg_linear_fwd)(float* z, const float* W, const float* b, elem_t* out, int B, int K, int N,
+                              float* stats, int C, const unsigned long long* gen_step, uint64_t gen_seed,
+                              hipStream_t s) {
   if (stats && (C <= 0 || N % C)) return -2;
   constexpr int RB = 8;  // (N/256) x (B/8) = 512 blocks for the 64x64 model at B=128
   dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
   hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N,
-                     stats, C);
+                     stats, C, gen_step, gen_seed);
   return (int)hipGetLastError();
 }
 

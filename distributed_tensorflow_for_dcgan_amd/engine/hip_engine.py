@@ -332,9 +332,12 @@ class HipEngine:
         cfg, B = self.cfg, self.B
         B2 = 2 * B
         Pg, Pd = self.model.g, self.model.d
-        if train_z:
-            prog.philox_uniform("z", _p(z), z.numel(), self.seed * 1000003 + 17 + 7919 * self.rank * int(self.rank_seeded_z),
-                                _p(self.step_counter), 0, -1.0, 1.0, 0)
+        zseed = self.seed * 1000003 + 17 + 7919 * self.rank * int(self.rank_seeded_z)
+        # train_z: z ~ U(-1,1) generated inside the projection kernel (Philox keyed by the device
+        # step counter; DCGAN_SEPARATE_PHILOX=1 keeps the standalone kernel for A/B)
+        gen_in_linear = train_z and os.environ.get("DCGAN_SEPARATE_PHILOX") != "1"
+        if train_z and not gen_in_linear:
+            prog.philox_uniform("z", _p(z), z.numel(), zseed, _p(self.step_counter), 0, -1.0, 1.0, 0)
         # G projection + g_bn0 + relu
         C0 = cfg.g_base_ch
         rows0 = B * cfg.g_base_hw ** 2
@@ -343,7 +346,8 @@ class HipEngine:
         P0 = -(-B // 8) * (cfg.g_lin_out // C0)
         part0 = self._stats_buf("g_bn0", P0, C0)
         prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
-                        B, cfg.z_dim, cfg.g_lin_out, 0, _p(part0), C0)
+                        B, cfg.z_dim, cfg.g_lin_out, 0, _p(part0), C0,
+                        _p(self.step_counter) if gen_in_linear else 0, zseed if gen_in_linear else 0)
         self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, P0, update_ema)
         a_prev = self.g_h0
         Wg, Wd = self.wbf_g, self.wbf_d

@@ -399,6 +399,16 @@ def test_linear_and_head():
     close(part[:, 1].sum(0), (o * o).sum((0, 1)), 1e-5, "linear stats sumsq")
     ob = torch.nn.functional.pad(o, (0, 0, 0, 0, 0, 40 - B)).reshape(5, 8, N // C, C).sum(1).reshape(-1, C)
     close(part[:, 0], ob, 1e-5, "linear stats per block")
+    # z generated inside the kernel == philox_uniform + linear (bit-identical z and output)
+    step = torch.tensor([7], dtype=torch.int64, device=dev)
+    z1, z2 = torch.empty(B, K, device=dev), torch.full((B, K), float("nan"), device=dev)
+    o1, o2 = torch.empty_like(out), torch.empty_like(out)
+    pr = _prog()
+    pr.philox_uniform("z", _p(z1), z1.numel(), 123457, _p(step), 0, -1.0, 1.0, 0)
+    pr.linear_fwd("lin", _p(z1), _p(W), _p(b), _p(o1), B, K, N, 0)
+    pr.linear_fwd("lin_gen", _p(z2), _p(W), _p(b), _p(o2), B, K, N, 0, 0, 0, _p(step), 123457)
+    h.run(pr)
+    assert torch.equal(z1, z2) and torch.equal(o1, o2)
     # D head
     R_, Kh = 2 * B, 8192
     x = bf(rnd(R_, Kh, seed=37))
