@@ -23,6 +23,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=0, help="timed steps at the end of the trace")
     ap.add_argument("--match", default="dcg", help="substring of our kernels (mangled names too)")
+    ap.add_argument("--marker", default="linear_fwd_kernel", help="first kernel of a training step")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, accum_vgpr_count, "
@@ -41,7 +42,11 @@ def main():
     if a.steps:
         per = len(ours) // max(1, a.steps + 0)
         # find the period: number of dispatches of the first kernel in the step (philox)
-        first = [i for i, r in enumerate(ours) if "philox" in r[0]]
+        # first kernel of every training step: the G projection (it also generates z); older
+        # traces started the step with the standalone Philox kernel
+        first = [i for i, r in enumerate(ours) if a.marker in r[0]]
+        if len(first) < 2:
+            first = [i for i, r in enumerate(ours) if "philox" in r[0]]
         if len(first) >= 2:
             per = first[-1] - first[-2]
             last = ours[first[-2]:first[-1]]
