@@ -444,7 +444,7 @@ class Program {
   // dx = dy * act'(y) and db = column sums of dx in one launch (last-arrival reduction)
   int act_bwd_dbias(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, int R, int C, int act, float leak,
                     uintptr_t db, int stream) {
-    const int max_blocks = 1024;
+    const int max_blocks = 256;  // every block bumps one arrival counter: keep the atomics few
     void* part = nullptr;
     void* ctr = nullptr;
     HIPCHECK(hipMalloc(&part, (size_t)max_blocks * C * sizeof(float)));
@@ -522,9 +522,21 @@ class Program {
       return KF(dcg_linear_wgrad)(P<const float>(z), P<const elem_t>(dh), P<float>(dW), P<float>(db), B, K, N, s);
     });
   }
-  int gemv_head(std::string name, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int R, int K, int stream) {
+  // loss_out != 0: the 3-loss BCE (gan_loss) runs in the GEMV's last-arriving block
+  int gemv_head(std::string name, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int R, int K, int stream,
+                uintptr_t loss_out, uintptr_t dl_d, uintptr_t dl_g, uintptr_t prob, uintptr_t ls) {
+    unsigned* ctr = nullptr;
+    if (loss_out) {
+      void* c = nullptr;
+      HIPCHECK(hipMalloc(&c, sizeof(unsigned)));
+      HIPCHECK(hipMemset(c, 0, sizeof(unsigned)));
+      dev_allocs_.push_back(c);
+      ctr = reinterpret_cast<unsigned*>(c);
+    }
     return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_gemv_head)(P<const elem_t>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, s);
+      return KF(dcg_gemv_head)(P<const elem_t>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, ctr,
+                               P<float>(loss_out), P<float>(dl_d), P<float>(dl_g), P<float>(prob), P<const float>(ls),
+                               s);
     });
   }
   int head_dgrad(std::string name, uintptr_t dl, uintptr_t w, uintptr_t dx, int R, int K, int stream) {
@@ -552,6 +564,22 @@ class Program {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_adam)(P<float>(w), P<elem_t>(wbf), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers),
                       n, lr, b1, b2, eps, gscale, P<const float>(ls), s);
+    });
+  }
+  // both TF-Adams (A first) + beta powers / step counter in one launch (see adam2_kernel)
+  int adam2(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA, uintptr_t pA,
+            size_t nA, float lrA, float b1A, float b2A, float epsA, uintptr_t wD, uintptr_t wbfD, uintptr_t gD,
+            uintptr_t mD, uintptr_t vD, uintptr_t pD, size_t nD, float lrD, float b1D, float b2D, float epsD,
+            float gscale, uintptr_t step, int stream) {
+    void* ctr = nullptr;
+    HIPCHECK(hipMalloc(&ctr, sizeof(unsigned)));
+    HIPCHECK(hipMemset(ctr, 0, sizeof(unsigned)));
+    dev_allocs_.push_back(ctr);
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_adam2)(P<float>(wA), P<elem_t>(wbfA), P<const float>(gA), P<float>(mA), P<float>(vA), P<float>(pA),
+                           nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD), P<float>(mD),
+                           P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, gscale,
+                           P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
     });
   }
   // TF-SAME stride-2 5x5 conv_transpose with 1..4 output channels (direct VALU kernel)
@@ -695,7 +723,9 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("out"), py::arg("B"), py::arg("K"), py::arg("N"), py::arg("stream"), py::arg("stats") = 0,
            py::arg("C") = 0, py::arg("gen_step") = 0, py::arg("gen_seed") = 0)
       .def("linear_wgrad", &Program::linear_wgrad)
-      .def("gemv_head", &Program::gemv_head)
+      .def("gemv_head", &Program::gemv_head, py::arg("name"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("out"),
+           py::arg("R"), py::arg("K"), py::arg("stream"), py::arg("loss_out") = 0, py::arg("dl_d") = 0,
+           py::arg("dl_g") = 0, py::arg("prob") = 0, py::arg("ls") = 0)
       .def("head_dgrad", &Program::head_dgrad)
       .def("head_wgrad", &Program::head_wgrad)
       .def("adam", &Program::adam)
@@ -705,6 +735,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("step_end", &Program::step_end, py::arg("name"), py::arg("pd"), py::arg("pg"), py::arg("b1d"),
            py::arg("b2d"), py::arg("b1g"), py::arg("b2g"), py::arg("step"), py::arg("stream"), py::arg("ls") = 0,
            py::arg("growth_interval") = 2000)
+      .def("adam2", &Program::adam2)
       .def("nonfinite_check", &Program::nonfinite_check)
       .def("narrow_deconv", &Program::narrow_deconv)
       .def("pack", &Program::pack)

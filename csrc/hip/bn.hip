@@ -870,7 +870,7 @@ extern "C" int DCG_API(dcg_act_bwd_dbias)(const elem_t* dy, const elem_t* y, ele
   if (C % 8 == 0) {
     if (C > 256 || 256 % (C / 8)) return -2;
     const int RL = 256 / (C / 8);
-    per_block = RL * 16;  // 16 rows per thread
+    per_block = RL * 16;  // 16 rows per thread (<= max_blocks: one same-address atomic per block)
     blocks = (R + per_block - 1) / per_block;
     if (blocks > max_blocks) { per_block = (R + max_blocks - 1) / max_blocks; blocks = (R + per_block - 1) / per_block; }
     hipLaunchKernelGGL(act_bwd_dbias_kernel<0>, dim3(blocks), dim3(256), 0, s, dy, y, dx, R, C, per_block, act, leak,

@@ -6,6 +6,8 @@
 //   * elem_t weight packing (natural + per-tap transposed / im2col-ordered copies)
 //   * Philox-4x32-10 z ~ U(-1,1) keyed by a device step counter (K19, graph-capturable)
 //   * stride-2 TF-SAME im2col for 3-channel tensors, dtype casts
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace dcg {
@@ -13,17 +15,19 @@ namespace dcg {
 // ---------------------------------------------------------------- losses
 // logits: [2B] (real rows first). out[0..3] = d_loss_real, d_loss_fake, g_loss, d_loss;
 // dl_d[2B] = d d_loss / d logit; dl_g[B] = d g_loss / d logit_fake; prob[2B] = sigmoid.
-__global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__ logits, int B,
-                                                       float* __restrict__ out, float* __restrict__ dl_d,
-                                                       float* __restrict__ dl_g, float* __restrict__ prob,
-                                                       const float* __restrict__ ls) {
+// The block-wide body, shared by the standalone kernel and the head GEMV's last-arriving block;
+// logit(i) fetches logit i.
+template <typename F>
+__device__ __forceinline__ void gan_loss_block(F logit, int B, float* __restrict__ out, float* __restrict__ dl_d,
+                                               float* __restrict__ dl_g, float* __restrict__ prob,
+                                               const float* __restrict__ ls) {
   __shared__ float red[3][256];
   float lr = 0.f, lf = 0.f, lg = 0.f;
   const float invB = 1.f / (float)B;
   // fp16 training: the gradient seeds carry the dynamic loss scale ls[0] (the losses do not)
   const float gB = ls ? ls[0] * invB : invB;
   for (int i = threadIdx.x; i < 2 * B; i += 256) {
-    const float x = logits[i];
+    const float x = logit(i);
     const float sp = log1pf(expf(-fabsf(x)));
     const float sg = 1.f / (1.f + expf(-x));
     if (prob) prob[i] = sg;
@@ -50,6 +54,13 @@ __global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__
     const float a = red[0][0] * invB, b = red[1][0] * invB, c = red[2][0] * invB;
     out[0] = a; out[1] = b; out[2] = c; out[3] = a + b;
   }
+}
+
+__global__ __launch_bounds__(256) void gan_loss_kernel(const float* __restrict__ logits, int B,
+                                                       float* __restrict__ out, float* __restrict__ dl_d,
+                                                       float* __restrict__ dl_g, float* __restrict__ prob,
+                                                       const float* __restrict__ ls) {
+  gan_loss_block([&](int i) { return logits[i]; }, B, out, dl_d, dl_g, prob, ls);
 }
 
 // ---------------------------------------------------------------- Philox z ~ U(-1, 1)
@@ -206,9 +217,18 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
 }
 
 // D head: logits[r] = sum_k x[r][k] * w[k] + b ; one wave per row, x elem_t [R][K], K % 512 == 0
+struct HeadLossArgs {  // fused gan loss (counter == nullptr: plain GEMV)
+  unsigned* counter;
+  float* out;
+  float* dl_d;
+  float* dl_g;
+  float* prob;
+  const float* ls;
+};
+
 __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ b, float* __restrict__ out, int R,
-                                                        int K) {
+                                                        int K, HeadLossArgs L) {
   // one workgroup per row, each of the 4 waves a quarter of K with all its loads issued up
   // front (one wave per row walked K serially: latency-bound, 9 us for 256 x 8192)
   __shared__ float part[4];
@@ -238,7 +258,28 @@ __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict
   s = wave_sum(s);
   if (lane == 0) part[wave] = s;
   __syncthreads();
-  if (threadIdx.x == 0) out[row] = ((part[0] + part[1]) + (part[2] + part[3])) + b[0];
+  const float logit = ((part[0] + part[1]) + (part[2] + part[3])) + b[0];
+  if (!L.counter) {
+    if (threadIdx.x == 0) out[row] = logit;
+    return;
+  }
+  // fused 3-loss BCE: the logit is written through (sc1), the last row's block computes the
+  // losses and seeds from `sc1` loads of all 2B logits (one launch less per step)
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(out, (uint32_t)(R * 4));
+  if (threadIdx.x == 0)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, logit), rl, (uint32_t)row * 4u, 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(L.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+    if (last) __hip_atomic_store(L.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  gan_loss_block([&](int i) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, (uint32_t)i * 4u, 0, 16)); },
+                 R / 2, L.out, L.dl_d, L.dl_g, L.prob, L.ls);
 }
 
 // dx[r][k] = dl[r] * w[k] (elem_t), 8 per thread
@@ -455,6 +496,72 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, elem_t
   }
 }
 
+// Both TF-Adams (G then D, each with its own lr_t from its own device beta powers) + the
+// step-end update in ONE launch (single-process bf16 path): the blocks walk the two flat
+// buffers' float4s as one index space; the last block to finish (agent counter) advances both
+// beta-power pairs and the global step -- after every block has read the powers (at its start).
+struct Adam2Set {
+  float* w;
+  elem_t* wbf;
+  const float* g;
+  float* m;
+  float* v;
+  float* powers;
+  size_t n;  // % 4 == 0 (64-aligned ParamSet padding)
+  float lr, b1, b2, eps;
+};
+
+__global__ __launch_bounds__(256) void adam2_kernel(Adam2Set A, Adam2Set D, float gscale,
+                                                    unsigned long long* __restrict__ step,
+                                                    unsigned* __restrict__ counter, unsigned blocksA) {
+  __shared__ int flag;
+  // block-uniform split of the grid between the two sets (per-lane selection of the kernarg
+  // structs made the compiler spill them to scratch: 116 us instead of ~52)
+  const unsigned gA = blocksA;
+  const bool inA = blockIdx.x < gA;
+  f32x4* __restrict__ w = reinterpret_cast<f32x4*>(inA ? A.w : D.w);
+  elem4* __restrict__ wbf = reinterpret_cast<elem4*>(inA ? A.wbf : D.wbf);
+  const f32x4* __restrict__ g = reinterpret_cast<const f32x4*>(inA ? A.g : D.g);
+  f32x4* __restrict__ m = reinterpret_cast<f32x4*>(inA ? A.m : D.m);
+  f32x4* __restrict__ v = reinterpret_cast<f32x4*>(inA ? A.v : D.v);
+  const float* pw = inA ? A.powers : D.powers;
+  const float b1 = inA ? A.b1 : D.b1, b2 = inA ? A.b2 : D.b2, eps = inA ? A.eps : D.eps;
+  const float lr_t = (inA ? A.lr : D.lr) * sqrtf(1.f - pw[1]) / (1.f - pw[0]);
+  const size_t n4 = (inA ? A.n : D.n) / 4;
+  const unsigned b0 = inA ? blockIdx.x : blockIdx.x - gA, nb = inA ? gA : gridDim.x - gA;
+  for (size_t i = (size_t)b0 * 256 + threadIdx.x; i < n4; i += (size_t)nb * 256) {
+    const f32x4 gv = g[i] * gscale;
+    f32x4 mv = m[i];
+    f32x4 vv = v[i];
+    f32x4 wv = w[i];
+    mv = b1 * mv + (1.f - b1) * gv;
+    vv = b2 * vv + (1.f - b2) * gv * gv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wv[k] -= lr_t * mv[k] / (sqrtf(vv[k]) + eps);
+    m[i] = mv;
+    v[i] = vv;
+    w[i] = wv;
+    const elem4 o = {(elem_t)wv[0], (elem_t)wv[1], (elem_t)wv[2], (elem_t)wv[3]};
+    wbf[i] = o;
+  }
+  // last arrival: every block has read the powers above before it increments the counter
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = old == gridDim.x - 1;
+    if (flag) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (flag && threadIdx.x == 0) {
+    A.powers[0] *= A.b1;
+    A.powers[1] *= A.b2;
+    D.powers[0] *= D.b1;
+    D.powers[1] *= D.b2;
+    if (step) step[0] += 1ull;
+  }
+}
+
 // after both Adams: beta powers *= beta (TF variable update) and the global step counter
 __global__ void step_end_kernel(float* __restrict__ pd, float* __restrict__ pg, float b1d, float b2d, float b1g,
                                 float b2g, unsigned long long* __restrict__ step, float* __restrict__ ls,
@@ -639,9 +746,12 @@ extern "C" int DCG_API(dcg_linear_wgrad)(const float* z, const elem_t* dh, float
   return (int)hipGetLastError();
 }
 
-extern "C" int DCG_API(dcg_gemv_head)(const elem_t* x, const float* w, const float* b, float* out, int R, int K, hipStream_t s) {
-  if (K % 32) return -2;
-  hipLaunchKernelGGL(gemv_head_kernel, dim3(R), dim3(256), 0, s, x, w, b, out, R, K);
+extern "C" int DCG_API(dcg_gemv_head)(const elem_t* x, const float* w, const float* b, float* out, int R, int K,
+                                      unsigned* counter, float* loss_out, float* dl_d, float* dl_g, float* prob,
+                                      const float* ls, hipStream_t s) {
+  if (K % 32 || (counter && (R % 2 || !loss_out || !dl_d || !dl_g))) return -2;
+  const dcg::HeadLossArgs L{counter, loss_out, dl_d, dl_g, prob, ls};
+  hipLaunchKernelGGL(gemv_head_kernel, dim3(R), dim3(256), 0, s, x, w, b, out, R, K, L);
   return (int)hipGetLastError();
 }
 
@@ -749,5 +859,23 @@ extern "C" int DCG_API(dcg_head_bwd)(const elem_t* x, const float* dl, const flo
     return -2;
   hipLaunchKernelGGL(head_bwd_kernel, dim3((K + 63) / 64), dim3(256), 0, s, x, dl, w, dx, dW, db, R, K, bx, by, mean,
                      rstd, C, rpg > 0 ? rpg : R, act, leak, part);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_adam2)(float* wA, elem_t* wbfA, const float* gA, float* mA, float* vA, float* pA, size_t nA,
+                                  float lrA, float b1A, float b2A, float epsA, float* wD, elem_t* wbfD, const float* gD,
+                                  float* mD, float* vD, float* pD, size_t nD, float lrD, float b1D, float b2D,
+                                  float epsD, float gscale, unsigned long long* step, unsigned* counter,
+                                  hipStream_t s) {
+  if (nA % 4 || nD % 4 || !wbfA || !wbfD) return -2;
+  const dcg::Adam2Set A{wA, wbfA, gA, mA, vA, pA, nA, lrA, b1A, b2A, epsA};
+  const dcg::Adam2Set D{wD, wbfD, gD, mD, vD, pD, nD, lrD, b1D, b2D, epsD};
+  // ~512 blocks in total (grid-stride loops): every block bumps ONE arrival counter, and a
+  // same-address atomic per block serialises (9k blocks: +60 us)
+  const size_t q = (nA + nD) / 4;
+  unsigned blocksA = (unsigned)std::max<size_t>(1, (512 * (nA / 4) + q - 1) / q);
+  unsigned blocksD = (unsigned)std::max<size_t>(1, 512 - std::min<size_t>(511, blocksA));
+  hipLaunchKernelGGL(dcg::adam2_kernel, dim3(blocksA + blocksD), dim3(256), 0, s, A, D, gscale, step, counter,
+                     blocksA);
   return (int)hipGetLastError();
 }

@@ -95,17 +95,17 @@ def test_engine_stagewise(size, c_dim, B, dtype, monkeypatch):
     for i in range(len(dl) - 1, -1, -1):
         L = dl[i]
         if L.bn:
-            gx, _, _ = bn_act_bwd64(eng.d_x[L.name][B:], eng.d_da[L.name][B:], Pd[L.bn + "/gamma"],
+            gx, _, _ = bn_act_bwd64(eng.d_x[L.name][B:], eng.gc_da[L.name], Pd[L.bn + "/gamma"],
                                     Pd[L.bn + "/beta"], "lrelu")
-            rep["g %s bn dx" % L.name] = rel(eng.d_dx[L.name][B:], gx)
+            rep["g %s bn dx" % L.name] = rel(eng.gc_dx[L.name], gx)
         src = eng.d_in[B:] if i == 0 else eng.d_a[dl[i - 1].name][B:]
-        gx, _ = conv_grads64(src, Pd[L.name + "/w"], eng.d_dx[L.name][B:], "conv", edt=edt)
+        gx, _ = conv_grads64(src, Pd[L.name + "/w"], eng.gc_dx[L.name], "conv", edt=edt)
         if i == 0:
             rep["g %s dgrad" % L.name] = rel(eng.img_grad, gx)
         elif dl[i - 1].bn:
-            rep["g %s dgrad" % L.name] = rel(eng.d_da[dl[i - 1].name][B:], gx)
+            rep["g %s dgrad" % L.name] = rel(eng.gc_da[dl[i - 1].name], gx)
         else:  # the act backward of a BN-less layer is fused into this GEMM: it stores dx
-            rep["g %s dgrad+act" % L.name] = rel(eng.d_dx[dl[i - 1].name][B:], gx * _lrelu_d(eng.d_a[dl[i - 1].name][B:]))
+            rep["g %s dgrad+act" % L.name] = rel(eng.gc_dx[dl[i - 1].name], gx * _lrelu_d(eng.d_a[dl[i - 1].name][B:]))
     fake = d64(eng.fake)
     img_g = d64(eng.img_grad) * (1 - fake * fake)
     rep["G tanh bwd"] = rel(eng.img_g, img_g)
@@ -131,7 +131,7 @@ def test_engine_stagewise(size, c_dim, B, dtype, monkeypatch):
     rep["G bn0 dx"] = rel(eng.g_dx0.reshape(gx.shape), gx)
     rep["G lin dW"] = rel(gG["g_h0_lin/Matrix"], d64(eng.z).t() @ d64(eng.g_dx0))
     rep["G lin db"] = rel(gG["g_h0_lin/bias"], d64(eng.g_dx0).sum(0))
-    H.run(eng.progB, st)          # D backward of d_loss (overwrites the fake halves of d_da / d_dx)
+    H.run(eng.progB, st)          # D backward of d_loss
     torch.cuda.synchronize()
     # head
     a_last = d64(eng.d_a[dl[-1].name]).reshape(B2, -1)

@@ -585,3 +585,25 @@ def test_head_bwd_bn_stats(R, groups):
         xh = (bx.float()[gi * rpg:(gi + 1) * rpg].reshape(rpg, S, C) - mean[gi]) * rstd[gi]
         close(part[gi * S:(gi + 1) * S, 0], gg.sum(0), 1e-4, "sum g")
         close(part[gi * S:(gi + 1) * S, 1], (gg * xh).sum(0), 1e-4, "sum g xhat")
+
+
+def test_head_gemv_fused_loss_matches_separate():
+    """gemv_head with the 3-loss BCE in its last-arriving block == gemv_head + gan_loss (bitwise),
+    and replays re-arm the arrival counter."""
+    h = H()
+    B, K = 64, 8192
+    x = bf(rnd(2 * B, K, seed=110))
+    w = rnd(K, scale=0.02, seed=111)
+    hb = rnd(1, seed=112)
+    bufs = [[torch.full((n,), float("nan"), device=dev) for n in (2 * B, 4, 2 * B, B, 2 * B)] for _ in range(2)]
+    pr = _prog()
+    lg, lo, dd, dg, pb = bufs[0]
+    pr.gemv_head("h", _p(x), _p(w), _p(hb), _p(lg), 2 * B, K, 0)
+    pr.gan_loss("l", _p(lg), B, _p(lo), _p(dd), _p(dg), _p(pb), 0)
+    lg2, lo2, dd2, dg2, pb2 = bufs[1]
+    pr.gemv_head("hl", _p(x), _p(w), _p(hb), _p(lg2), 2 * B, K, 0, _p(lo2), _p(dd2), _p(dg2), _p(pb2), 0)
+    for _ in range(2):
+        h.run(pr)
+        torch.cuda.synchronize()
+        for a, b in zip(bufs[0], bufs[1]):
+            assert torch.equal(a, b)
