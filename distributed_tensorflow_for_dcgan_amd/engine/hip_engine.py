@@ -757,26 +757,57 @@ class HipEngine:
             self._side_stream = torch.cuda.Stream(device=self.device)
         return [torch.cuda.current_stream(self.device), self._side_stream]
 
-    def _segments(self):
-        """The step as (program, begin, end) segments. Single process: one segment. DDP: the
-        collectives sit between segments -- G-grad all-reduce overlaps D's backward (B1, B2),
-        the all-reduce of D's top layer + head overlaps the rest of D's backward (B2), Adam(G)
-        overlaps the last (small) D all-reduce."""
-        if self.world == 1 and not self._timing:
-            return [[(self.progA, 0, -1), (self.progB, 0, -1), (self.progC, 0, -1)]]
-        return [[(self.progA, 0, -1)], [(self.progB, 0, self._b_split)], [(self.progB, self._b_split, -1)],
-                [(self.progC, 0, self._c_split)], [(self.progC, self._c_split, -1)]]
+    # Schedules:
+    #   "fused"       single process: ONE graph; D's d_loss backward (progB) on its own streams
+    #                 concurrently with the g_loss chain + G's backward (progA tail)
+    #   "concurrent"  DDP (and the timed single-process step): the same two concurrent chains,
+    #                 cut into 6 graphs so the collectives can be issued between them from the
+    #                 host: D's top layer + head (76 % of D's bytes) is all-reduced as soon as the
+    #                 D chain has produced it, G's gradients as soon as G's backward ends, the
+    #                 rest of D's when the D chain ends; Adam(G) / Adam(D) wait for their own
+    #                 collectives only
+    #   "serial"      DCGAN_SERIAL_DBWD=1: fwd + G backward, then D's backward, as 5 segments
+    #                 (G all-reduce overlaps D's backward)
+    MAIN, ALT = 0, 1
 
-    PHASES = ("fwd+G_bwd", "D_bwd_top", "D_bwd_rest", "wait_allreduce_G", "adam_G", "wait_allreduce_D",
-              "adam_D")
+    def _schedule(self) -> str:
+        if self.world == 1 and not self._timing:
+            return "fused"
+        if os.environ.get("DCGAN_SERIAL_DBWD") == "1" or self._adam_g_side:
+            return "serial"
+        return "concurrent"
+
+    @property
+    def _hybrid(self) -> bool:
+        """Concurrent schedule variant (DCGAN_DDP_SCHEDULE=hybrid): only D's top layer + head
+        run beside the G chain; the rest of D's backward starts when the G chain ends, so it
+        overlaps G's all-reduce (the largest one, 20.5 MB fp32) instead of delaying it."""
+        return os.environ.get("DCGAN_DDP_SCHEDULE", "concurrent") == "hybrid"
+
+    def _segments(self):
+        """The step as a list of (name, [(program, begin, end)], stream) segments."""
+        sch = self._schedule()
+        A, B, C = self.progA, self.progB, self.progC
+        M = self.MAIN
+        if sch == "fused":
+            return [("step", [(A, 0, -1), (B, 0, -1), (C, 0, -1)], M)]
+        if sch == "serial":
+            return [("fwd+G_bwd", [(A, 0, -1)], M), ("D_bwd_top", [(B, 0, self._b_split)], M),
+                    ("D_bwd_rest", [(B, self._b_split, -1)], M), ("adam_G", [(C, 0, self._c_split)], M),
+                    ("adam_D", [(C, self._c_split, -1)], M)]
+        return [("fwd", [(A, 0, self._a_fwd)], M), ("D_bwd_top", [(B, 0, self._b_split)], self.ALT),
+                ("G_chain", [(A, self._a_fwd, -1)], M), ("D_bwd_rest", [(B, self._b_split, -1)], self.ALT),
+                ("adam_G", [(C, 0, self._c_split)], M), ("adam_D", [(C, self._c_split, -1)], M)]
 
     def enable_timing(self) -> None:
-        """Per-phase GPU timers: the step runs as 5 segments with events
-        between them. Call before the first train_step (graphs are captured per segment)."""
+        """Per-phase GPU timers: the step runs as segments with events between
+        them. Call before the first train_step (graphs are captured per segment). Concurrent
+        schedule: each phase is reported as ms from the step start to the END of that phase
+        (the D and G chains overlap); serial schedule: phase durations."""
         if self._graphs:
             raise RuntimeError("enable_timing() must precede the first train_step")
         self._timing = True
-        self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self.PHASES) + 1)]
+        self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self._segments()) + 1)]
 
     def phase_times(self) -> Dict[str, float]:
         """Milliseconds of the last step's phases (synchronises on its last event)."""
@@ -784,20 +815,27 @@ class HipEngine:
             return {}
         ev = self._ev
         ev[-1].synchronize()
-        return {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(self.PHASES)}
+        segs = self._segments()
+        if self._schedule() == "concurrent":
+            return {n + "@end": ev[0].elapsed_time(ev[i + 1]) for i, (n, _, _) in enumerate(segs)}
+        return {n: ev[i].elapsed_time(ev[i + 1]) for i, (n, _, _) in enumerate(segs)}
 
     def _concurrent_dbwd(self) -> bool:
-        """Single process: D's d_loss backward runs on its own stream concurrently with the
-        g_loss chain + G's backward (independent buffers; two chains of GEMMs and small
-        latency-bound BN kernels fill each other's gaps). Measured on MI355X at 64x64, B=128:
-        1.39 vs 1.58 ms/step. DCGAN_SERIAL_DBWD=1 serialises (DDP keeps its segment order)."""
-        return self.world == 1 and not self._timing and os.environ.get("DCGAN_SERIAL_DBWD") != "1"
+        """D's d_loss backward runs on its own streams concurrently with the g_loss chain + G's
+        backward (independent buffers; two chains of GEMMs and small latency-bound BN kernels
+        fill each other's gaps). Measured on MI355X at 64x64, B=128, single process: 1.32 vs
+        1.50 ms/step. DCGAN_SERIAL_DBWD=1 serialises."""
+        return self._schedule() != "serial"
 
-    def _run_concurrent(self, cs):
+    def _alt(self):
         if not hasattr(self, "_alt_streams"):
             self._alt_streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
+        return self._alt_streams
+
+    def _run_fused(self, cs):
+        """The "fused" schedule issued onto cs (+ forked alt streams); also what gets captured."""
         side = self._streams()[1]
-        alt = self._alt_streams
+        alt = self._alt()
         H.run(self.progA, [cs, side], 0, self._a_fwd)
         fork = torch.cuda.Event()
         fork.record(cs)
@@ -809,47 +847,86 @@ class HipEngine:
         cs.wait_event(join)
         H.run(self.progC, [cs, side])
 
-    def _run_segment(self, i, st):
+    def _seg(self, i, stream):
+        """Run segment i on `stream` (graph replay, or eager replay of its program ranges)."""
         if self.graph_enabled:
-            if self._graphs[i] is not None:
-                self._graphs[i].replay()
-        elif self._concurrent_dbwd():
-            self._run_concurrent(st[0])
-        else:
-            for prog, b, e in self._segments()[i]:
-                H.run(prog, st, b, e)
+            g = self._graphs[i]
+            if g is not None:
+                with torch.cuda.stream(stream):
+                    g.replay()
+            return
+        _, parts, which = self._segments()[i]
+        sec = self._streams()[1] if which == self.MAIN else self._alt()[1]
+        for prog, b, e in parts:
+            H.run(prog, [stream, sec], b, e)
 
     def _run_step(self):
         st = self._streams()
-        if self.world == 1 and not self._timing:
-            self._run_segment(0, st)
-            return
         cs = st[0]
-        tick = (lambda i: self._ev[i].record(cs)) if self._timing else (lambda i: None)
+        sch = self._schedule()
+        if sch == "fused":
+            if self.graph_enabled:
+                self._seg(0, cs)
+            else:
+                self._run_fused(cs)
+            return
+        tick = (lambda i, s: self._ev[i].record(s)) if self._timing else (lambda i, s: None)
         ddp = self.world > 1
-        tick(0)
-        self._run_segment(0, st)          # fwd, g_loss chain through D(fake), G backward -> grad_g final
-        tick(1)
+        if sch == "concurrent":
+            alt = self._alt()[0]
+            tick(0, cs)
+            self._seg(0, cs)              # z, G fwd, D fwd (real | fake), losses
+            tick(1, cs)
+            alt.wait_stream(cs)
+            self._seg(1, alt)             # D chain: head + top layer gradients
+            tick(2, alt)
+            if ddp:
+                with torch.cuda.stream(alt):
+                    self._ar_dtop.launch()
+            self._seg(2, cs)              # G chain: g_loss through D(fake), G backward -> grad_g final
+            tick(3, cs)
+            if ddp:
+                with torch.cuda.stream(cs):
+                    self._ar_g.launch()
+            if self._hybrid:              # the rest of D's backward overlaps G's all-reduce instead
+                alt.wait_stream(cs)
+            self._seg(3, alt)             # D chain: rest of D's backward -> grad_d final
+            tick(4, alt)
+            if ddp:
+                with torch.cuda.stream(cs):
+                    self._ar_g.wait(scale_in_place=False)   # cs waits for dtop + G on the comm stream
+            self._seg(4, cs)              # Adam G -> G mirror (overlaps the last D all-reduce)
+            tick(5, cs)
+            if ddp:
+                with torch.cuda.stream(alt):
+                    self._ar_drest.launch()
+                with torch.cuda.stream(cs):
+                    self._ar_drest.wait(scale_in_place=False)
+            cs.wait_stream(alt)
+            self._seg(5, cs)              # Adam D, step counter, D mirror
+            tick(6, cs)
+            return
+        tick(0, cs)
+        self._seg(0, cs)                  # fwd, g_loss chain through D(fake), G backward -> grad_g final
+        tick(1, cs)
         if ddp:
             self._ar_g.launch()
-        self._run_segment(1, st)          # D backward: head + top layer (overlaps the G all-reduce)
-        tick(2)
+        self._seg(1, cs)                  # D backward: head + top layer (overlaps the G all-reduce)
+        tick(2, cs)
         if ddp:
             self._ar_dtop.launch()
-        self._run_segment(2, st)          # rest of D's backward -> grad_d final
-        tick(3)
+        self._seg(2, cs)                  # rest of D's backward -> grad_d final
+        tick(3, cs)
         if ddp:
             self._ar_drest.launch()
             self._ar_g.wait(scale_in_place=False)
-        tick(4)
-        self._run_segment(3, st)          # Adam G -> G mirror (overlaps the last D all-reduce)
-        tick(5)
+        self._seg(3, cs)                  # Adam G -> G mirror (overlaps the last D all-reduce)
+        tick(4, cs)
         if ddp:
             self._ar_dtop.wait(scale_in_place=False)
             self._ar_drest.wait(scale_in_place=False)
-        tick(6)
-        self._run_segment(4, st)          # Adam D, step counter, D mirror
-        tick(7)
+        self._seg(4, cs)                  # Adam D, step counter, D mirror
+        tick(5, cs)
 
     def _ensure_comm(self):
         if self.world > 1 and not hasattr(self, "_ar_g"):
@@ -867,18 +944,20 @@ class HipEngine:
         try:
             torch.cuda.synchronize(self.device)
             graphs = []
-            for seg in self._segments():
-                if all((p.size() if e < 0 else e) <= b for p, b, e in seg):
+            fused = self._schedule() == "fused"
+            for name, parts, which in self._segments():
+                if all((p.size() if e < 0 else e) <= b for p, b, e in parts):
                     graphs.append(None)  # empty segment (fp16: no separate D update)
                     continue
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     cs = torch.cuda.current_stream(self.device)
-                    if self._concurrent_dbwd():
-                        self._run_concurrent(cs)
+                    if fused:
+                        self._run_fused(cs)
                     else:
-                        for prog, b, e in seg:
-                            H.run(prog, [cs, self._streams()[1]], b, e)
+                        sec = self._streams()[1] if which == self.MAIN else self._alt()[1]
+                        for prog, b, e in parts:
+                            H.run(prog, [cs, sec], b, e)
                 graphs.append(g)
             self._graphs = graphs
             return True

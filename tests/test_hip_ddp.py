@@ -44,7 +44,9 @@ def _run(eng):
     return eng.model.d.flat.cpu(), eng.model.g.flat.cpu(), eng.global_step
 
 
-def _worker(rank, world, port, graph, out_dir):
+def _worker(rank, world, port, graph, out_dir, schedule="concurrent"):
+    if schedule == "serial":
+        os.environ["DCGAN_SERIAL_DBWD"] = "1"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["DCGAN_DIST_BACKEND"] = "gloo"
@@ -53,16 +55,19 @@ def _worker(rank, world, port, graph, out_dir):
     D.init_distributed(world, rank, torch.device("cuda", 0))
     eng = _make(world, rank, graph)
     d, g, step = _run(eng)
+    assert eng._schedule() == schedule
     torch.save({"d": d, "g": g, "step": step, "graph": eng.graph_enabled}, os.path.join(out_dir, "r%d.pt" % rank))
     D.barrier()
     D.shutdown()
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph):
+@pytest.mark.parametrize("graph,schedule", [(False, "concurrent"), (True, "concurrent"), (True, "serial")])
+def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
+    """Both DDP schedules: "concurrent" (D chain and G chain on separate streams, 6 graph
+    segments, collectives issued from both chains) and "serial" (DCGAN_SERIAL_DBWD=1)."""
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, str(tmp_path), schedule)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -77,3 +82,18 @@ def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph):
     d, g, _ = _run(eng)
     assert torch.equal(r0["d"], d), (r0["d"] - d).abs().max()
     assert torch.equal(r0["g"], g), (r0["g"] - g).abs().max()
+
+
+def test_timed_concurrent_schedule_matches_fused():
+    """The per-phase timed step (6 concurrent graph segments, the DDP schedule at W=1) is the
+    same computation as the single fused graph, bit for bit; phase ends are reported."""
+    a = _make(1, 0, True)
+    b = _make(1, 0, True)
+    b.enable_timing()
+    assert a._schedule() == "fused" and b._schedule() == "concurrent"
+    d0, g0, _ = _run(a)
+    d1, g1, _ = _run(b)
+    assert torch.equal(d0, d1) and torch.equal(g0, g1)
+    pt = b.phase_times()
+    assert set(pt) == {"fwd@end", "D_bwd_top@end", "G_chain@end", "D_bwd_rest@end", "adam_G@end", "adam_D@end"}
+    assert all(v > 0 for v in pt.values())
