@@ -110,6 +110,94 @@ __global__ __launch_bounds__(256) void narrow_deconv_kernel(const elem_t* __rest
   }
 }
 
+// MFMA form of the same operation (C a multiple of 32): identical tile, halo and weight
+// staging, but each wave computes its phase's 8x8 = 64 output pixels as 4 M-blocks of a
+// v_mfma_f32_16x16x32 GEMM: A = 16 pixels x 32 channels read straight from the staged halo at
+// the tap's shift (lane l: pixel l&15, 8-channel chunk l>>4 -- one ds_read_b128), B = 32
+// channels x 16 outputs of the tap's weights (outputs >= N are zero lanes). N=3 pads to 16
+// (5.3x the useful MACs), but one MFMA replaces 64 lanes x 32 MACs of v_dot2 work at 4x the
+// per-SIMD rate of the VALU kernel above (measured: see BASELINE.md / profiles).
+template <int N, int C8>
+__global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* __restrict__ x,
+                                                                 const elem_t* __restrict__ w,
+                                                                 const float* __restrict__ bias,
+                                                                 elem_t* __restrict__ y, int Hi, int Wi, int Ho,
+                                                                 int Wo, int pad, int act, float leak, int tiles_x,
+                                                                 int tiles_per_img) {
+  static_assert(C8 == 8, "the bank swizzle below assumes 8 chunks (64 channels) per pixel");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  elem8* xs = reinterpret_cast<elem8*>(smem);  // [HALO*HALO][C8], chunk c of pixel (row, col) at c ^ sw(col)
+  elem8* ws = xs + NW_HALO * NW_HALO * C8;     // [25][N][C8]
+  // sw(col) = 2 * ((col >> 1) & 3): an A-fragment read (ds_read_b128, 4 lane groups of 16) takes 8
+  // consecutive halo columns (any shift) for each of two chunk quarters qq, qq+1 of one k-block;
+  // bank slot = (col & 1) * 8 + (chunk ^ sw): the 8 columns fill 8 distinct slots and the two
+  // chunks land on opposite chunk parities -> conflict-free for every tap.
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / tiles_per_img;
+  const int trem = blockIdx.x - b * tiles_per_img;
+  const int ty0 = (trem / tiles_x) * NW_TILE, tx0 = (trem % tiles_x) * NW_TILE;
+  const int iy_lo = (ty0 + pad - 4) >> 1, ix_lo = (tx0 + pad - 4) >> 1;
+  const elem8 zero8 = {};
+  for (int q = tid; q < NW_HALO * NW_HALO * C8; q += 256) {
+    const int pix = q >> 3, c = q & 7;
+    const int row = pix / NW_HALO, col = pix - row * NW_HALO;
+    const int iy = iy_lo + row, ix = ix_lo + col;
+    elem8 v = zero8;
+    if ((unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
+      v = *reinterpret_cast<const elem8*>(x + (((size_t)b * Hi + iy) * Wi + ix) * (C8 * 8) + c * 8);
+    xs[pix * C8 + (c ^ (((col >> 1) & 3) << 1))] = v;
+  }
+  for (int q = tid; q < 25 * N * C8; q += 256) ws[q] = reinterpret_cast<const elem8*>(w)[q];
+  __syncthreads();
+
+  const int py = wave >> 1, px = wave & 1;  // this wave's sub-pixel phase
+  const int r = lane & 15, qq = lane >> 4;
+  // A rows of M-block m: phase pixel p = 16 m + r of the 8x8 grid -> (gy, gx) = (2 m + (r >> 3), r & 7);
+  // its input pixel for tap (ky, kx) is (gy + oyk, gx + oxk), oyk = ((ty0 + py + pad - ky) >> 1) - iy_lo
+  // (ty0 even: the shift is exact per tap)
+  const int gy0 = r >> 3, gx = r & 7;
+  const int kys = (ty0 + py + pad) & 1, kxs = (tx0 + px + pad) & 1;
+  f32x4 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ky = kys; ky < 5; ky += 2) {
+    const int oyk = ((ty0 + py + pad - ky) >> 1) - iy_lo;
+    for (int kx = kxs; kx < 5; kx += 2) {
+      const int col = gx + (((tx0 + px + pad - kx) >> 1) - ix_lo);
+      const int sw = ((col >> 1) & 3) << 1;
+      const elem8* wr = ws + (ky * 5 + kx) * N * C8;
+      const elem8* xr = xs + ((gy0 + oyk) * NW_HALO + col) * C8;  // M-block m adds 2 m halo rows
+#pragma unroll
+      for (int kb = 0; kb < C8 / 4; ++kb) {
+        const int ch = 4 * kb + qq;
+        const elem8 bf = r < N ? wr[r * C8 + ch] : zero8;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const elem8 af = xr[2 * m * NW_HALO * C8 + (ch ^ sw)];
+          acc[m] = DCG_MFMA_16x16x32(af, bf, acc[m], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue through LDS: the N useful accumulator columns (lanes r < N) -> [64 pixels][N] fp32 per
+  // wave, then one lane per pixel applies bias + activation and stores its N outputs
+  __syncthreads();  // every wave is done reading the halo
+  float* ob = reinterpret_cast<float*>(smem) + wave * 64 * N;
+  if (r < N) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ob[(16 * m + 4 * qq + i) * N + r] = acc[m][i];
+  }
+  __syncthreads();
+  const int oy = ty0 + 2 * (lane >> 3) + py, ox = tx0 + 2 * (lane & 7) + px;
+  if (oy < Ho && ox < Wo) {
+    elem_t* dst = y + (((size_t)b * Ho + oy) * Wo + ox) * N;
+#pragma unroll
+    for (int n = 0; n < N; ++n) dst[n] = f2bf(apply_act(ob[lane * N + n] + (bias ? bias[n] : 0.f), act, leak));
+  }
+}
+
 }  // namespace dcg
 
 extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, const float* bias, elem_t* y, int B,
@@ -121,6 +209,29 @@ extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, cons
   const size_t shm = (size_t)(dcg::NW_HALO * dcg::NW_HALO + 25 * N) * C * sizeof(elem_t);
   if (shm > 160 * 1024) return -2;
   dim3 grid(B * tiles_x * tiles_y);
+  static const bool valu_only = getenv("DCGAN_NARROW_VALU") != nullptr;  // A/B: the v_dot2 kernel
+  if (C == 64 && !valu_only) {
+#define NW_MFMA(NN)                                                                                            \
+  {                                                                                                            \
+    auto k = dcg::narrow_deconv_mfma_kernel<NN, 8>;                                                            \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return (int)e;                                                                      \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm, s, x, w, bias, y, Hi, Wi, Ho, Wo, pad, act, leak, tiles_x,     \
+                       tiles_x * tiles_y);                                                                     \
+  }
+    switch (N) {
+      case 1: NW_MFMA(1) break;
+      case 2: NW_MFMA(2) break;
+      case 3: NW_MFMA(3) break;
+      default: NW_MFMA(4) break;
+    }
+#undef NW_MFMA
+    return (int)hipGetLastError();
+  }
 #define NW_LAUNCH(NN)                                                                                          \
   {                                                                                                            \
     auto k = C == 64 ? dcg::narrow_deconv_kernel<NN, 8> : dcg::narrow_deconv_kernel<NN, 0>;                    \

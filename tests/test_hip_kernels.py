@@ -447,10 +447,12 @@ def test_philox_uniform_range_and_determinism():
 
 
 @pytest.mark.parametrize("B,Hi,Ho,C,N,dtype", [(4, 32, 64, 64, 3, "bf16"), (2, 4, 7, 64, 3, "bf16"),
-                                                (3, 14, 28, 64, 1, "bf16"), (2, 16, 32, 128, 3, "fp16")])
+                                                (3, 14, 28, 64, 1, "bf16"), (2, 16, 32, 128, 3, "fp16"),
+                                                (2, 16, 32, 64, 3, "fp16"), (2, 9, 17, 64, 4, "bf16")])
 def test_narrow_deconv(B, Hi, Ho, C, N, dtype):
-    """Direct VALU conv_transpose for N <= 4 outputs (G's RGB layer, D layer-0 data gradient):
-    bias + tanh, odd sizes (pad 2), 1 channel, fp16 build."""
+    """Direct conv_transpose for N <= 4 outputs (G's RGB layer, D layer-0 data gradient): the
+    MFMA kernel (C = 64) and the v_dot2 VALU kernel (other C): bias + tanh, odd sizes (pad 2),
+    1 and 4 channels, fp16 build."""
     h = H()
     edt = torch.float16 if dtype == "fp16" else torch.bfloat16
     x = rnd(B, Hi, Hi, C, seed=60).to(edt)
