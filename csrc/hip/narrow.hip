@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void narrow_deconv_kernel(const elem_t* __rest
 // channels x 16 outputs of the tap's weights (outputs >= N are zero lanes). N=3 pads to 16
 // (5.3x the useful MACs), but one MFMA replaces 64 lanes x 32 MACs of v_dot2 work at 4x the
 // per-SIMD rate of the VALU kernel above (measured: see BASELINE.md / profiles).
-template <int N, int C8>
+template <int N, int C8, bool WG>  // WG: B fragments straight from global/L1 (no LDS weight copy)
 __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* __restrict__ x,
                                                                  const elem_t* __restrict__ w,
                                                                  const float* __restrict__ bias,
@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* _
       v = *reinterpret_cast<const elem8*>(x + (((size_t)b * Hi + iy) * Wi + ix) * (C8 * 8) + c * 8);
     xs[pix * C8 + (c ^ (((col >> 1) & 3) << 1))] = v;
   }
-  for (int q = tid; q < 25 * N * C8; q += 256) ws[q] = reinterpret_cast<const elem8*>(w)[q];
+  if (!WG)
+    for (int q = tid; q < 25 * N * C8; q += 256) ws[q] = reinterpret_cast<const elem8*>(w)[q];
   __syncthreads();
 
   const int py = wave >> 1, px = wave & 1;  // this wave's sub-pixel phase
@@ -165,12 +166,15 @@ __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* _
     for (int kx = kxs; kx < 5; kx += 2) {
       const int col = gx + (((tx0 + px + pad - kx) >> 1) - ix_lo);
       const int sw = ((col >> 1) & 3) << 1;
-      const elem8* wr = ws + (ky * 5 + kx) * N * C8;
+      const elem8* wr = (WG ? reinterpret_cast<const elem8*>(w) : ws) + (ky * 5 + kx) * N * C8;
       const elem8* xr = xs + ((gy0 + oyk) * NW_HALO + col) * C8;  // M-block m adds 2 m halo rows
+      elem8 bfs[C8 / 4];
+#pragma unroll
+      for (int kb = 0; kb < C8 / 4; ++kb) bfs[kb] = r < N ? wr[r * C8 + 4 * kb + qq] : zero8;
 #pragma unroll
       for (int kb = 0; kb < C8 / 4; ++kb) {
         const int ch = 4 * kb + qq;
-        const elem8 bf = r < N ? wr[r * C8 + ch] : zero8;
+        const elem8 bf = bfs[kb];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const elem8 af = xr[2 * m * NW_HALO * C8 + (ch ^ sw)];
@@ -210,17 +214,19 @@ extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, cons
   if (shm > 160 * 1024) return -2;
   dim3 grid(B * tiles_x * tiles_y);
   static const bool valu_only = getenv("DCGAN_NARROW_VALU") != nullptr;  // A/B: the v_dot2 kernel
+  static const bool w_lds = getenv("DCGAN_NARROW_WLDS") != nullptr;       // A/B: weights staged in LDS
   if (C == 64 && !valu_only) {
+    const size_t shm_m = w_lds ? shm : (size_t)dcg::NW_HALO * dcg::NW_HALO * C * sizeof(elem_t);
 #define NW_MFMA(NN)                                                                                            \
   {                                                                                                            \
-    auto k = dcg::narrow_deconv_mfma_kernel<NN, 8>;                                                            \
+    auto k = w_lds ? dcg::narrow_deconv_mfma_kernel<NN, 8, false> : dcg::narrow_deconv_mfma_kernel<NN, 8, true>; \
     static bool attr = false;                                                                                  \
     if (!attr) {                                                                                               \
       hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
       if (e != hipSuccess) return (int)e;                                                                      \
       attr = true;                                                                                             \
     }                                                                                                          \
-    hipLaunchKernelGGL(k, grid, dim3(256), shm, s, x, w, bias, y, Hi, Wi, Ho, Wo, pad, act, leak, tiles_x,     \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm_m, s, x, w, bias, y, Hi, Wi, Ho, Wo, pad, act, leak, tiles_x,   \
                        tiles_x * tiles_y);                                                                     \
   }
     switch (N) {
