@@ -624,24 +624,20 @@ class HipEngine:
     # ---- two-stream structure inside a segment: fork = side waits for main's progress so far,
     # join = main waits for everything queued on side (every segment ends joined, so a segment
     # captures into one hipGraph with parallel branches)
-    SIDE = 1
+    SIDE = 0
 
     def _fork(self, prog):
-        # Measured on MI355X (64x64, B=128): the conv GEMMs already fill all 256 CUs, so running
-        # the weight gradients concurrently only adds contention (69.4k vs 71.8k img/s serial).
-        # Kept as an opt-in for small-batch configs.
-        if os.environ.get("DCGAN_CONCURRENT_WGRAD") != "1":
-            self.SIDE = 0
-            return
-        ev = prog.new_event()
-        prog.record(ev, 0)
-        prog.wait(ev, self.SIDE)
-        self._side_open = True
+        # Weight gradients stay on the chain's own stream. Running them on a side stream beside
+        # the data-gradient chain was measured slower on MI355X (64x64, B=128): 69.4k vs 71.8k
+        # img/s with the serial step, and 1.332 vs 1.303 ms/step for G's weight gradients beside
+        # the concurrent G chain (profiles/ab_r1_concurrent_wgrad.txt) -- the two backward chains
+        # already fill the CUs. The side stream is used by the opt-in split forward only.
+        self.SIDE = 0
 
     def _join(self, prog):
         if getattr(self, "_side_open", False):
             ev = prog.new_event()
-            prog.record(ev, self.SIDE)
+            prog.record(ev, 1)
             prog.wait(ev, 0)
             self._side_open = False
 

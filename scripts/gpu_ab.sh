@@ -1,12 +1,18 @@
 #!/bin/bash
-# GPU tests, then A/B of engine variants: interleaved bench runs (env var toggles in $AB)
-mkdir -p gpurun_out; : > gpurun_out/ab.log
-timeout -k 10 900 python -m pytest tests -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -1 gpurun_out/gpu_tests.log
+# generic A/B: bash scripts/gpu_ab.sh "ENV1=.." "ENV2=.." ...  (3 rounds of bench.py each)
+set -o pipefail
+mkdir -p gpurun_out
+: > gpurun_out/ab.log
 for i in 1 2 3; do
-  for v in "X=0" "$1"; do
-    env $v timeout -k 10 300 python bench.py --steps 100 --warmup 10 > gpurun_out/ab1.log 2>&1 || { tail gpurun_out/ab1.log; exit 1; }
-    echo "[$v] $(tail -1 gpurun_out/ab1.log | cut -c90-150)" >> gpurun_out/ab.log
-  done
-done
-cat gpurun_out/ab.log
+for env in "$@"; do
+echo "[$env]" >> gpurun_out/ab.log
+env $env timeout -k 10 120 python bench.py --steps 100 --warmup 20 >> gpurun_out/ab.log 2>&1 || exit 1
+done; done
+python - <<'PY' >> gpurun_out/ab.log
+import json, collections
+d = collections.defaultdict(list); cur = None
+for l in open("gpurun_out/ab.log"):
+    if l.startswith("["): cur = l.strip()
+    elif l.startswith("{"): d[cur].append(json.loads(l)["ms_per_step"])
+for k, v in d.items(): print("SUMMARY", k, "min %.4f mean %.4f" % (min(v), sum(v) / len(v)))
+PY
