@@ -221,6 +221,18 @@ class HipEngine:
             self._build_update(self.progC, first=True)
             self._c_split = self.progC.size()
             self._build_update(self.progC, first=False)
+        # opt-in (single process, bf16): Adam(D) on the D chain's stream as soon as D's gradients
+        # are final AND the g_loss chain has left D (it reads the pre-update D weights); Adam(G) +
+        # the beta-power / step update after the join (see _run_fused). Measured on MI355X at
+        # 64x64, B=128: 1.325 vs 1.293 ms/step for the fused two-set Adam after the join -- the
+        # memory-bound Adam slows G's backward GEMMs more than it hides
+        # (profiles/ab_r1_early_adam_d.txt).
+        self._early_adam_d = (self.world == 1 and not self.f16 and not self._adam_g_side
+                              and os.environ.get("DCGAN_EARLY_ADAM_D") == "1")
+        if self._early_adam_d:
+            self.progCd = ext.Program(self.f16)
+            self.progCg = ext.Program(self.f16)
+            self._build_update_split(self.progCd, self.progCg)
         # D-gradient slice final after segment B1: the top conv layer (+ its BN) and the head,
         # which the ParamSet lays out last
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
@@ -711,7 +723,8 @@ class HipEngine:
                 else:
                     self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw,
                                 L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
-        # ---------------- G backward
+        # ---------------- G backward (reads no D state: Adam(D) may run from here on)
+        self._a_gd = prog.size()
         n = len(self.gl)
         Lg = self.gl[-1]
         self._act_bwd_dbias(prog, "g_out.tanh_bwd", self.img_grad, self.fake, self.img_g, B * Lg.out_hw ** 2,
@@ -800,6 +813,21 @@ class HipEngine:
                          gs, 0, ls)
             prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
                           _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
+
+    def _build_update_split(self, prog_d, prog_g):
+        """Single-process bf16: TF-Adam(D) alone (prog_d, run beside G's backward), then
+        TF-Adam(G) + the beta-power / global-step update (prog_g) -- the same kernels and
+        arithmetic as _build_update."""
+        od, og = self.opt_d, self.opt_g
+        ls = _p(self.loss_scale)
+        prog_d.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
+                       _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
+                       1.0, 0, ls)
+        prog_g.adam_bf("adam_g", _p(self.model.g.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
+                       _p(og.v.flat), _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
+                       1.0, 0, ls)
+        prog_g.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
+                        _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
 
     def _build_update_fused(self, prog):
         """Single-process bf16: both TF-Adams + the beta-power / global-step update in one launch
@@ -905,11 +933,19 @@ class HipEngine:
         fork.record(cs)
         alt[0].wait_event(fork)
         H.run(self.progB, alt)
-        H.run(self.progA, [cs, side], self._a_fwd, -1)
+        if self._early_adam_d:
+            H.run(self.progA, [cs, side], self._a_fwd, self._a_gd)   # g_loss chain through D(fake)
+            left_d = torch.cuda.Event()
+            left_d.record(cs)
+            alt[0].wait_event(left_d)
+            H.run(self.progCd, alt)                                   # Adam(D) beside G's backward
+            H.run(self.progA, [cs, side], self._a_gd, -1)            # G's backward
+        else:
+            H.run(self.progA, [cs, side], self._a_fwd, -1)
         join = torch.cuda.Event()
         join.record(alt[0])
         cs.wait_event(join)
-        H.run(self.progC, [cs, side])
+        H.run(self.progCg if self._early_adam_d else self.progC, [cs, side])
 
     def _seg(self, i, stream):
         """Run segment i on `stream` (graph replay, or eager replay of its program ranges)."""
