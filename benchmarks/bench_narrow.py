@@ -28,6 +28,22 @@ def main():
     e1.synchronize()
     us = e0.elapsed_time(e1) * 1000 / 100
     print("narrow %s: %.2f us/launch" % ("valu" if os.environ.get("DCGAN_NARROW_VALU") else "mfma", us))
+    # D layer 0 forward on the direct kernel (2B = 256 images, 64x64x3 -> 32x32x64, + bias + lrelu)
+    xi = (torch.rand(256, 64, 64, 3, device=dev) * 2 - 1).to(torch.bfloat16)
+    w0 = (torch.randn(5, 5, 3, 64, device=dev) * 0.05).to(torch.bfloat16)
+    b0 = torch.zeros(64, device=dev)
+    y0 = torch.empty(256, 32, 32, 64, device=dev, dtype=torch.bfloat16)
+    prog = H.ext().Program(False)
+    for _ in range(20):
+        prog.conv3_direct("c3", _p(xi), _p(w0), _p(b0), _p(y0), 256, 64, 64, 3, 32, 32, 64, 1, 1, 2, 0.2, 0)
+    H.run(prog)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(5):
+        H.run(prog)
+    e1.record()
+    e1.synchronize()
+    print("conv3 direct (D0 fwd, 2B=256): %.2f us/launch" % (e0.elapsed_time(e1) * 1000 / 100))
 
 
 if __name__ == "__main__":

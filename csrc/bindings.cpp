@@ -582,6 +582,14 @@ class Program {
                            P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
     });
   }
+  // TF-SAME stride-2 5x5 conv with 1..4 input and 64 output channels (direct MFMA kernel, conv3.hip)
+  int conv3_direct(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int H, int W,
+                   int Cin, int Ho, int Wo, int Cout, int pad_y, int pad_x, int act, float leak, int stream) {
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_conv3_direct)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B, H,
+                                  W, Cin, Ho, Wo, Cout, pad_y, pad_x, act, leak, s);
+    });
+  }
   // TF-SAME stride-2 5x5 conv_transpose with 1..4 output channels (direct VALU kernel)
   int narrow_deconv(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int Hi, int Wi,
                     int C, int Ho, int Wo, int N, int pad, int act, float leak, int stream) {
@@ -738,6 +746,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("adam2", &Program::adam2)
       .def("nonfinite_check", &Program::nonfinite_check)
       .def("narrow_deconv", &Program::narrow_deconv)
+      .def("conv3_direct", &Program::conv3_direct)
       .def("pack", &Program::pack)
       .def("philox_uniform", &Program::philox_uniform)
       .def("im2col_s2", &Program::im2col_s2)

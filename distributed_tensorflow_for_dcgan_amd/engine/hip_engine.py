@@ -391,6 +391,12 @@ class HipEngine:
                              P, update_ema, slot=half, stream=stream)
             prev = hs(self.d_a[L.name])
 
+    def _d0_direct(self) -> bool:
+        """D layer 0 forward on the direct conv3 kernel (Cin <= 4, Cout = 64) instead of
+        im2col + GEMM; DCGAN_D0_IM2COL=1 keeps the im2col forward."""
+        L = self.dl[0]
+        return L.cin <= 4 and L.cout == 64 and os.environ.get("DCGAN_D0_IM2COL") != "1"
+
     def _split_dfwd_ok(self) -> bool:
         """Split forward (opt-in, DCGAN_SPLIT_DFWD=1): D(real) on the side stream beside G's
         forward, D(fake) after G. Measured on MI355X at 64x64, B=128: 1.334 vs 1.321 ms/step
@@ -463,7 +469,11 @@ class HipEngine:
             w = Wd[L.name + "/w"]  # HWIO [5,5,ci,co] = [tap][K][N]
             pad = same_pads(L.in_hw)[0]
             rows = B2 * L.out_hw ** 2
-            if i == 0 and L.cin % 8 != 0:
+            if i == 0 and self._d0_direct():  # image tile in LDS, no column matrix (conv3.hip)
+                prog.conv3_direct("d0.conv3", _p(prev), _p(w), _p(Pd[L.name + "/biases"]), _p(self.d_a[L.name]), B2,
+                                  L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad, pad, LRELU,
+                                  cfg.lrelu_leak, 0)
+            elif i == 0 and L.cin % 8 != 0:
                 prog.im2col_s2("d0.im2col", _p(prev), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                L.out_hw, pad, pad, self.kp_d0, 0)
                 self._igemm(prog, L.name, 2, self.d0_col, w, self.d_a[L.name], B2, 1, 1, self.kp_d0, L.out_hw,
@@ -538,6 +548,10 @@ class HipEngine:
             src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
             pad = same_pads(L.in_hw)[0]
             if i == 0 and L.cin % 8 != 0:
+                if self._d0_direct():  # the forward ran without a column matrix: build it here, off the
+                    # critical path (D's chain is the shorter of the two concurrent backward chains)
+                    prog.im2col_s2("d0.im2col", _p(self.d_in), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin,
+                                   L.out_hw, L.out_hw, pad, pad, self.kp_d0, 0)
                 self._wgrad(prog, L.name, 2, self.d0_col, 1, 1, self.kp_d0, dx, B2 * L.out_hw ** 2, 1, 1, L.cout, 0,
                             gD[L.name + "/w"])
             else:

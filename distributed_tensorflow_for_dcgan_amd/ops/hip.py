@@ -333,6 +333,22 @@ def conv2d_transpose_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, ou
     return (y, st) if stats else y
 
 
+def conv3_direct(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
+                 leak: float = 0.2) -> torch.Tensor:
+    """TF-SAME stride-2 5x5 conv with Cin <= 4 and Cout = 64 on the direct MFMA kernel
+    (conv3.hip: image tile staged in LDS, no column matrix). x [B,H,W,Cin], w HWIO [5,5,Cin,64]."""
+    _check_bf16(x, w)
+    B, Hh, Ww, C = x.shape
+    N = w.shape[-1]
+    Ho, Wo = -(-Hh // 2), -(-Ww // 2)
+    y = torch.empty(B, Ho, Wo, N, device=x.device, dtype=x.dtype)
+    prog = ext().Program(x.dtype == torch.float16)
+    prog.conv3_direct("conv3", _p(x), _p(w), _p(bias), _p(y), B, Hh, Ww, C, Ho, Wo, N, same_pads(Hh)[0],
+                      same_pads(Ww)[0], ACT[act], leak, 0)
+    run(prog)
+    return y
+
+
 def narrow_deconv(x: torch.Tensor, w: torch.Tensor, out_hw: Tuple[int, int], bias: Optional[torch.Tensor] = None,
                   act: Optional[str] = None, leak: float = 0.2) -> torch.Tensor:
     """TF-SAME stride-2 5x5 conv_transpose with N <= 4 output channels on the direct VALU

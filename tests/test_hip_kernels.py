@@ -468,6 +468,21 @@ def test_narrow_deconv(B, Hi, Ho, C, N, dtype):
     close(h.narrow_deconv(x, w, (Ho, Ho)), gx, 1e-2, "narrow as conv dgrad")
 
 
+@pytest.mark.parametrize("B,Hh,C,dtype", [(4, 64, 3, "bf16"), (2, 28, 1, "bf16"), (3, 33, 4, "bf16"),
+                                          (2, 64, 3, "fp16"), (1, 7, 3, "bf16")])
+def test_conv3_direct(B, Hh, C, dtype):
+    """Direct MFMA conv for D layer 0 (Cin <= 4 -> 64, + bias + lrelu): RGB, gray, 4-channel,
+    odd sizes (partial tiles, pad 2 at 7), fp16 build; vs the fp32 TF-SAME oracle."""
+    h = H()
+    edt = torch.float16 if dtype == "fp16" else torch.bfloat16
+    x = rnd(B, Hh, Hh, C, seed=70).to(edt)
+    w = rnd(5, 5, C, 64, scale=0.1, seed=71).to(edt)
+    bias = rnd(64, scale=0.1, seed=72)
+    y = h.conv3_direct(x, w, bias=bias, act="lrelu")
+    ref = R.lrelu(R.conv2d_same(x.float(), w.float(), bias))
+    close(y, ref, 1e-2, "conv3 direct")
+
+
 @pytest.mark.parametrize("P,groups,C", [(2048, 2, 80), (700, 1, 512), (96, 2, 64)])
 def test_bn_finalize_split_paths(P, groups, C):
     """Many partial rows -> the sliced finalize with a last-arrival combine (counters reset, so a
