@@ -939,7 +939,9 @@ class HipEngine:
         return self._alt_streams
 
     def _run_fused(self, cs):
-        """The "fused" schedule issued onto cs (+ forked alt streams); also what gets captured."""
+        """The "fused" schedule issued onto cs (+ forked alt streams); also what gets captured.
+        D's backward starts right after the forward: holding it until the g_loss chain has left
+        D (so it overlaps only G's backward) measured 1.314 vs 1.297 ms/step on MI355X."""
         side = self._streams()[1]
         alt = self._alt()
         H.run(self.progA, [cs, side], 0, self._a_fwd)
