@@ -53,7 +53,10 @@ def main():
     from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
     from distributed_tensorflow_for_dcgan_amd.engine.factory import build_engine
 
-    device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    # (local_rank modulo the visible GPUs only matters for the 1-GPU rehearsal of the multi-rank
+    # path over gloo, DCGAN_DIST_BACKEND=gloo; one rank per GPU otherwise)
+    device = (torch.device("cuda", local_rank % max(1, torch.cuda.device_count())) if torch.cuda.is_available()
+              else torch.device("cpu"))
     if device.type == "cuda":
         torch.cuda.set_device(device)
     pg = D.init_distributed(world, rank, device)

@@ -97,3 +97,25 @@ def test_timed_concurrent_schedule_matches_fused():
     pt = b.phase_times()
     assert set(pt) == {"fwd@end", "D_bwd_top@end", "G_chain@end", "D_bwd_rest@end", "adam_G@end", "adam_D@end"}
     assert all(v > 0 for v in pt.values())
+
+
+def test_bench_two_ranks_json_contract(tmp_path):
+    """bench.py's multi-rank path (torch.distributed.run, barrier + sync bracketing, MAX over
+    ranks, one JSON line from rank 0) with two ranks on this one GPU over gloo -- the driver's
+    N>1 scaling runs take the same code with RCCL, one rank per GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DCGAN_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "2",
+           "--steps", "4", "--warmup", "2"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 4 and res["warmup"] == 2
+    assert res["config"]["global_batch"] == 256 and res["config"]["parallelism"] == "dp2"
+    assert res["value"] > 0 and res["higher_is_better"] is True and res["scaling"] == "weak"
