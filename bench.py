@@ -86,6 +86,16 @@ def main():
     dt = time.perf_counter() - t0
     dt = D.max_over_ranks(dt, device)
     losses = eng.last_losses()
+    # self-verifying multi-GPU record: which backend the process group used, how many ranks it
+    # saw, and every rank's HIP device (all-gathered), so "RCCL saw N distinct GPUs" is checkable
+    backend, world_seen, devices = "none", 1, [torch.cuda.current_device() if device.type == "cuda" else -1]
+    if D.is_initialized():
+        import torch.distributed as tdist
+        backend, world_seen = tdist.get_backend(), tdist.get_world_size()
+        mine = torch.tensor([devices[0]], dtype=torch.int64, device=device if backend == "nccl" else "cpu")
+        allv = [torch.zeros_like(mine) for _ in range(world_seen)]
+        tdist.all_gather(allv, mine)
+        devices = [int(v.item()) for v in allv]
     imgs = args.gpus * args.batch_size * args.steps
     value = imgs / dt
     ms = dt / args.steps * 1e3
@@ -112,6 +122,8 @@ def main():
                        "global_batch": args.batch_size * args.gpus, "per_gpu_batch": args.batch_size,
                        "seq_len": None, "parallelism": "dp%d" % args.gpus, "engine": eng.name,
                        "hip_graph": bool(getattr(eng, "graph_enabled", False)),
+                       "backend": backend, "world_size": world_seen, "devices": devices,
+                       "kernels_per_step": eng.kernel_count() if hasattr(eng, "kernel_count") else None,
                        "gflop_per_image": round(cfg.flops_per_image() / 1e9, 4),
                        "tflops_achieved": round(value * cfg.flops_per_image() / 1e12, 2),
                        "last_losses": {k: round(float(v), 5) for k, v in losses.items()}},

@@ -17,17 +17,12 @@ class FakeReducer:
     all-reduce, to see which schedule hides which collective latency (no bandwidth
     contention is modelled)."""
 
-    def __init__(self, stream, us, cycles_per_us):
-        self.stream, self.cycles = stream, int(us * cycles_per_us)
+    def __init__(self, us, cycles_per_us):
+        self.cycles = int(us * cycles_per_us)
 
-    def launch(self):
-        self.stream.wait_stream(torch.cuda.current_stream())
+    def issue(self):  # on the comm stream (the engine's executor orders it after the producers)
         if self.cycles > 0:
-            with torch.cuda.stream(self.stream):
-                torch.cuda._sleep(self.cycles)
-
-    def wait(self, scale_in_place=False):
-        torch.cuda.current_stream().wait_stream(self.stream)
+            torch.cuda._sleep(self.cycles)
 
 
 def _cycles_per_us():
@@ -50,13 +45,15 @@ def main():
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig()
     eng = HipEngine(cfg, a.batch_size, dev)
-    eng.enable_timing()
+    eng.enable_timing()  # the segmented "concurrent" schedule, Adam(G) / Adam(D) apart
     if a.fake_comm_us:
         g_us, top_us, rest_us = (float(x) for x in a.fake_comm_us.split(","))
-        cs = torch.cuda.Stream(device=dev)
         cpu = _cycles_per_us()
-        eng.world = 2  # schedule + collective call points of DDP; the Adam 1/W scale stays 1
-        eng._ar_g, eng._ar_dtop, eng._ar_drest = (FakeReducer(cs, u, cpu) for u in (g_us, top_us, rest_us))
+        # collective call points of DDP on a comm stream (the programs were built for W=1, so the
+        # Adam 1/W scale stays 1 -- only the stream order of the DDP step is emulated)
+        eng.world = 2
+        eng.comm_stream = torch.cuda.Stream(device=dev)
+        eng._ar_g, eng._ar_dtop, eng._ar_drest = (FakeReducer(u, cpu) for u in (g_us, top_us, rest_us))
     eng.set_synthetic_batch(torch.rand(a.batch_size, 64, 64, 3, device=dev) * 2 - 1)
     for _ in range(a.warmup):
         eng.train_step()
@@ -71,7 +68,7 @@ def main():
         eng.train_step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.steps
-    print(json.dumps({"schedule": eng._schedule(), "hybrid": eng._hybrid, "fake_comm_us": a.fake_comm_us, "ms_per_step_timed": round(ms, 4),
+    print(json.dumps({"schedule": eng._schedule(), "fake_comm_us": a.fake_comm_us, "ms_per_step_timed": round(ms, 4),
                       "phases_ms": {k: round(v, 4) for k, v in acc.items()}}))
 
 

@@ -8,6 +8,15 @@
 // compute, 1.. = side streams) and event ops express cross-stream dependencies, so
 // gradient all-reduces can overlap backward compute.
 //
+// Every op also records the device byte ranges it reads and writes (`accesses`). The schedule
+// checker (engine/schedule_check.py) walks a whole training step -- programs, cross-stream
+// events, collectives -- and proves that no two ops on unordered streams touch overlapping
+// bytes with at least one write. A Program built with dry=true records ops and accesses but
+// allocates nothing on the device (workspaces get disjoint fake addresses) and cannot run:
+// that is how the checker runs on a CPU-only machine.
+//
+// Element type per Program: 0 = bf16, 1 = fp16, 2 = fp32 (the reference-precision build).
+//
 // No torch headers: pointers are passed as integers (tensor.data_ptr()), streams as the raw
 // hipStream_t integer (torch.cuda.Stream.cuda_stream). Built with hipcc for gfx950.
 #include <pybind11/pybind11.h>
@@ -19,22 +28,29 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "hip/kernels.h"
 
-// The fp16 build of the same kernels (csrc/build.py compiles every .hip twice): identical C
-// signatures -- element pointers are 16-bit either way -- with a `_f16` suffix.
+// The fp16 and fp32 builds of the same kernels (csrc/build.py compiles every .hip three times):
+// identical C signatures (element pointers are void-compatible at the ABI level) with `_f16` /
+// `_f32` suffixes.
 #undef DCG_API
 #define DCG_API(name) name##_f16
 extern "C" {
 #include "hip/launchers.inc"
 }
 #undef DCG_API
+#define DCG_API(name) name##_f32
+extern "C" {
+#include "hip/launchers.inc"
+}
+#undef DCG_API
 #define DCG_API(name) name
 
-// launcher of the Program's element type (bf16 or fp16)
-#define KF(fn) (f16_ ? fn##_f16 : fn)
+// launcher of the Program's element type (bf16, fp16 or fp32)
+#define KF(fn) (dt_ == 2 ? fn##_f32 : dt_ == 1 ? fn##_f16 : fn)
 
 namespace py = pybind11;
 using namespace dcg;
@@ -48,18 +64,43 @@ using namespace dcg;
 template <class T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 
+struct Acc {
+  uintptr_t p;
+  size_t n;
+  bool w;
+};
+
+enum OpKind { OP_LAUNCH = 0, OP_RECORD = 1, OP_WAIT = 2 };
+
 struct Op {
   std::string name;
   int stream;  // slot
+  int kind;
+  int event;
+  std::vector<Acc> acc;
   std::function<int(hipStream_t)> fn;
+};
+
+// access-list builder: null pointers / empty ranges are dropped
+struct AccList {
+  std::vector<Acc> v;
+  AccList& r(uintptr_t p, size_t n) { if (p && n) v.push_back({p, n, false}); return *this; }
+  AccList& w(uintptr_t p, size_t n) { if (p && n) v.push_back({p, n, true}); return *this; }
 };
 
 class Program {
  public:
-  explicit Program(bool f16 = false) : f16_(f16) {}
-  bool f16() const { return f16_; }
+  explicit Program(int dtype = 0, bool dry = false) : dt_(dtype), dry_(dry) {
+    if (dtype < 0 || dtype > 2) throw std::runtime_error("Program dtype must be 0 (bf16), 1 (fp16) or 2 (fp32)");
+    es_ = dtype == 2 ? 4 : 2;
+  }
+  int dtype() const { return dt_; }
+  bool f16() const { return dt_ == 1; }
+  bool dry() const { return dry_; }
+  int elem_size() const { return (int)es_; }
 
   ~Program() {
+    if (dry_) return;
     for (void* p : dev_allocs_) (void)hipFree(p);
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   }
@@ -67,7 +108,16 @@ class Program {
   int size() const { return (int)ops_.size(); }
   std::string name(int i) const { return ops_.at(i).name; }
 
+  // (name, stream slot, kind, event, [(ptr, bytes, is_write), ...]) of op i
+  py::tuple op_info(int i) const {
+    const Op& o = ops_.at(i);
+    py::list acc;
+    for (const Acc& a : o.acc) acc.append(py::make_tuple(a.p, a.n, a.w));
+    return py::make_tuple(o.name, o.stream, o.kind, o.event, acc);
+  }
+
   void run(std::vector<uintptr_t> streams, int begin, int end) {
+    if (dry_) throw std::runtime_error("a dry Program records only; it cannot run");
     if (end < 0 || end > (int)ops_.size()) end = (int)ops_.size();
     for (int i = begin; i < end; ++i) {
       const Op& op = ops_[i];
@@ -80,29 +130,30 @@ class Program {
 
   // ------------------------------------------------------------------ events
   int new_event() {
-    hipEvent_t e;
-    HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipEvent_t e = nullptr;
+    if (!dry_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     events_.push_back(e);
     return (int)events_.size() - 1;
   }
   int record(int ev, int stream) {
     hipEvent_t e = events_.at(ev);
-    return add("record", stream, [e](hipStream_t s) { return (int)hipEventRecord(e, s); });
+    return add("record", stream, [e](hipStream_t s) { return (int)hipEventRecord(e, s); }, {}, OP_RECORD, ev);
   }
   int wait(int ev, int stream) {
     hipEvent_t e = events_.at(ev);
-    return add("wait", stream, [e](hipStream_t s) { return (int)hipStreamWaitEvent(s, e, 0); });
+    return add("wait", stream, [e](hipStream_t s) { return (int)hipStreamWaitEvent(s, e, 0); }, {}, OP_WAIT, ev);
   }
   int memset(uintptr_t ptr, size_t bytes, int stream) {
     void* p = reinterpret_cast<void*>(ptr);
-    return add("memset", stream, [p, bytes](hipStream_t s) { return (int)hipMemsetAsync(p, 0, bytes, s); });
+    return add("memset", stream, [p, bytes](hipStream_t s) { return (int)hipMemsetAsync(p, 0, bytes, s); },
+               AccList().w(ptr, bytes).v);
   }
   int copy(uintptr_t dst, uintptr_t src, size_t bytes, int stream) {
     void* d = reinterpret_cast<void*>(dst);
     const void* sp = reinterpret_cast<const void*>(src);
     return add("copy", stream, [d, sp, bytes](hipStream_t s) {
       return (int)hipMemcpyAsync(d, sp, bytes, hipMemcpyDeviceToDevice, s);
-    });
+    }, AccList().r(src, bytes).w(dst, bytes).v);
   }
 
   // ------------------------------------------------------------------ implicit GEMM conv
@@ -116,6 +167,7 @@ class Program {
 
   // cfg < 200: igemm.hip tiles (Bw k-contiguous only, no split-K); cfg 200..219: igemm3.hip
   // (bkn = 1 reads Bw as [tap][Kc][N]; kb_valid = number of real B k-rows; splits = split-K).
+  // The fp32 build has one tile family (igemm_f32.hip) behind the same entry points.
   int igemm_ex(std::string name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win, int Kc,
                int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
                uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
@@ -123,12 +175,13 @@ class Program {
                int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
     int bm = 0, bn = 0, ns = 0;
     const bool v3 = cfg >= 200;
-    if (v3 ? dcg_igemm3_tile(cfg, &bm, &bn, &ns) : dcg_igemm_tile(cfg, &bm, &bn))
-      throw std::runtime_error("bad igemm cfg " + std::to_string(cfg));
+    if (v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
+      throw std::runtime_error("bad igemm cfg " + std::to_string(cfg) + " for this element type");
     if (!v3 && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
     if (splits < 1) throw std::runtime_error("splits must be >= 1");
-    if (Kc % 8) throw std::runtime_error("igemm needs Kc % 8 == 0 (16-byte A rows)");
-    if (bkn && N % 8) throw std::runtime_error("igemm bkn needs N % 8 == 0");
+    const int kal = (int)(16 / es_);  // 16-byte A rows
+    if (Kc % kal) throw std::runtime_error("igemm needs 16-byte A rows (Kc % " + std::to_string(kal) + " == 0)");
+    if (bkn && N % kal) throw std::runtime_error("igemm bkn needs 16-byte B rows");
     if (kb_valid < 0) kb_valid = Kc;
     if (kb_valid > Kc) throw std::runtime_error("kb_valid > Kc");
     std::vector<IGemmPhase> ph;
@@ -137,7 +190,7 @@ class Program {
     a.Bw = P<const elem_t>(Bw); a.N = N;
     a.C = P<void>(C); a.out_f32 = out_f32; a.outH = Hout; a.outW = Wout; a.ldc = ldc; a.cofs = cofs;
     a.bias = P<const float>(bias); a.act = act; a.leak = leak; a.stats = P<float>(stats);
-    size_t a_elems, b_elems;
+    size_t a_elems, b_elems, c_rows;
     if (mode == 0) {
       a.sstride = 2; a.plain = 0; a.ostride = 1;
       IGemmPhase p{};
@@ -148,6 +201,7 @@ class Program {
       p.fd_hw = fastdiv_make(Hout * Wout); p.fd_w = fastdiv_make(Wout);
       ph.push_back(p);
       a_elems = (size_t)Bn * Hin * Win * Kc; b_elems = (size_t)25 * N * Kc;
+      c_rows = (size_t)Bn * Hout * Wout;
     } else if (mode == 1) {
       a.sstride = 1; a.plain = 0; a.ostride = 2;
       for (int py = 0; py < 2; ++py)
@@ -169,6 +223,7 @@ class Program {
           if (p.M > 0) ph.push_back(p);
         }
       a_elems = (size_t)Bn * Hin * Win * Kc; b_elems = (size_t)25 * N * Kc;
+      c_rows = (size_t)Bn * Hout * Wout;
     } else if (mode == 2) {
       a.sstride = 1; a.plain = 1; a.ostride = 1;
       IGemmPhase p{};
@@ -176,12 +231,13 @@ class Program {
       p.fd_hw = fastdiv_make(1); p.fd_w = fastdiv_make(1);
       ph.push_back(p);
       a_elems = (size_t)p.M * Kc; b_elems = bkn ? (size_t)kb_valid * N : (size_t)N * Kc;
+      c_rows = (size_t)p.M;
     } else {
       throw std::runtime_error("bad igemm mode");
     }
-    if (a_elems * 2 >= OOB || b_elems * 2 >= OOB)
+    if (a_elems * es_ >= OOB || b_elems * es_ >= OOB)
       throw std::runtime_error("igemm operand exceeds the 3.875 GiB buffer-descriptor range");
-    a.a_bytes = (uint32_t)(a_elems * 2); a.b_bytes = (uint32_t)(b_elems * 2);
+    a.a_bytes = (uint32_t)(a_elems * es_); a.b_bytes = (uint32_t)(b_elems * es_);
     for (auto& q : ph)
       for (int t = 0; t < q.ntaps; ++t)
         q.tap[t] = (q.dy[t] & 0xff) | ((q.dx[t] & 0xff) << 8) | ((int)q.wtap[t] << 16);
@@ -198,23 +254,27 @@ class Program {
     for (auto& p : ph) maxM = std::max(maxM, p.M);
     const int mtiles = (maxM + bm - 1) / bm, ntiles = (N + bn - 1) / bn;
     a.mtiles = mtiles;
-    void* dph = nullptr;
-    HIPCHECK(hipMalloc(&dph, ph.size() * sizeof(IGemmPhase)));
-    HIPCHECK(hipMemcpy(dph, ph.data(), ph.size() * sizeof(IGemmPhase), hipMemcpyHostToDevice));
-    dev_allocs_.push_back(dph);
-    a.ph = reinterpret_cast<const IGemmPhase*>(dph);
+    a.ph = reinterpret_cast<const IGemmPhase*>(dev_alloc(ph.size() * sizeof(IGemmPhase), ph.data()));
     last_mtiles_ = mtiles;
     last_nphases_ = a.nphases;
     a.kb_valid = kb_valid;
     a.splits = splits;
+    const size_t out_es = out_f32 ? 4 : es_;
+    AccList acc;
+    acc.r(A, a_elems * es_).r(Bw, b_elems * es_).r(bias, (size_t)N * 4)
+        .w(C, (c_rows - 1) * ldc * out_es + (size_t)(cofs + N) * out_es)
+        .w(stats, (size_t)mtiles * a.nphases * 2 * N * 4);
     if (bnb_x) {
       const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
+      if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
       if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 16384 > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
+      const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
       if (bnb_store_g) {  // activation backward only (no BN): x, mean, rstd and groups unused
         if (!stats || !bnb_y) throw std::runtime_error("igemm act-backward store: needs stats and y");
         a.bnb_x = P<const elem_t>(bnb_y); a.bnb_y = P<const elem_t>(bnb_y);
         a.bnb_rpg = 1 << 30; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak; a.bnb_store_g = 1;
+        acc.r(bnb_y, xy_bytes);
       } else {
         if (!stats || bnb_rpg <= 0 || !bnb_y || !bnb_mean || !bnb_rstd)
           throw std::runtime_error("igemm bnb: needs stats, rows-per-group, y, mean, rstd");
@@ -223,6 +283,8 @@ class Program {
         a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
         a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
         a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
+        const size_t groups = (size_t)(maxM / bnb_rpg);
+        acc.r(bnb_x, xy_bytes).r(bnb_y, xy_bytes).r(bnb_mean, groups * N * 4).r(bnb_rstd, groups * N * 4);
       }
     }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
@@ -230,21 +292,16 @@ class Program {
     if (!v3)
       return add(name, stream, [this, a, cfg, mtiles, ntiles](hipStream_t s) {
         return KF(dcg_igemm_launch)(&a, cfg, mtiles, ntiles, s);
-      });
+      }, acc.v);
     const size_t tiles = (size_t)mtiles * ntiles * a.nphases;
     if (splits > 1) {  // per-op workspace + zeroed arrival counters (reset by the kernel itself)
-      void* ws = nullptr;
-      void* ctr = nullptr;
-      HIPCHECK(hipMalloc(&ws, tiles * splits * (size_t)bm * bn * sizeof(float)));
-      HIPCHECK(hipMalloc(&ctr, tiles * sizeof(unsigned)));
-      HIPCHECK(hipMemset(ctr, 0, tiles * sizeof(unsigned)));
-      dev_allocs_.push_back(ws);
-      dev_allocs_.push_back(ctr);
-      a.ws = reinterpret_cast<float*>(ws);
-      a.counters = reinterpret_cast<unsigned*>(ctr);
+      a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * (size_t)bm * bn * sizeof(float)));
+      a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
+      acc.w((uintptr_t)a.ws, tiles * splits * (size_t)bm * bn * sizeof(float)).w((uintptr_t)a.counters, tiles * 4);
     }
     const unsigned blocks = (unsigned)(tiles * splits);
-    return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); });
+    return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); },
+               acc.v);
   }
   int last_mtiles() const { return last_mtiles_; }
   int last_nphases() const { return last_nphases_; }
@@ -264,15 +321,16 @@ class Program {
     a.kt_per_split = (KT + splits - 1) / splits;
     const size_t g_elems = mode == 2 ? (size_t)a.K * Mc : (size_t)Bn * Hg * Wg * Mc;
     const size_t d_elems = (size_t)a.K * Nc;
-    if (g_elems * 2 >= OOB || d_elems * 2 >= OOB)
+    if (g_elems * es_ >= OOB || d_elems * es_ >= OOB)
       throw std::runtime_error("wgrad operand exceeds the 3.875 GiB buffer-descriptor range");
-    a.g_bytes = (uint32_t)(g_elems * 2); a.d_bytes = (uint32_t)(d_elems * 2);
+    a.g_bytes = (uint32_t)(g_elems * es_); a.d_bytes = (uint32_t)(d_elems * es_);
     a.fd_hw = fastdiv_make(Hd * Wd); a.fd_w = fastdiv_make(Wd); a.Hd = Hd; a.Wd = Wd;
     const size_t n = (size_t)a.ntaps * Mc * Nc;
     if (dst_elems > n) throw std::runtime_error("wgrad dst larger than result");
     float* slab = P<float>(slabs);
     float* d = P<float>(dst);
-    add(name, stream, [this, a, cfg, splits](hipStream_t s) { return KF(dcg_wgrad_launch)(&a, cfg, splits, s); });
+    add(name, stream, [this, a, cfg, splits](hipStream_t s) { return KF(dcg_wgrad_launch)(&a, cfg, splits, s); },
+        AccList().r(G, g_elems * es_).r(Dm, d_elems * es_).w(slabs, (size_t)splits * n * 4).v);
     // plain mode may carry padded rows (im2col K padding): reduce only the first dst_elems of
     // each slab's leading part -- rows are m-major so the valid prefix is contiguous.
     return add(name + ".reduce", stream, [this, slab, splits, n, d, dst_elems, scale](hipStream_t s) {
@@ -281,7 +339,7 @@ class Program {
       int rc = KF(dcg_splitk_reduce)(slab, splits, n, slab, scale, s);
       if (rc) return rc;
       return (int)hipMemcpyAsync(d, slab, dst_elems * sizeof(float), hipMemcpyDeviceToDevice, s);
-    });
+    }, AccList().w(slabs, (size_t)splits * n * 4).w(dst, dst_elems * 4).v);
   }
 
   // weight gradient v3 (wgrad3.hip): the 25-tap gather GEMM with the split-K reduction in-kernel,
@@ -289,8 +347,9 @@ class Program {
   int wgrad3(std::string name, uintptr_t G, int Hg, int Wg, int Mc, uintptr_t Dm, int Bn, int Hd, int Wd, int Nc,
              int pad, int cfg, int splits, uintptr_t dst, float scale, int stream) {
     int bm = 0, bn = 0, ns = 0;
-    if (dcg_wgrad3_tile(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
-    if (Mc % 8 || Nc % 8) throw std::runtime_error("wgrad3 needs Mc % 8 == 0 and Nc % 8 == 0 (16-byte DMA chunks)");
+    if (KF(dcg_wgrad3_tile)(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
+    const int al = (int)(16 / es_);
+    if (Mc % al || Nc % al) throw std::runtime_error("wgrad3 needs 16-byte channel rows (Mc, Nc multiples of 16 bytes)");
     if (splits < 1) throw std::runtime_error("splits must be >= 1");
     WGrad3Args a{};
     a.G = P<const elem_t>(G); a.Hg = Hg; a.Wg = Wg; a.Mc = Mc;
@@ -299,164 +358,139 @@ class Program {
     const int KT = (a.K + 63) / 64;
     a.kt_per_split = (KT + splits - 1) / splits;
     const size_t g_elems = (size_t)Bn * Hg * Wg * Mc, d_elems = (size_t)a.K * Nc;
-    if (g_elems * 2 >= OOB || d_elems * 2 >= OOB)
+    if (g_elems * es_ >= OOB || d_elems * es_ >= OOB)
       throw std::runtime_error("wgrad3 operand exceeds the 3.875 GiB buffer-descriptor range");
-    a.g_bytes = (uint32_t)(g_elems * 2); a.d_bytes = (uint32_t)(d_elems * 2);
+    a.g_bytes = (uint32_t)(g_elems * es_); a.d_bytes = (uint32_t)(d_elems * es_);
     a.fd_hw = fastdiv_make(Hd * Wd); a.fd_w = fastdiv_make(Wd); a.Hd = Hd; a.Wd = Wd;
     a.out = P<float>(dst); a.scale = scale;
+    AccList acc;
+    acc.r(G, g_elems * es_).r(Dm, d_elems * es_).w(dst, (size_t)25 * Mc * Nc * 4);
     const size_t tiles = (size_t)((Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * 25;
     if (splits > 1) {
       if ((size_t)splits * bm * bn * 4 >= OOB) throw std::runtime_error("wgrad3: split slabs too large");
-      void* ws = nullptr;
-      void* ctr = nullptr;
-      HIPCHECK(hipMalloc(&ws, tiles * splits * (size_t)bm * bn * sizeof(float)));
-      HIPCHECK(hipMalloc(&ctr, tiles * sizeof(unsigned)));
-      HIPCHECK(hipMemset(ctr, 0, tiles * sizeof(unsigned)));
-      dev_allocs_.push_back(ws);
-      dev_allocs_.push_back(ctr);
-      a.ws = reinterpret_cast<float*>(ws);
-      a.counters = reinterpret_cast<unsigned*>(ctr);
+      a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * (size_t)bm * bn * sizeof(float)));
+      a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
+      acc.w((uintptr_t)a.ws, tiles * splits * (size_t)bm * bn * 4).w((uintptr_t)a.counters, tiles * 4);
     }
-    return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad3_launch)(&a, cfg, s); });
+    return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad3_launch)(&a, cfg, s); }, acc.v);
   }
 
   // ------------------------------------------------------------------ BN / activations
   int colstats(std::string name, int mode, uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                int act, float leak, int R, int C, int rows_per_block, int rows_per_group, uintptr_t part,
                int stream) {
+    const size_t t = (size_t)R * C * es_;
+    const int Pn = (R + rows_per_block - 1) / rows_per_block;
+    const size_t groups = (size_t)((R + rows_per_group - 1) / rows_per_group);
+    AccList acc;
+    acc.r(x, t).w(part, (size_t)Pn * 2 * C * 4);
+    if (mode == 1) acc.r(dy, t).r(y, t).r(mean, groups * C * 4).r(rstd, groups * C * 4);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_colstats)(mode, P<const elem_t>(x), P<const elem_t>(dy), P<const elem_t>(y), P<const float>(mean),
                           P<const float>(rstd), act, leak, R, C, rows_per_block, rows_per_group, P<float>(part), s);
-    });
+    }, acc.v);
   }
   int bn_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, double count, uintptr_t gamma,
                   uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
                   uintptr_t ema_mean, uintptr_t ema_var, float decay, int stream) {
-    if (use_rows_fin()) {
-      const int PS = rows_slices(ppg, C);
-      double* ws = nullptr;
-      unsigned* ctr = nullptr;
-      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)groups);
-      return add(name, stream, [=](hipStream_t s) {
-        return KF(dcg_bn_finalize_rows)(0, P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
-                                        P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
-                                        P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, nullptr,
-                                        nullptr, nullptr, ws, ctr, PS, s);
-      });
-    }
+    const size_t gc = (size_t)groups * C * 4;
+    AccList acc;
+    acc.r(part, (size_t)groups * ppg * 2 * C * 4).r(gamma, (size_t)C * 4).r(beta, (size_t)C * 4)
+        .w(mean, gc).w(rstd, gc).w(scale, gc).w(shift, gc).w(ema_mean, gc).w(ema_var, gc);
     int PS = split_slices(ppg);
     if (PS > 1) {  // many partial rows: sliced reduction + last-arrival finalize
       double* ws = nullptr;
       unsigned* ctr = nullptr;
-      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)groups * ((C + 15) / 16));
+      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)groups * ((C + 15) / 16), acc);
       return add(name, stream, [=](hipStream_t s) {
         return KF(dcg_bn_finalize_split)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                                          P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
                                          P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, ws, ctr, PS, s);
-      });
+      }, acc.v);
     }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_finalize)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                              P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
                              P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, s);
-    });
+    }, acc.v);
   }
   static int split_slices(int ppg) { return ppg > 64 ? std::min(32, (ppg + 63) / 64) : 1; }
-  // row-wide finalize (bn_finalize_rows_kernel): ~8 partial rows per row lane per slice
-  // measured slower than the 16-channel split finalize on the 64x64 step (+85 us): opt-in only
-  static bool use_rows_fin() {
-    const char* e = getenv("DCGAN_BN_FIN_V2");
-    return e && e[0] == '1';
+  void alloc_split(double** ws, unsigned** ctr, size_t ws_elems, size_t counters, AccList& acc) {
+    *ws = reinterpret_cast<double*>(dev_alloc(ws_elems * sizeof(double)));
+    *ctr = reinterpret_cast<unsigned*>(dev_alloc(counters * sizeof(unsigned), nullptr, true));
+    acc.w((uintptr_t)*ws, ws_elems * 8).w((uintptr_t)*ctr, counters * 4);
   }
-  static int rows_slices(int ppg, int C) {
-    const int lanes = C <= 512 ? std::max(1, 512 / C) : 1;
-    return std::max(1, std::min(64, (ppg + lanes * 8 - 1) / (lanes * 8)));
-  }
-  void alloc_split(double** ws, unsigned** ctr, size_t ws_elems, size_t counters) {
-    void* w = nullptr;
-    void* c = nullptr;
-    HIPCHECK(hipMalloc(&w, ws_elems * sizeof(double)));
-    HIPCHECK(hipMalloc(&c, counters * sizeof(unsigned)));
-    HIPCHECK(hipMemset(c, 0, counters * sizeof(unsigned)));
-    dev_allocs_.push_back(w);
-    dev_allocs_.push_back(c);
-    *ws = reinterpret_cast<double*>(w);
-    *ctr = reinterpret_cast<unsigned*>(c);
-  }
+  // debias_ptr (optional): device scalar multiplying the moving averages (TF zero-debiasing,
+  // 1 / (1 - decay^t) written by the host before the sampler runs); else the constant debias
   int bn_coef_eval(std::string name, int C, uintptr_t gamma, uintptr_t beta, float eps, uintptr_t mean,
-                   uintptr_t var, float debias, uintptr_t scale, uintptr_t shift, int stream) {
+                   uintptr_t var, float debias, uintptr_t scale, uintptr_t shift, int stream, uintptr_t debias_ptr) {
+    const size_t c4 = (size_t)C * 4;
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_coef_eval)(C, P<const float>(gamma), P<const float>(beta), eps, P<const float>(mean),
-                              P<const float>(var), debias, P<float>(scale), P<float>(shift), s);
-    });
+                              P<const float>(var), debias, P<const float>(debias_ptr), P<float>(scale),
+                              P<float>(shift), s);
+    }, AccList().r(gamma, c4).r(beta, c4).r(mean, c4).r(var, c4).r(debias_ptr, 4).w(scale, c4).w(shift, c4).v);
   }
   int bn_apply_act(std::string name, uintptr_t x, uintptr_t y, uintptr_t scale, uintptr_t shift, int R, int C,
                    int rows_per_group, int act, float leak, int stream) {
+    const size_t t = (size_t)R * C * es_, gc = (size_t)((R + rows_per_group - 1) / rows_per_group) * C * 4;
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_apply_act)(P<const elem_t>(x), P<elem_t>(y), P<const float>(scale), P<const float>(shift), R, C,
                               rows_per_group, act, leak, s);
-    });
+    }, AccList().r(x, t).w(y, t).r(scale, gc).r(shift, gc).v);
   }
   int bn_bwd_finalize(std::string name, uintptr_t part, int ppg, int groups, int C, float count, uintptr_t gamma,
                       uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
                       int stream) {
-    if (use_rows_fin()) {
-      const int PS = rows_slices(ppg, C);
-      double* ws = nullptr;
-      unsigned* ctr = nullptr;
-      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, 1);
-      return add(name, stream, [=](hipStream_t s) {
-        return KF(dcg_bn_finalize_rows)(1, P<const float>(part), ppg, groups, C, (double)count, P<const float>(gamma),
-                                        nullptr, 0.f, P<float>(mean), P<float>(rstd), nullptr, nullptr, nullptr,
-                                        nullptr, 0.f, P<float>(dgamma), P<float>(dbeta), P<float>(coef), ws, ctr, PS,
-                                        s);
-      });
-    }
+    const size_t gc = (size_t)groups * C * 4;
+    AccList acc;
+    acc.r(part, (size_t)groups * ppg * 2 * C * 4).r(gamma, (size_t)C * 4).r(mean, gc).r(rstd, gc)
+        .w(dgamma, (size_t)C * 4).w(dbeta, (size_t)C * 4).w(coef, 3 * gc);
     int PS = split_slices(ppg);
     if (PS > 1) {
       double* ws = nullptr;
       unsigned* ctr = nullptr;
-      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)((C + 15) / 16));
+      alloc_split(&ws, &ctr, (size_t)groups * PS * 2 * C, (size_t)((C + 15) / 16), acc);
       return add(name, stream, [=](hipStream_t s) {
         return KF(dcg_bn_bwd_finalize_split)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                                              P<const float>(mean), P<const float>(rstd), P<float>(dgamma),
                                              P<float>(dbeta), P<float>(coef), ws, ctr, PS, s);
-      });
+      }, acc.v);
     }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_bwd_finalize)(P<const float>(part), ppg, groups, C, count, P<const float>(gamma),
                                  P<const float>(mean), P<const float>(rstd), P<float>(dgamma), P<float>(dbeta),
                                  P<float>(coef), s);
-    });
+    }, acc.v);
   }
   int bn_bwd_apply(std::string name, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t coef, uintptr_t dx, int R,
                    int C, int rows_per_group, int act, float leak, int stream) {
+    const size_t t = (size_t)R * C * es_, gc = (size_t)((R + rows_per_group - 1) / rows_per_group) * C * 4;
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_bwd_apply)(P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x), P<const float>(coef),
                               P<elem_t>(dx), R, C, rows_per_group, act, leak, s);
-    });
+    }, AccList().r(dy, t).r(y, t).r(x, t).r(coef, 3 * gc).w(dx, t).v);
   }
   int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_act_bwd)(P<const elem_t>(dy), P<const elem_t>(y), P<elem_t>(dx), n, act, leak, s);
-    });
+    }, AccList().r(dy, n * es_).r(y, n * es_).w(dx, n * es_).v);
   }
   // dx = dy * act'(y) and db = column sums of dx in one launch (last-arrival reduction)
   int act_bwd_dbias(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, int R, int C, int act, float leak,
                     uintptr_t db, int stream) {
     const int max_blocks = 256;  // every block bumps one arrival counter: keep the atomics few
-    void* part = nullptr;
-    void* ctr = nullptr;
-    HIPCHECK(hipMalloc(&part, (size_t)max_blocks * C * sizeof(float)));
-    HIPCHECK(hipMalloc(&ctr, sizeof(unsigned)));
-    HIPCHECK(hipMemset(ctr, 0, sizeof(unsigned)));
-    dev_allocs_.push_back(part);
-    dev_allocs_.push_back(ctr);
+    AccList acc;
+    const size_t t = (size_t)R * C * es_;
+    acc.r(dy, t).r(y, t).w(dx, t).w(db, (size_t)C * 4);
+    void* part = dev_alloc((size_t)max_blocks * C * sizeof(float));
+    void* ctr = dev_alloc(sizeof(unsigned), nullptr, true);
+    acc.w((uintptr_t)part, (size_t)max_blocks * C * 4).w((uintptr_t)ctr, 4);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_act_bwd_dbias)(P<const elem_t>(dy), P<const elem_t>(y), P<elem_t>(dx), R, C, act, leak,
                                    reinterpret_cast<float*>(part), max_blocks, reinterpret_cast<unsigned*>(ctr),
                                    P<float>(db), s);
-    });
+    }, acc.v);
   }
 
   // D head backward (weight + bias + data gradient) in one launch
@@ -465,36 +499,41 @@ class Program {
   int head_bwd(std::string name, uintptr_t x, uintptr_t dl, uintptr_t w, uintptr_t dx, uintptr_t dW, uintptr_t db,
                int R, int K, int stream, uintptr_t bx, uintptr_t by, uintptr_t mean, uintptr_t rstd, int C, int rpg,
                int act, float leak, uintptr_t part) {
+    const size_t t = (size_t)R * K * es_;
+    AccList acc;
+    acc.r(x, t).r(dl, (size_t)R * 4).r(w, (size_t)K * 4).w(dx, t).w(dW, (size_t)K * 4).w(db, 4);
+    if (bx) {
+      const size_t groups = (size_t)((R + rpg - 1) / rpg);
+      acc.r(bx, t).r(by, t).r(mean, groups * C * 4).r(rstd, groups * C * 4).w(part, groups * (K / C) * 2 * C * 4);
+    }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_head_bwd)(P<const elem_t>(x), P<const float>(dl), P<const float>(w), P<elem_t>(dx), P<float>(dW),
                               P<float>(db), R, K, P<const elem_t>(bx), P<const elem_t>(by), P<const float>(mean),
                               P<const float>(rstd), C, rpg, act, leak, P<float>(part), s);
-    });
+    }, acc.v);
   }
 
   int sum_partials(std::string name, uintptr_t part, int Pn, int stride, int C, uintptr_t dst, int stream) {
+    AccList acc;
+    acc.r(part, ((size_t)(Pn - 1) * stride + C) * 4).w(dst, (size_t)C * 4);
     const int PS = split_slices(Pn);
     if (PS > 1) {  // many rows: sliced + last-arrival combine
-      void* ws = nullptr;
-      void* ctr = nullptr;
-      HIPCHECK(hipMalloc(&ws, (size_t)PS * C * sizeof(float)));
-      HIPCHECK(hipMalloc(&ctr, (size_t)((C + 15) / 16) * sizeof(unsigned)));
-      HIPCHECK(hipMemset(ctr, 0, (size_t)((C + 15) / 16) * sizeof(unsigned)));
-      dev_allocs_.push_back(ws);
-      dev_allocs_.push_back(ctr);
+      void* ws = dev_alloc((size_t)PS * C * sizeof(float));
+      void* ctr = dev_alloc((size_t)((C + 15) / 16) * sizeof(unsigned), nullptr, true);
+      acc.w((uintptr_t)ws, (size_t)PS * C * 4).w((uintptr_t)ctr, (size_t)((C + 15) / 16) * 4);
       return add(name, stream, [=](hipStream_t s) {
         return KF(dcg_sum_partials_split)(P<const float>(part), Pn, stride, C, P<float>(dst),
                                           reinterpret_cast<float*>(ws), reinterpret_cast<unsigned*>(ctr), PS, s);
-      });
+      }, acc.v);
     }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_sum_partials)(P<const float>(part), Pn, stride, C, P<float>(dst), s);
-    });
+    }, acc.v);
   }
   int colsum_small(std::string name, uintptr_t x, int R, int C, uintptr_t part, int blocks, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_colsum_small)(P<const elem_t>(x), R, C, P<float>(part), blocks, s);
-    });
+    }, AccList().r(x, (size_t)R * C * es_).w(part, (size_t)blocks * C * 4).v);
   }
 
   // ------------------------------------------------------------------ heads, losses, optimiser
@@ -503,7 +542,8 @@ class Program {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_gan_loss)(P<const float>(logits), B, P<float>(out), P<float>(dl_d), P<float>(dl_g),
                           P<float>(prob), P<const float>(ls), s);
-    });
+    }, AccList().r(logits, (size_t)B * 8).w(out, 16).w(dl_d, (size_t)B * 8).w(dl_g, (size_t)B * 4)
+           .w(prob, (size_t)B * 8).r(ls, 12).v);
   }
   // stats (optional): BN partial statistics of the output, channel = column % C ->
   // [(B / 8) * (N / C)][2][C] partial rows (the row block of the kernel is 8)
@@ -511,48 +551,54 @@ class Program {
   // step counter, identical to philox_uniform) and written to z
   int linear_fwd(std::string name, uintptr_t z, uintptr_t W, uintptr_t b, uintptr_t out, int B, int K, int N,
                  int stream, uintptr_t stats = 0, int C = 0, uintptr_t gen_step = 0, uint64_t gen_seed = 0) {
+    AccList acc;
+    if (gen_step) acc.w(z, (size_t)B * K * 4).r(gen_step, 8);
+    else acc.r(z, (size_t)B * K * 4);
+    acc.r(W, (size_t)K * N * 4).r(b, (size_t)N * 4).w(out, (size_t)B * N * es_);
+    if (stats) acc.w(stats, (size_t)((B + 7) / 8) * (N / C) * 2 * C * 4);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_linear_fwd)(P<float>(z), P<const float>(W), P<const float>(b), P<elem_t>(out), B, K, N,
                                 P<float>(stats), C, P<const unsigned long long>(gen_step), gen_seed, s);
-    });
+    }, acc.v);
   }
   int linear_wgrad(std::string name, uintptr_t z, uintptr_t dh, uintptr_t dW, uintptr_t db, int B, int K, int N,
                    int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_linear_wgrad)(P<const float>(z), P<const elem_t>(dh), P<float>(dW), P<float>(db), B, K, N, s);
-    });
+    }, AccList().r(z, (size_t)B * K * 4).r(dh, (size_t)B * N * es_).w(dW, (size_t)K * N * 4).w(db, (size_t)N * 4).v);
   }
   // loss_out != 0: the 3-loss BCE (gan_loss) runs in the GEMV's last-arriving block
   int gemv_head(std::string name, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int R, int K, int stream,
                 uintptr_t loss_out, uintptr_t dl_d, uintptr_t dl_g, uintptr_t prob, uintptr_t ls) {
     unsigned* ctr = nullptr;
+    AccList acc;
+    acc.r(x, (size_t)R * K * es_).r(w, (size_t)K * 4).r(b, 4).w(out, (size_t)R * 4);
     if (loss_out) {
-      void* c = nullptr;
-      HIPCHECK(hipMalloc(&c, sizeof(unsigned)));
-      HIPCHECK(hipMemset(c, 0, sizeof(unsigned)));
-      dev_allocs_.push_back(c);
-      ctr = reinterpret_cast<unsigned*>(c);
+      ctr = reinterpret_cast<unsigned*>(dev_alloc(sizeof(unsigned), nullptr, true));
+      acc.w((uintptr_t)ctr, 4).w(loss_out, 16).w(dl_d, (size_t)R * 4).w(dl_g, (size_t)R * 2).w(prob, (size_t)R * 4)
+          .r(ls, 12);
     }
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_gemv_head)(P<const elem_t>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, ctr,
                                P<float>(loss_out), P<float>(dl_d), P<float>(dl_g), P<float>(prob), P<const float>(ls),
                                s);
-    });
+    }, acc.v);
   }
   int head_dgrad(std::string name, uintptr_t dl, uintptr_t w, uintptr_t dx, int R, int K, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_head_dgrad)(P<const float>(dl), P<const float>(w), P<elem_t>(dx), R, K, s);
-    });
+    }, AccList().r(dl, (size_t)R * 4).r(w, (size_t)K * 4).w(dx, (size_t)R * K * es_).v);
   }
   int head_wgrad(std::string name, uintptr_t x, uintptr_t dl, uintptr_t part, int R, int K, int splits,
                  uintptr_t dW, uintptr_t db, int stream) {
     add(name, stream, [=](hipStream_t s) {
       return KF(dcg_head_wgrad)(P<const elem_t>(x), P<const float>(dl), P<float>(part), R, K, splits, s);
-    });
+    }, AccList().r(x, (size_t)R * K * es_).r(dl, (size_t)R * 4).w(part, (size_t)splits * K * 4).v);
     add(name + ".reduce", stream, [=](hipStream_t s) {
       return KF(dcg_splitk_reduce)(P<const float>(part), splits, (size_t)K, P<float>(dW), 1.f, s);
-    });
-    return add(name + ".bias", stream, [=](hipStream_t s) { return KF(dcg_sum_vec)(P<const float>(dl), R, P<float>(db), s); });
+    }, AccList().r(part, (size_t)splits * K * 4).w(dW, (size_t)K * 4).v);
+    return add(name + ".bias", stream, [=](hipStream_t s) { return KF(dcg_sum_vec)(P<const float>(dl), R, P<float>(db), s); },
+               AccList().r(dl, (size_t)R * 4).w(db, 4).v);
   }
   int adam(std::string name, uintptr_t w, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers, size_t n, float lr,
            float b1, float b2, float eps, float gscale, int stream) {
@@ -564,23 +610,24 @@ class Program {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_adam)(P<float>(w), P<elem_t>(wbf), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers),
                       n, lr, b1, b2, eps, gscale, P<const float>(ls), s);
-    });
+    }, AccList().w(w, n * 4).w(wbf, n * es_).r(g, n * 4).w(m, n * 4).w(v, n * 4).r(powers, 8).r(ls, 12).v);
   }
   // both TF-Adams (A first) + beta powers / step counter in one launch (see adam2_kernel)
   int adam2(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA, uintptr_t pA,
             size_t nA, float lrA, float b1A, float b2A, float epsA, uintptr_t wD, uintptr_t wbfD, uintptr_t gD,
             uintptr_t mD, uintptr_t vD, uintptr_t pD, size_t nD, float lrD, float b1D, float b2D, float epsD,
             float gscale, uintptr_t step, int stream) {
-    void* ctr = nullptr;
-    HIPCHECK(hipMalloc(&ctr, sizeof(unsigned)));
-    HIPCHECK(hipMemset(ctr, 0, sizeof(unsigned)));
-    dev_allocs_.push_back(ctr);
+    void* ctr = dev_alloc(sizeof(unsigned), nullptr, true);
+    AccList acc;
+    acc.w(wA, nA * 4).w(wbfA, nA * es_).r(gA, nA * 4).w(mA, nA * 4).w(vA, nA * 4).w(pA, 8)
+        .w(wD, nD * 4).w(wbfD, nD * es_).r(gD, nD * 4).w(mD, nD * 4).w(vD, nD * 4).w(pD, 8).w(step, 8)
+        .w((uintptr_t)ctr, 4);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_adam2)(P<float>(wA), P<elem_t>(wbfA), P<const float>(gA), P<float>(mA), P<float>(vA), P<float>(pA),
                            nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD), P<float>(mD),
                            P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, gscale,
                            P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
-    });
+    }, acc.v);
   }
   // TF-SAME stride-2 5x5 conv with 1..4 input and 64 output channels (direct MFMA kernel, conv3.hip)
   int conv3_direct(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int H, int W,
@@ -588,7 +635,8 @@ class Program {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_conv3_direct)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B, H,
                                   W, Cin, Ho, Wo, Cout, pad_y, pad_x, act, leak, s);
-    });
+    }, AccList().r(x, (size_t)B * H * W * Cin * es_).r(w, (size_t)25 * Cin * Cout * es_).r(bias, (size_t)Cout * 4)
+           .w(y, (size_t)B * Ho * Wo * Cout * es_).v);
   }
   // TF-SAME stride-2 5x5 conv_transpose with 1..4 output channels (direct VALU kernel)
   int narrow_deconv(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int Hi, int Wi,
@@ -596,72 +644,110 @@ class Program {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_narrow_deconv)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B, Hi,
                                    Wi, C, Ho, Wo, N, pad, act, leak, s);
-    });
+    }, AccList().r(x, (size_t)B * Hi * Wi * C * es_).r(w, (size_t)25 * N * C * es_).r(bias, (size_t)N * 4)
+           .w(y, (size_t)B * Ho * Wo * N * es_).v);
   }
   // dynamic loss scaling: flag ls[1] if any gradient is non-finite
   int nonfinite_check(std::string name, uintptr_t g, size_t n, uintptr_t ls, int stream) {
-    return add(name, stream, [=](hipStream_t s) { return KF(dcg_nonfinite_check)(P<const float>(g), n, P<float>(ls), s); });
+    return add(name, stream, [=](hipStream_t s) { return KF(dcg_nonfinite_check)(P<const float>(g), n, P<float>(ls), s); },
+               AccList().r(g, n * 4).w(ls, 12).v);
   }
   int step_end(std::string name, uintptr_t pd, uintptr_t pg, float b1d, float b2d, float b1g, float b2g,
                uintptr_t step, int stream, uintptr_t ls, int growth_interval) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_step_end)(P<float>(pd), P<float>(pg), b1d, b2d, b1g, b2g, P<unsigned long long>(step), P<float>(ls),
                           growth_interval, s);
-    });
+    }, AccList().w(pd, 8).w(pg, 8).w(step, 8).w(ls, 12).v);
   }
   int pack(std::string name, uintptr_t src, int T, int A, int Bd, uintptr_t nat, uintptr_t tr, int st, int sb, int sa,
            int stream) {
+    const size_t n = (size_t)T * A * Bd;
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_pack)(P<const float>(src), T, A, Bd, P<elem_t>(nat), P<elem_t>(tr), st, sb, sa, s);
-    });
+    }, AccList().r(src, n * 4).w(nat, n * es_).w(tr, n * es_).v);
   }
   int philox_uniform(std::string name, uintptr_t out, size_t n, uint64_t seed, uintptr_t step, uint64_t stream_id,
                      float lo, float hi, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_philox_uniform)(P<float>(out), n, seed, P<const unsigned long long>(step), stream_id, lo, hi, s);
-    });
+    }, AccList().w(out, n * 4).r(step, 8).v);
   }
   int im2col_s2(std::string name, uintptr_t src, uintptr_t dst, int Bn, int H, int W, int C, int Ho, int Wo, int pl_y,
                 int pl_x, int Kpad, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_im2col_s2)(P<const elem_t>(src), P<elem_t>(dst), Bn, H, W, C, Ho, Wo, pl_y, pl_x, Kpad, s);
-    });
+    }, AccList().r(src, (size_t)Bn * H * W * C * es_).w(dst, (size_t)Bn * Ho * Wo * Kpad * es_).v);
   }
   int cast_to_bf16(std::string name, uintptr_t src, int src_dtype, uintptr_t dst, size_t n, float scale, float shift,
                    int stream) {
+    const size_t ss = src_dtype == 1 ? 8 : src_dtype == 2 ? 1 : 4;
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_cast_to_bf16)(P<const void>(src), src_dtype, P<elem_t>(dst), n, scale, shift, s);
-    });
+    }, AccList().r(src, n * ss).w(dst, n * es_).v);
   }
   int cast_bf16_f32(std::string name, uintptr_t src, uintptr_t dst, size_t n, int stream) {
-    return add(name, stream, [=](hipStream_t s) { return KF(dcg_cast_bf16_f32)(P<const elem_t>(src), P<float>(dst), n, s); });
+    return add(name, stream, [=](hipStream_t s) { return KF(dcg_cast_bf16_f32)(P<const elem_t>(src), P<float>(dst), n, s); },
+               AccList().r(src, n * es_).w(dst, n * 4).v);
   }
   int splitk_reduce(std::string name, uintptr_t src, int splits, size_t n, uintptr_t dst, float scale, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_splitk_reduce)(P<const float>(src), splits, n, P<float>(dst), scale, s);
-    });
+    }, AccList().r(src, (size_t)splits * n * 4).w(dst, n * 4).v);
   }
+  // summary statistics of one tensor (zero fraction + fixed-bucket histogram), see summary.hip
+  int tensor_summary(std::string name, uintptr_t x, int x_dtype, size_t n, uintptr_t edges, int nbins, uintptr_t out,
+                     int stream) {
+    const int blocks = summary_blocks(n);
+    void* part = dev_alloc((size_t)blocks * (nbins + 6) * sizeof(double));
+    void* ctr = dev_alloc(sizeof(unsigned), nullptr, true);
+    const size_t xs = x_dtype == 0 ? 4 : (x_dtype == 3 ? 4 : (size_t)es_);
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_tensor_summary)(P<const void>(x), x_dtype, n, P<const double>(edges), nbins, P<double>(out),
+                                    reinterpret_cast<double*>(part), reinterpret_cast<unsigned*>(ctr), blocks, s);
+    }, AccList().r(x, n * xs).r(edges, (size_t)(nbins - 1) * 8).w(out, (size_t)(nbins + 6) * 8)
+           .w((uintptr_t)part, (size_t)blocks * (nbins + 6) * 8).w((uintptr_t)ctr, 4).v);
+  }
+  static int summary_blocks(size_t n) { return (int)std::max<size_t>(1, std::min<size_t>(256, (n + 8191) / 8192)); }
 
  private:
-  int add(const std::string& name, int stream, std::function<int(hipStream_t)> fn) {
-    ops_.push_back(Op{name, stream, std::move(fn)});
+  int add(const std::string& name, int stream, std::function<int(hipStream_t)> fn, std::vector<Acc> acc,
+          int kind = OP_LAUNCH, int ev = -1) {
+    ops_.push_back(Op{name, stream, kind, ev, std::move(acc), std::move(fn)});
     return (int)ops_.size() - 1;
+  }
+  // device allocation owned by the program (optionally initialised from host / zeroed); a dry
+  // program hands out disjoint fake addresses above any real one
+  void* dev_alloc(size_t bytes, const void* init = nullptr, bool zero = false) {
+    if (dry_) {  // process-wide counter: fake ranges of different programs never overlap
+      static uintptr_t fake_next = (uintptr_t)1 << 60;
+      const uintptr_t p = fake_next;
+      fake_next += (bytes + 255) / 256 * 256 + 256;
+      return reinterpret_cast<void*>(p);
+    }
+    void* p = nullptr;
+    HIPCHECK(hipMalloc(&p, bytes));
+    if (init) HIPCHECK(hipMemcpy(p, init, bytes, hipMemcpyHostToDevice));
+    if (zero) HIPCHECK(hipMemset(p, 0, bytes));
+    dev_allocs_.push_back(p);
+    return p;
   }
   std::vector<Op> ops_;
   std::vector<void*> dev_allocs_;
   std::vector<hipEvent_t> events_;
   int last_mtiles_ = 0, last_nphases_ = 0;
-  bool f16_ = false;  // element type of every activation / weight-mirror pointer: fp16, else bf16
+  int dt_ = 0;       // element type of every activation / weight-mirror pointer
+  size_t es_ = 2;    // its size in bytes
+  bool dry_ = false;
 };
 
-static py::tuple igemm_tile(int cfg) {
-  if (cfg >= 200) {
-    int bm, bn, ns;
-    if (dcg_igemm3_tile(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad cfg");
-    return py::make_tuple(bm, bn);
-  }
-  int bm = 0, bn = 0;
-  if (dcg_igemm_tile(cfg, &bm, &bn)) throw std::runtime_error("bad cfg");
+static py::tuple igemm_tile(int cfg, int dtype) {
+  int bm = 0, bn = 0, ns = 0;
+  int rc;
+#define DT(fn) (dtype == 2 ? fn##_f32 : dtype == 1 ? fn##_f16 : fn)
+  if (cfg >= 200) rc = DT(dcg_igemm3_tile)(cfg, &bm, &bn, &ns);
+  else rc = DT(dcg_igemm_tile)(cfg, &bm, &bn);
+#undef DT
+  if (rc) throw std::runtime_error("bad cfg");
   return py::make_tuple(bm, bn);
 }
 static py::tuple wgrad_tile(int cfg) {
@@ -684,15 +770,22 @@ static std::string device_arch() {
 
 PYBIND11_MODULE(_dcgan_hip, m) {
   m.doc() = "gfx950 (MI355X) kernel library + recorded launch programs for the DCGAN framework";
-  m.def("igemm_tile", &igemm_tile);
+  m.def("igemm_tile", &igemm_tile, py::arg("cfg"), py::arg("dtype") = 0);
   m.def("wgrad_tile", &wgrad_tile);
   m.def("device_arch", &device_arch);
   m.attr("built_for") = "gfx950";
+  m.attr("OP_LAUNCH") = (int)OP_LAUNCH;
+  m.attr("OP_RECORD") = (int)OP_RECORD;
+  m.attr("OP_WAIT") = (int)OP_WAIT;
   py::class_<Program>(m, "Program")
-      .def(py::init<bool>(), py::arg("f16") = false)
+      .def(py::init<int, bool>(), py::arg("dtype") = 0, py::arg("dry") = false)
       .def_property_readonly("f16", &Program::f16)
+      .def_property_readonly("dtype", &Program::dtype)
+      .def_property_readonly("dry", &Program::dry)
+      .def_property_readonly("elem_size", &Program::elem_size)
       .def("size", &Program::size)
       .def("name", &Program::name)
+      .def("op_info", &Program::op_info)
       .def("run", &Program::run, py::arg("streams"), py::arg("begin") = 0, py::arg("end") = -1)
       .def("new_event", &Program::new_event)
       .def("record", &Program::record)
@@ -713,7 +806,9 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("wgrad3", &Program::wgrad3)
       .def("colstats", &Program::colstats)
       .def("bn_finalize", &Program::bn_finalize)
-      .def("bn_coef_eval", &Program::bn_coef_eval)
+      .def("bn_coef_eval", &Program::bn_coef_eval, py::arg("name"), py::arg("C"), py::arg("gamma"), py::arg("beta"),
+           py::arg("eps"), py::arg("mean"), py::arg("var"), py::arg("debias"), py::arg("scale"), py::arg("shift"),
+           py::arg("stream"), py::arg("debias_ptr") = 0)
       .def("bn_apply_act", &Program::bn_apply_act)
       .def("bn_bwd_finalize", &Program::bn_bwd_finalize)
       .def("bn_bwd_apply", &Program::bn_bwd_apply)
@@ -752,5 +847,6 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("im2col_s2", &Program::im2col_s2)
       .def("cast_to_bf16", &Program::cast_to_bf16)
       .def("cast_bf16_f32", &Program::cast_bf16_f32)
-      .def("splitk_reduce", &Program::splitk_reduce);
+      .def("splitk_reduce", &Program::splitk_reduce)
+      .def("tensor_summary", &Program::tensor_summary);
 }

@@ -48,6 +48,18 @@ def _run(cmd):
     return r.stdout
 
 
+VARIANTS = {"bf16": ("", []), "f16": (".f16", ["-DDCG_F16"]), "f32": (".f32", ["-DDCG_F32"])}
+
+
+def _variants(path: str):
+    """Element-type builds of one kernel file from its first line ``// dcg-variants: bf16 f16 f32``
+    (bf16 = default symbols, fp16 = ``*_f16``, fp32 = ``*_f32``); files without the line get all."""
+    with open(path) as f:
+        first = f.readline()
+    names = first.split(":", 1)[1].split() if first.startswith("// dcg-variants:") else list(VARIANTS)
+    return [VARIANTS[n] for n in names]
+
+
 def build_hip(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(CSRC, "hip", h) for h in os.listdir(os.path.join(CSRC, "hip"))
@@ -56,8 +68,8 @@ def build_hip(verbose: bool = False, jobs: int = 8) -> str:
     common = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC]
     jobs_list = []
     objs = []
-    for s in srcs:  # every kernel file twice: bf16 element type, and fp16 (-DDCG_F16, *_f16 symbols)
-        for tag, defs in (("", []), (".f16", ["-DDCG_F16"])):
+    for s in srcs:  # every kernel file once per element type it declares (`// dcg-variants:`)
+        for tag, defs in _variants(s):
             o = os.path.join(BUILD, os.path.basename(s) + tag + ".o")
             objs.append(o)
             if _newer([s] + hdrs, o):

@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16 f32
 // BatchNorm (TF batch_norm_with_global_normalization semantics) and
 // activation kernels for gfx950, NHWC elem_t activations, fp32 statistics.
 //
@@ -18,8 +19,7 @@
 namespace dcg {
 
 __device__ __forceinline__ void load8(const elem_t* p, float* f) {
-  const u32x4 v = *reinterpret_cast<const u32x4*>(p);
-  const elem8 b = __builtin_bit_cast(elem8, v);
+  const elem8 b = ld8(p);
 #pragma unroll
   for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
 }
@@ -28,7 +28,7 @@ __device__ __forceinline__ void store8(elem_t* p, const float* f) {
   elem8 b;
 #pragma unroll
   for (int i = 0; i < 8; ++i) b[i] = (elem_t)f[i];
-  *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, b);
+  st8(p, b);
 }
 
 __device__ __forceinline__ void load8f(const float* p, float* f) {
@@ -197,11 +197,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 }
 
 // inference-mode BN coefficients from moving averages (sampler, distriubted_model.py:46-47)
+// debias_ptr (optional): TF zero-debiasing factor 1 / (1 - decay^t), written by the host before
+// the sampler program runs (the recorded program keeps the pointer, not the value)
 __global__ void bn_coef_eval_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
                                     float eps, const float* __restrict__ mean, const float* __restrict__ var,
-                                    float debias, float* __restrict__ scale_out, float* __restrict__ shift_out) {
+                                    float debias, const float* __restrict__ debias_ptr, float* __restrict__ scale_out,
+                                    float* __restrict__ shift_out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  if (debias_ptr) debias = debias_ptr[0];
   const float m = mean[c] * debias, v = var[c] * debias;
   const float sc = gamma[c] * rsqrtf(v + eps);
   scale_out[c] = sc;
@@ -292,32 +296,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const elem_t* __restr
 // sums with `sc1` stores, and the workgroup that arrives last (agent-scope counter, reset for
 // the next launch / graph replay) combines the PS slices in slice order -- deterministic -- and
 // runs the finalize. ws: [groups][PS][2][C] doubles; counters: zero-initialised.
-__device__ __forceinline__ void st_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 16);
-}
-__device__ __forceinline__ double ld_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
-}
-__device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 16);
-}
-__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
-}
-
-// returns true in the last-arriving workgroup of `expected`; every thread of the block agrees
-__device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned expected, int* flag_lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag_lds = old == expected - 1;
-    if (*flag_lds) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  return *flag_lds != 0;
-}
-
 // sum of the PS slice rows of group g, column c (and C + c), in slice order; 8 slices' loads in
 // flight at a time (a plain loop waited on every `sc1` load: ~60 dependent L2 round trips)
 __device__ __forceinline__ void slice_sums(__amdgpu_buffer_rsrc_t rw, int g, int PS, int C, int c, double& a,
@@ -448,132 +426,6 @@ __global__ __launch_bounds__(256) void sum_partials_split_kernel(const float* __
   dst[c] = a;
 }
 
-// ---------------------------------------------------------------- row-wide finalizes (v2)
-// Same math as the split finalizes above, different reduction layout: a workgroup owns a slice
-// of partial ROWS and all 2C columns of them (16-byte loads along the row; 256 / (C/2) rows in
-// flight per pass), instead of 16 channels x a slice (64-byte row segments). Per-thread double
-// accumulators, a fixed-order LDS tree over the row lanes, one double row per slice in ws
-// (`sc1` stores); the last-arriving slice (agent counter, re-armed) combines the slices in
-// slice order and runs the finalize for every channel. grid = (PS, groups).
-//   MODE 0: BN forward  -- mean / rstd / scale / shift (+ EMA) per group; counter per group.
-//   MODE 1: BN backward -- per-group coefficients + dgamma / dbeta summed over the groups;
-//           one counter for all (PS x groups) workgroups.
-template <int MODE>
-__global__ __launch_bounds__(256) void bn_finalize_rows_kernel(
-    const float* __restrict__ part, int ppg, int groups, int C, double count, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, float* __restrict__ mean_io, float* __restrict__ rstd_io,
-    float* __restrict__ scale_out, float* __restrict__ shift_out, float* __restrict__ ema_mean,
-    float* __restrict__ ema_var, float decay, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ coef, double* ws, unsigned* counters) {
-  __shared__ double red[1024];
-  __shared__ int flag;
-  const int PS = gridDim.x, ps = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
-  const int V4 = C >> 1;  // float4 columns of a partial row [2][C]
-  const int chunk = (ppg + PS - 1) / PS;
-  const int p0 = g * ppg + ps * chunk, p1 = min(g * ppg + ppg, p0 + chunk);
-  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ws, (uint32_t)((size_t)groups * PS * 2 * C * 8));
-  const size_t wrow = ((size_t)g * PS + ps) * 2 * C;
-  if (V4 <= 256) {
-    const int lanes = 256 / V4, c4 = tid % V4, ln = tid / V4;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    if (ln < lanes) {
-      int p = p0 + ln;
-      for (; p + 3 * lanes < p1; p += 4 * lanes) {  // 4 rows in flight
-        f32x4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(part + (size_t)(p + u * lanes) * 2 * C + 4 * c4);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
-      }
-      for (; p < p1; p += lanes) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(part + (size_t)p * 2 * C + 4 * c4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) red[ln * 2 * C + 4 * c4 + e] = a[e];
-    }
-    __syncthreads();
-    int nl = lanes;
-    if ((lanes & (lanes - 1)) == 0) {
-      for (int h = lanes / 2; h > 0; h >>= 1) {
-        for (int q = tid; q < h * 2 * C; q += 256) red[q] += red[q + h * 2 * C];
-        __syncthreads();
-      }
-      nl = 1;
-    }
-    for (int col = tid; col < 2 * C; col += 256) {
-      double t = 0.0;
-      for (int l = 0; l < nl; ++l) t += red[l * 2 * C + col];
-      st_sc1_f64(rw, (uint32_t)((wrow + col) * 8), t);
-    }
-  } else {  // wide rows (C > 512): one row lane, 256-column passes
-    for (int c4 = tid; c4 < V4; c4 += 256) {
-      double a[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int p = p0; p < p1; ++p) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(part + (size_t)p * 2 * C + 4 * c4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) st_sc1_f64(rw, (uint32_t)((wrow + 4 * c4 + e) * 8), a[e]);
-    }
-  }
-  if (MODE == 0) {
-    if (!last_arrival(counters + g, (unsigned)PS, &flag)) return;
-    for (int c = tid; c < C; c += 256) {
-      double a = 0.0, b = 0.0;
-      for (int q = 0; q < PS; ++q) {
-        a += ld_sc1_f64(rw, (uint32_t)(((((size_t)g * PS + q) * 2 + 0) * C + c) * 8));
-        b += ld_sc1_f64(rw, (uint32_t)(((((size_t)g * PS + q) * 2 + 1) * C + c) * 8));
-      }
-      const int idx = g * C + c;
-      const double m = a / count;
-      double v = b / count - m * m;
-      if (v < 0.0) v = 0.0;
-      const float mf = (float)m, vf = (float)v;
-      const float r = rsqrtf(vf + eps);
-      mean_io[idx] = mf;
-      rstd_io[idx] = r;
-      const float sc = gamma[c] * r;
-      scale_out[idx] = sc;
-      shift_out[idx] = beta[c] - mf * sc;
-      if (ema_mean) {  // TF ExponentialMovingAverage: shadow -= (1 - decay) * (shadow - value)
-        const float al = 1.f - decay;
-        ema_mean[idx] -= al * (ema_mean[idx] - mf);
-        ema_var[idx] -= al * (ema_var[idx] - vf);
-      }
-    }
-  } else {
-    if (!last_arrival(counters, (unsigned)(PS * groups), &flag)) return;
-    const float cnt = (float)count;
-    for (int c = tid; c < C; c += 256) {
-      float dg = 0.f, db = 0.f;
-      for (int gg = 0; gg < groups; ++gg) {
-        double a = 0.0, b = 0.0;
-        for (int q = 0; q < PS; ++q) {
-          a += ld_sc1_f64(rw, (uint32_t)(((((size_t)gg * PS + q) * 2 + 0) * C + c) * 8));
-          b += ld_sc1_f64(rw, (uint32_t)(((((size_t)gg * PS + q) * 2 + 1) * C + c) * 8));
-        }
-        const float sg1 = (float)a, sg2 = (float)b;
-        dg += sg2;
-        db += sg1;
-        const float r = rstd_io[gg * C + c], mu = mean_io[gg * C + c];
-        const float A = gamma[c] * r;
-        const float c2 = -A * sg2 / cnt;
-        const float bb = -A * sg1 / cnt;
-        coef[(gg * 3 + 0) * C + c] = A;
-        coef[(gg * 3 + 1) * C + c] = c2 * r;
-        coef[(gg * 3 + 2) * C + c] = bb - c2 * mu * r;
-      }
-      if (dgamma) dgamma[c] = dg;
-      if (dbeta) dbeta[c] = db;
-    }
-  }
-}
-
 // ---------------------------------------------------------------- activation backward (no BN)
 // dx = dy * act'(y); 8 per thread + scalar tail
 __global__ __launch_bounds__(256) void act_bwd_kernel(const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
@@ -643,26 +495,26 @@ __global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __rest
     if (rl < RL) {
       // 4 rows per iteration, all loads issued before any use (memory-level parallelism)
       for (int rb = r0 + rl; rb < r1; rb += 4 * RL) {
-        u32x4 dvv[4], yvv[4];
+        elem8 dvv[4], yvv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int r = rb + u * RL;
           const size_t o = (size_t)(r < r1 ? r : r0) * C + 8 * c;
-          dvv[u] = *reinterpret_cast<const u32x4*>(dy + o);
-          yvv[u] = *reinterpret_cast<const u32x4*>(y + o);
+          dvv[u] = ld8(dy + o);
+          yvv[u] = ld8(y + o);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int r = rb + u * RL;
           if (r >= r1) break;
-          const elem8 dv = __builtin_bit_cast(elem8, dvv[u]), yv = __builtin_bit_cast(elem8, yvv[u]);
+          const elem8 dv = dvv[u], yv = yvv[u];
           elem8 out;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             out[i] = f2bf((float)dv[i] * act_grad_from_out((float)yv[i], act, leak));
             s[i] += (float)out[i];
           }
-          *reinterpret_cast<u32x4*>(dx + (size_t)r * C + 8 * c) = __builtin_bit_cast(u32x4, out);
+          st8(dx + (size_t)r * C + 8 * c, out);
         }
       }
 #pragma unroll
@@ -684,12 +536,12 @@ __global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __rest
     // full 8-element chunks: 2 per iteration, loads first; the scalar tail after
     const uint32_t nfull = (uint32_t)((min(e1, n & ~(size_t)7) - min(e0, n & ~(size_t)7)) / 8);
     for (uint32_t q0 = tid; q0 < nfull; q0 += 2 * 256) {
-      u32x4 dvv[2], yvv[2];
+      elem8 dvv[2], yvv[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const uint32_t q = q0 + u * 256 < nfull ? q0 + u * 256 : q0;
-        dvv[u] = *reinterpret_cast<const u32x4*>(dy + e0 + 8 * (size_t)q);
-        yvv[u] = *reinterpret_cast<const u32x4*>(y + e0 + 8 * (size_t)q);
+        dvv[u] = ld8(dy + e0 + 8 * (size_t)q);
+        yvv[u] = ld8(y + e0 + 8 * (size_t)q);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -697,7 +549,7 @@ __global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __rest
         if (q >= nfull) break;
         const size_t e = e0 + 8 * (size_t)q;
         int ch = (int)((uint32_t)(e % CC));
-        const elem8 dv = __builtin_bit_cast(elem8, dvv[u]), yv = __builtin_bit_cast(elem8, yvv[u]);
+        const elem8 dv = dvv[u], yv = yvv[u];
         elem8 out;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -707,7 +559,7 @@ __global__ __launch_bounds__(256) void act_bwd_dbias_kernel(const elem_t* __rest
           for (int k = 0; k < CC; ++k) s[k] += ch == k ? v : 0.f;
           ch = ch == CC - 1 ? 0 : ch + 1;
         }
-        *reinterpret_cast<u32x4*>(dx + e) = __builtin_bit_cast(u32x4, out);
+        st8(dx + e, out);
       }
     }
     for (size_t e = e0 + 8 * (size_t)nfull + tid; e < e1; e += 256) {  // tail (< 8 elements)
@@ -795,9 +647,10 @@ extern "C" int DCG_API(dcg_bn_finalize)(const float* part, int ppg, int groups, 
 }
 
 extern "C" int DCG_API(dcg_bn_coef_eval)(int C, const float* gamma, const float* beta, float eps, const float* mean,
-                                const float* var, float debias, float* scale, float* shift, hipStream_t s) {
+                                const float* var, float debias, const float* debias_ptr, float* scale, float* shift,
+                                hipStream_t s) {
   hipLaunchKernelGGL(bn_coef_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, eps, mean, var,
-                     debias, scale, shift);
+                     debias, debias_ptr, scale, shift);
   return (int)hipGetLastError();
 }
 
@@ -892,22 +745,6 @@ extern "C" int DCG_API(dcg_act_bwd_dbias)(const elem_t* dy, const elem_t* y, ele
   } else {
     return -2;
   }
-  return (int)hipGetLastError();
-}
-
-extern "C" int DCG_API(dcg_bn_finalize_rows)(int mode, const float* part, int ppg, int groups, int C, double count,
-                                             const float* gamma, const float* beta, float eps, float* mean, float* rstd,
-                                             float* scale, float* shift, float* ema_mean, float* ema_var, float decay,
-                                             float* dgamma, float* dbeta, float* coef, double* ws, unsigned* counters,
-                                             int PS, hipStream_t s) {
-  if (C % 2 || (C / 2 <= 256 && 2 * C * (256 / (C / 2)) > 1024)) return -2;
-  const dim3 grid(PS, groups);
-  if (mode == 0)
-    hipLaunchKernelGGL(bn_finalize_rows_kernel<0>, grid, dim3(256), 0, s, part, ppg, groups, C, count, gamma, beta, eps,
-                       mean, rstd, scale, shift, ema_mean, ema_var, decay, dgamma, dbeta, coef, ws, counters);
-  else
-    hipLaunchKernelGGL(bn_finalize_rows_kernel<1>, grid, dim3(256), 0, s, part, ppg, groups, C, count, gamma, beta, eps,
-                       mean, rstd, scale, shift, ema_mean, ema_var, decay, dgamma, dbeta, coef, ws, counters);
   return (int)hipGetLastError();
 }
 

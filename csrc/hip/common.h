@@ -1,11 +1,12 @@
 // Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels of this framework.
 //
-// Element type: every kernel file is compiled TWICE by csrc/build.py -- once with elem_t =
-// bf16 (the default training dtype) and once with -DDCG_F16, elem_t = fp16 (the 256x256 fp16
-// config, with dynamic loss scaling in the engine). The fp16 build lives in namespace dcg_f16
-// and its C launchers carry a `_f16` suffix (DCG_API), so both coexist in one .so and the
-// Program picks one set per engine. MFMA: v_mfma_f32_16x16x32_{bf16,f16} (same lane maps,
-// same cycles).
+// Element type: every kernel file is compiled once per element type it declares
+// (`// dcg-variants:` line, csrc/build.py): elem_t = bf16 (the default training dtype), fp16
+// (-DDCG_F16: the 256x256 fp16 config, dynamic loss scaling in the engine) and fp32 (-DDCG_F32:
+// the reference precision). Each build lives in its own namespace (dcg, dcg_f16, dcg_f32) and
+// its C launchers carry a suffix (DCG_API: none, `_f16`, `_f32`), so all coexist in one .so and
+// the Program picks one set per engine. 16-bit MFMA: v_mfma_f32_16x16x32_{bf16,f16} (same lane
+// maps, same cycles); fp32: v_mfma_f32_16x16x4_f32 (igemm_f32.hip).
 // Wave = 64 lanes. 16x16x32 MFMA fragment lane maps:
 //   A: lane l holds A[row l&15][k = 8*(l>>4) + j], j = 0..7
 //   B: lane l holds B[k = 8*(l>>4) + j][col l&15]
@@ -14,7 +15,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifdef DCG_F16
+#if defined(DCG_F32)
+// reference-precision build: fp32 activations / weight mirrors, fp32-input MFMA
+// (v_mfma_f32_16x16x4_f32, exact f32 fma chains) in igemm_f32.hip
+typedef float elem_t;
+typedef float elem8 __attribute__((ext_vector_type(8)));
+typedef float elem4 __attribute__((ext_vector_type(4)));
+typedef float elem2 __attribute__((ext_vector_type(2)));
+#define DCG_API(name) name##_f32
+#define dcg dcg_f32
+#elif defined(DCG_F16)
 typedef _Float16 elem_t;
 typedef _Float16 elem8 __attribute__((ext_vector_type(8)));
 typedef _Float16 elem4 __attribute__((ext_vector_type(4)));
@@ -42,6 +52,24 @@ namespace dcg {
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
 
 __device__ __forceinline__ float bf2f(elem_t x) { return (float)x; }
+
+// 8 consecutive elements (16 bytes for 16-bit types, 32 for fp32: two 16-byte accesses)
+__device__ __forceinline__ elem8 ld8(const elem_t* p) {
+#if defined(DCG_F32)
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  return (elem8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+#else
+  return __builtin_bit_cast(elem8, *reinterpret_cast<const u32x4*>(p));
+#endif
+}
+__device__ __forceinline__ void st8(elem_t* p, elem8 v) {
+#if defined(DCG_F32)
+  *reinterpret_cast<f32x4*>(p) = (f32x4){v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+#else
+  *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, v);
+#endif
+}
 __device__ __forceinline__ elem_t f2bf(float x) { return (elem_t)x; }
 
 __device__ __forceinline__ float apply_act(float v, int act, float leak) {
@@ -115,6 +143,33 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// ---- cross-workgroup hand-off helpers (sc1 = write-through / L1-bypassing buffer accesses)
+__device__ __forceinline__ void st_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 16);
+}
+__device__ __forceinline__ double ld_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+}
+__device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 16);
+}
+__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+
+// returns true in the last-arriving workgroup of `expected`; every thread of the block agrees
+__device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned expected, int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = old == expected - 1;
+    if (*flag_lds) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return *flag_lds != 0;
 }
 
 }  // namespace dcg

@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16
 // Direct MFMA convolution for the narrow-INPUT stride-2 5x5 TF-SAME conv: D layer 0 (RGB / gray
 // image -> 64 channels, + bias + LeakyReLU). The im2col + GEMM pair it replaces on the forward
 // path wrote and re-read a [rows][80] column matrix (2 x 42 MB at 64x64, 2B = 256) for a GEMM

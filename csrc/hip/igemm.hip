@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16
 // Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC, elem_t in / fp32 acc.
 //
 // One kernel family covers every conv-shaped op of the DCGAN step:

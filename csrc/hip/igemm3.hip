@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16
 // Implicit-GEMM convolution, version 3: big wave tiles + deep LDS-DMA pipeline + in-kernel
 // deterministic split-K + either weight layout. Same conv/deconv/plain semantics and fused
 // epilogue as igemm.hip (read that header first); what changes is how the K loop is fed.

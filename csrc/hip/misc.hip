@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16 f32
 // Small fused kernels of the DCGAN step for gfx950:
 //   * BCE-with-logits, all 3 reference losses + both logit gradients in ONE kernel (K15/K16)
 //   * linear layers: G projection z->h0 (K1), its weight gradient (K2), D's 1-output head
@@ -238,19 +239,19 @@ __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict
   const float* wr = w + wave * kq;
   float s = 0.f;
   for (int k0 = lane * 8; k0 < kq; k0 += 4 * 512) {
-    u32x4 xv[4];
+    elem8 xv[4];
     f32x4 w0[4], w1[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = k0 + u * 512 < kq ? k0 + u * 512 : k0;
-      xv[u] = *reinterpret_cast<const u32x4*>(xr + k);
+      xv[u] = ld8(xr + k);
       w0[u] = *reinterpret_cast<const f32x4*>(wr + k);
       w1[u] = *reinterpret_cast<const f32x4*>(wr + k + 4);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (k0 + u * 512 >= kq) break;
-      const elem8 xb = __builtin_bit_cast(elem8, xv[u]);
+      const elem8 xb = xv[u];
       s += (float)xb[0] * w0[u][0] + (float)xb[1] * w0[u][1] + (float)xb[2] * w0[u][2] + (float)xb[3] * w0[u][3] +
            (float)xb[4] * w1[u][0] + (float)xb[5] * w1[u][1] + (float)xb[6] * w1[u][2] + (float)xb[7] * w1[u][3];
     }
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(256) void head_dgrad_kernel(const float* __restrict
     elem8 o;
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (elem_t)(g * w[k + i]);
-    *reinterpret_cast<u32x4*>(dx + e) = __builtin_bit_cast(u32x4, o);
+    st8(dx + e, o);
   }
 }
 
@@ -309,8 +310,7 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const elem_t* __restric
   const int r0 = split * rows_per_split, r1 = min(R, r0 + rows_per_split);
   for (int r = r0; r < r1; ++r) {
     const float g = dl[r];
-    const u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)r * K + k8 * 8);
-    const elem8 xb = __builtin_bit_cast(elem8, v);
+    const elem8 xb = ld8(x + (size_t)r * K + k8 * 8);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] += (float)xb[i] * g;
   }
@@ -370,16 +370,16 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
   const float slope = act == ACT_LRELU ? leak : 0.f;
   if (kok) {
     for (int rb = rl; rb < R; rb += 4 * 32) {  // 4 rows per iteration, loads first
-      u32x4 xv[4], yv[4], xb[4];
+      elem8 xv[4], yv[4], xb[4];
       float gv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = rb + 32 * u < R ? rb + 32 * u : rb;
         const size_t o = (size_t)r * K + k;
-        xv[u] = xa ? *reinterpret_cast<const u32x4*>(xa + o) : u32x4{0, 0, 0, 0};
+        xv[u] = xa ? ld8(xa + o) : (elem8)(elem_t)0.f;
         if (stats) {
-          yv[u] = *reinterpret_cast<const u32x4*>(by + o);
-          xb[u] = *reinterpret_cast<const u32x4*>(bx + o);
+          yv[u] = ld8(by + o);
+          xb[u] = ld8(bx + o);
         }
         gv[u] = dl[r];
       }
@@ -388,16 +388,16 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
         const int r = rb + 32 * u;
         if (r >= R) break;
         const int grp = r >= rpg ? 1 : 0;
-        const elem8 xe = __builtin_bit_cast(elem8, xv[u]);
+        const elem8 xe = xv[u];
         elem8 ob;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           s[i] += (float)xe[i] * gv[u];
           ob[i] = (elem_t)(gv[u] * wv[i]);
         }
-        *reinterpret_cast<u32x4*>(dx + (size_t)r * K + k) = __builtin_bit_cast(u32x4, ob);
+        st8(dx + (size_t)r * K + k, ob);
         if (stats) {
-          const elem8 ye = __builtin_bit_cast(elem8, yv[u]), be = __builtin_bit_cast(elem8, xb[u]);
+          const elem8 ye = yv[u], be = xb[u];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float g = (float)ob[i] * ((float)ye[i] > 0.f ? 1.f : slope);
@@ -690,7 +690,7 @@ __global__ __launch_bounds__(256) void im2col_s2_kernel(const elem_t* __restrict
       }
       o[j] = val;
     }
-    *reinterpret_cast<u32x4*>(drow + (size_t)q * 8) = __builtin_bit_cast(u32x4, o);
+    st8(drow + (size_t)q * 8, o);
   }
 }
 
@@ -708,6 +708,47 @@ __global__ __launch_bounds__(256) void cast_u8_bf16_kernel(const uint8_t* __rest
 }
 __global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const elem_t* __restrict__ s, float* __restrict__ d, size_t n) {
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) d[i] = (float)s[i];
+}
+
+// sum of `splits` fp32 slabs of `n` elements -> dst (scaled). Block = (256/L) float4 columns x L
+// split lanes; each lane sums every L-th slab, then the L partial sums are combined in LDS in a
+// fixed order (deterministic). Handles the few-elements / many-slabs shape of small wgrads.
+template <int L>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* src, int splits, size_t n,
+                                                            float* dst, float scale) {
+  constexpr int COLS = 256 / L;
+  __shared__ f32x4 red[L][COLS];
+  const int col = threadIdx.x % COLS, lane = threadIdx.x / COLS;
+  const size_t n4 = n / 4;
+  const size_t i = (size_t)blockIdx.x * COLS + col;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    auto slab = [&](int k) { return reinterpret_cast<const f32x4*>(src + (size_t)k * n)[i]; };
+    int k = lane;
+    for (; k + 3 * L < splits; k += 4 * L) {  // 4 slabs in flight per lane, summed in slab order
+      const f32x4 a = slab(k), b = slab(k + L), c = slab(k + 2 * L), d = slab(k + 3 * L);
+      s += a;
+      s += b;
+      s += c;
+      s += d;
+    }
+    for (; k < splits; k += L) s += slab(k);
+  }
+  red[lane][col] = s;
+  __syncthreads();
+  if (lane == 0 && i < n4) {
+    f32x4 t = red[0][col];
+#pragma unroll
+    for (int l = 1; l < L; ++l) t += red[l][col];
+    reinterpret_cast<f32x4*>(dst)[i] = t * scale;
+  }
+  // scalar tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (int)(n - n4 * 4)) {
+    const size_t j = n4 * 4 + threadIdx.x;
+    float t = 0.f;
+    for (int k = 0; k < splits; ++k) t += src[(size_t)k * n + j];
+    dst[j] = t * scale;
+  }
 }
 
 }  // namespace dcg
@@ -877,5 +918,20 @@ extern "C" int DCG_API(dcg_adam2)(float* wA, elem_t* wbfA, const float* gA, floa
   unsigned blocksD = (unsigned)std::max<size_t>(1, 512 - std::min<size_t>(511, blocksA));
   hipLaunchKernelGGL(dcg::adam2_kernel, dim3(blocksA + blocksD), dim3(256), 0, s, A, D, gscale, step, counter,
                      blocksA);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_splitk_reduce)(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s) {
+  const size_t n4 = n / 4;
+  if (splits >= 64) {
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  } else if (splits >= 8) {
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  } else {
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  }
   return (int)hipGetLastError();
 }

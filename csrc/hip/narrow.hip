@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16
 // Narrow-output TF-SAME stride-2 5x5 conv_transpose (N = 1..4 output channels), direct on VALU:
 // the two 3-channel GEMMs of the step -- G's last layer (64 -> 3, + bias + tanh) and D layer 0's
 // data gradient for the fake half (64 -> 3) -- where an MFMA tile pads N=3 to 16 (5x waste;

@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16
 // Weight-gradient ("wgrad") for the TF-'SAME' stride-2 5x5 conv and
 // conv_transpose on CDNA4 MFMA, NHWC, elem_t in / fp32 out.
 //
@@ -175,47 +176,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     }
 }
 
-// sum of `splits` fp32 slabs of `n` elements -> dst (scaled). Block = (256/L) float4 columns x L
-// split lanes; each lane sums every L-th slab, then the L partial sums are combined in LDS in a
-// fixed order (deterministic). Handles the few-elements / many-slabs shape of small wgrads.
-template <int L>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* src, int splits, size_t n,
-                                                            float* dst, float scale) {
-  constexpr int COLS = 256 / L;
-  __shared__ f32x4 red[L][COLS];
-  const int col = threadIdx.x % COLS, lane = threadIdx.x / COLS;
-  const size_t n4 = n / 4;
-  const size_t i = (size_t)blockIdx.x * COLS + col;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (i < n4) {
-    auto slab = [&](int k) { return reinterpret_cast<const f32x4*>(src + (size_t)k * n)[i]; };
-    int k = lane;
-    for (; k + 3 * L < splits; k += 4 * L) {  // 4 slabs in flight per lane, summed in slab order
-      const f32x4 a = slab(k), b = slab(k + L), c = slab(k + 2 * L), d = slab(k + 3 * L);
-      s += a;
-      s += b;
-      s += c;
-      s += d;
-    }
-    for (; k < splits; k += L) s += slab(k);
-  }
-  red[lane][col] = s;
-  __syncthreads();
-  if (lane == 0 && i < n4) {
-    f32x4 t = red[0][col];
-#pragma unroll
-    for (int l = 1; l < L; ++l) t += red[l][col];
-    reinterpret_cast<f32x4*>(dst)[i] = t * scale;
-  }
-  // scalar tail (n % 4)
-  if (blockIdx.x == 0 && threadIdx.x < (int)(n - n4 * 4)) {
-    const size_t j = n4 * 4 + threadIdx.x;
-    float t = 0.f;
-    for (int k = 0; k < splits; ++k) t += src[(size_t)k * n + j];
-    dst[j] = t * scale;
-  }
-}
-
 }  // namespace dcg
 
 #define DCG_WGRAD_CONFIGS(X) \
@@ -241,17 +201,3 @@ extern "C" int DCG_API(dcg_wgrad_launch)(const dcg::WGradArgs* a, int cfg, int s
   return -1;
 }
 
-extern "C" int DCG_API(dcg_splitk_reduce)(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s) {
-  const size_t n4 = n / 4;
-  if (splits >= 64) {
-    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16 + 1)), dim3(256), 0, s, src,
-                       splits, n, dst, scale);
-  } else if (splits >= 8) {
-    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64 + 1)), dim3(256), 0, s, src,
-                       splits, n, dst, scale);
-  } else {
-    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256 + 1)), dim3(256), 0, s, src,
-                       splits, n, dst, scale);
-  }
-  return (int)hipGetLastError();
-}

@@ -1,3 +1,4 @@
+// dcg-variants: bf16 f16
 // Weight gradient, version 3: the igemm3.hip recipe (LDS-DMA multi-stage pipeline, 64x64 wave
 // tiles, XCD-aware tile order, in-kernel deterministic split-K) applied to wgrad.hip's problem.
 //

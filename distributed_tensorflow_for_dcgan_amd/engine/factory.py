@@ -1,4 +1,5 @@
-"""Engine selection: the fused HIP engine on an MI355X, the reference engine elsewhere.
+"""Engine selection: the fused HIP engine on an MI355X (bf16, fp16 or fp32), the reference
+(PyTorch autograd) engine on the CPU or when asked for explicitly.
 
 Both expose the same small interface used by the trainer and ``bench.py``:
 ``set_synthetic_batch(real)``, ``set_batch(real)``, ``train_step()``, ``last_losses()``,
@@ -116,8 +117,8 @@ def build_engine(cfg: DCGANConfig, batch_size: int, device: torch.device, engine
                  dtype: str = "bf16", seed: int = 0, rank: int = 0, world: int = 1, graph: bool = True,
                  allreduce_dtype: str = "fp32", lr: float = 2e-4, beta1: float = 0.5,
                  zero_debias: bool = False, bucket_mb: float = 32.0):
-    if engine == "auto":
-        engine = "hip" if device.type == "cuda" and dtype in ("bf16", "fp16") else "reference"
+    if engine == "auto":  # every dtype (bf16 / fp16 / fp32) runs on the HIP kernels on an MI355X
+        engine = "hip" if device.type == "cuda" else "reference"
     if engine == "reference":
         return ReferenceEngine(cfg, batch_size, device, seed=seed, lr=lr, beta1=beta1,
                                zero_debias=zero_debias, rank=rank, world=world)

@@ -2,35 +2,45 @@
 
 The step (``image_train.py:151-158`` semantics) is recorded ONCE into
 native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buffers, then
-replayed every step -- optionally captured into hipGraphs so a step is a handful of graph
-launches:
+replayed every step -- captured into hipGraphs so a step is one (single process) or six (DDP)
+graph launches:
 
-  segment A   z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
-              2B batch [real | fake] with per-half BN statistics (= the reference's two
-              D calls) -> fused 3-loss BCE -> the g_loss chain back through D(fake)
-              (pre-update D weights) into G's backward (G grads final)
-  [DDP]       G-gradient all-reduce starts on the comm stream ...
-  segment B1  ... while D's backward of d_loss runs (both halves): head + top conv layer
-              first, i.e. 76 % of D's gradient bytes (d_h3_conv/w at 64x64) ...
-  [DDP]       ... whose all-reduce overlaps ...
-  segment B2  ... the rest of D's backward (D grads final); small last all-reduce
-  segment C   TF-Adam(G) (its all-reduce is long done), TF-Adam(D), step counter (device
-              beta powers, 1/W folded in); each Adam also writes the bf16/fp16 weight mirror
-              that the next step's kernels read
+  progA[:a_fwd]  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
+                 2B batch [real | fake] with per-half BN statistics (= the reference's two
+                 D calls) -> fused 3-loss BCE
+  progA[a_fwd:]  the g_loss chain back through D(fake) (pre-update D weights) and G's
+                 backward (G grads final)                          -- the "G chain"
+  progB          D's backward of d_loss, both halves (D grads final) -- the "D chain";
+                 runs on its own stream concurrently with the G chain (disjoint buffers,
+                 both only READ D's forward state and weights)
+  progC          TF-Adam(G), TF-Adam(D), beta powers, global step (device-resident); each
+                 Adam also writes the 16-bit weight mirror the next step's GEMMs read
 
-G's backward finalises its largest gradient (g_h1/w) LAST and D's backward finalises its
-largest FIRST, so running G's backward before D's leaves only a few MB of the 37.8 MB fp32
-exchange exposed -- on xGMI rings the bytes, not the number of calls, set the cost.
+Schedules (``_schedule``), all three covered by the stream-hazard checker
+(``engine/schedule_check.py``) and by GPU bit-exactness tests:
+  "fused"       single process: ONE hipGraph; the two backward chains on two streams; ONE
+                Adam launch for both models after the join (16-bit dtypes)
+  "concurrent"  DDP (and the per-phase timed step): the same two chains cut into 6 graph
+                segments so the collectives are issued between them from the host -- D's top
+                layer + head (76 % of D's gradient bytes at 64x64) as soon as the D chain has
+                produced it, G's gradients when the G chain ends, the rest of D's when the D
+                chain ends; Adam(G) waits for G's collective only, Adam(D) for all
+  "serial"      ``schedule="serial"`` / DCGAN_SERIAL_DBWD=1: fwd + G chain, then the D chain, as
+                5 segments (the G all-reduce overlaps D's backward)
 
-Layouts: activations NHWC bf16; master weights fp32 in TF layout inside the flat
-``ParamSet`` buffers (what the checkpoint writes and DDP reduces); each conv weight also
-has bf16 copies packed for the implicit-GEMM kernels ([25][N][Kc]: natural and per-tap
-transposed, or an im2col-ordered [N][80] matrix for the 3-channel layers).
+Every schedule is issued through an executor (``_TorchExec``; the checker substitutes a
+recording one), so the stream order the checker proves is the order the GPU runs.
+
+Layouts: activations NHWC in the compute dtype (bf16 / fp16 / fp32); master weights fp32 in
+TF layout inside the flat ``ParamSet`` buffers (what the checkpoint writes and DDP reduces);
+16-bit runs keep one mirror of every weight in the same flat layout, which every GEMM reads
+in whichever orientation it needs (fp32 runs read the masters directly).
 """
 from __future__ import annotations
 
 import math
 import os
+from collections import OrderedDict
 from typing import Dict, List, Optional
 
 import torch
@@ -42,6 +52,8 @@ from ..ops import hip as H
 from ..parallel import dist as D
 
 RELU, LRELU, TANH, NONE = 1, 2, 3, 0
+DTYPES = {"bf16": (0, torch.bfloat16), "fp16": (1, torch.float16), "fp32": (2, torch.float32)}
+SCHEDULES = ("fused", "concurrent", "serial")
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
@@ -50,6 +62,50 @@ def _p(t: Optional[torch.Tensor]) -> int:
 
 def _kpad(c: int) -> int:
     return -(-25 * c // 16) * 16
+
+
+class _TorchExec:
+    """Issues a schedule onto real HIP streams (torch.cuda.Stream objects)."""
+
+    def __init__(self, eng: "HipEngine"):
+        dev = eng.device
+        self.dev = dev
+        self.side = torch.cuda.Stream(device=dev)                        # slot 1 of main-stream segments
+        self.alt = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]  # D chain (+ its slot 1)
+        self.comm = eng.comm_stream
+
+    def main(self):
+        return torch.cuda.current_stream(self.dev)
+
+    @staticmethod
+    def run(prog, streams, begin: int = 0, end: int = -1) -> None:
+        H.run(prog, streams, begin, end)
+
+    @staticmethod
+    def wait(dst, src) -> None:
+        """dst waits for everything queued on src so far."""
+        dst.wait_stream(src)
+
+    @staticmethod
+    def mark(stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
+
+    @staticmethod
+    def wait_mark(dst, ev) -> None:
+        """dst waits for the work queued on the marked stream up to the mark."""
+        dst.wait_event(ev)
+
+    @staticmethod
+    def collective(reducer, stream) -> None:
+        with torch.cuda.stream(stream):
+            reducer.issue()
+
+    @staticmethod
+    def replay(graph, stream) -> None:
+        with torch.cuda.stream(stream):
+            graph.replay()
 
 
 class HipEngine:
@@ -61,15 +117,16 @@ class HipEngine:
     def __init__(self, cfg: DCGANConfig, batch_size: int, device: torch.device, dtype: str = "bf16",
                  seed: int = 0, lr: float = 2e-4, beta1: float = 0.5, zero_debias: bool = False, rank: int = 0,
                  world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 32.0,
-                 rank_seeded_z: bool = True, **_):
-        if dtype not in ("bf16", "fp16"):
-            raise ValueError("the HIP engine computes in bf16 or fp16 (fp32 master weights / statistics / "
-                             "accumulation); fp32 runs on --engine=reference")
+                 rank_seeded_z: bool = True, schedule: Optional[str] = None, dry_run: bool = False, **_):
+        if dtype not in DTYPES:
+            raise ValueError("HIP engine dtype must be one of %s" % sorted(DTYPES))
         self.dtype_name = dtype
+        self.dt, self.edt = DTYPES[dtype]
         self.f16 = dtype == "fp16"
-        self.edt = torch.float16 if self.f16 else torch.bfloat16
-        if device.type != "cuda":
-            raise ValueError("HipEngine needs a GPU")
+        self.f32 = dtype == "fp32"
+        self.dry = bool(dry_run)  # record programs on the CPU for the schedule checker; never runs
+        if device.type != "cuda" and not self.dry:
+            raise ValueError("HipEngine needs a GPU (dry_run=True only records the step)")
         self.ext = H.ext()
         self.cfg = cfg
         self.B = int(batch_size)
@@ -78,8 +135,13 @@ class HipEngine:
         self.seed = int(seed)
         self.rank_seeded_z = bool(rank_seeded_z)  # False only in equivalence tests
         self.lr, self.beta1 = float(lr), float(beta1)
+        if schedule is None and os.environ.get("DCGAN_SERIAL_DBWD") == "1":
+            schedule = "serial"
+        if schedule is not None and schedule not in SCHEDULES:
+            raise ValueError("schedule must be one of %s" % (SCHEDULES,))
+        self._sched_req = schedule
         self.model = DCGAN(cfg, device=device, seed=seed, zero_debias=zero_debias)
-        if world > 1:
+        if world > 1 and not self.dry:
             D.broadcast_tensors([self.model.g.flat, self.model.d.flat, self.model.g_bn.flat, self.model.d_bn.flat])
         self.opt_d = TFAdam(self.model.d, lr, beta1, power_suffix="")
         self.opt_g = TFAdam(self.model.g, lr, beta1, power_suffix="_1")
@@ -88,16 +150,21 @@ class HipEngine:
         self.grad_g = self.model.g.like()
         self._step_host = 0
         self.step_counter = torch.zeros(1, dtype=torch.int64, device=device)  # device global step
-        self.graph_requested = bool(graph)
+        self.graph_requested = bool(graph) and not self.dry
         self.graph_enabled = False
         self._timing = False
         self._graphs: List[Optional[torch.cuda.CUDAGraph]] = []
-        self.comm_stream = torch.cuda.Stream(device=device) if world > 1 else None
+        self.comm_stream = torch.cuda.Stream(device=device) if (world > 1 and not self.dry) else None
         self.allreduce_dtype = allreduce_dtype
         self.bucket_mb = bucket_mb
+        self._exec = None
         self._alloc()
         self._build()
-        self._repack_weights_now()
+        if not self.dry:
+            self._repack_weights_now()
+
+    def _prog(self):
+        return self.ext.Program(self.dt, self.dry)
 
     # ------------------------------------------------------------------ buffers
     def _t(self, *shape, dtype=None, zero=False):
@@ -124,7 +191,6 @@ class HipEngine:
             self.g_a[L.name] = t(B, L.out_hw, L.out_hw, L.cout)
         # ---------------- D input [real | fake]
         self.d_in = t(B2, s, s, cfg.c_dim, zero=True)
-        self.real_src = t(B, s, s, cfg.c_dim)
         self.fake = self.d_in[B:]
         self.d_x, self.d_a = {}, {}
         for i, L in enumerate(self.dl):
@@ -148,11 +214,9 @@ class HipEngine:
         self.d_da = {L.name: t(B2, L.out_hw, L.out_hw, L.cout) for L in self.dl}
         self.d_dx = {L.name: t(B2, L.out_hw, L.out_hw, L.cout) for L in self.dl}
         # the g_loss chain back through D(fake) has its own gradient buffers (B rows), so it never
-        # shares memory with D's d_loss backward (the two may run concurrently)
+        # shares memory with D's d_loss backward (the two run concurrently)
         self.gc_da = {L.name: t(B, L.out_hw, L.out_hw, L.cout) for L in self.dl}
         self.gc_dx = {L.name: t(B, L.out_hw, L.out_hw, L.cout) for L in self.dl}
-        self.d_head_dx = t(B2, cfg.d_lin_in)
-        self.d_head_part = t(16, cfg.d_lin_in, dtype=torch.float32)
         self.img_grad = t(B, s, s, cfg.c_dim)
         self.img_g = t(B, s, s, cfg.c_dim)
         Lg = self.gl[-1]
@@ -168,16 +232,22 @@ class HipEngine:
         self.coef = {name: t(2, C, 3, dtype=torch.float32) for name, C in cfg.d_bn_layers()}
         self.coef.update({name: t(1, C, 3, dtype=torch.float32) for name, C in cfg.g_bn_layers()})
         self.coef_g = {name: t(1, C, 3, dtype=torch.float32) for name, C in cfg.d_bn_layers()}
-        self.small_part = t(64, 16, dtype=torch.float32)
-        # ---------------- bf16 weight mirrors: the SAME flat layout as the fp32 masters (TF layouts:
-        # HWIO conv, [kh,kw,out,in] deconv), written by the Adam kernel; every conv GEMM reads
-        # its weight from here in whichever orientation it needs (igemm3 bkn flag)
-        self.wbf_d = self.model.d.like(self.edt)
-        self.wbf_g = self.model.g.like(self.edt)
+        # one column-sum scratch per chain: the two chains run concurrently
+        self.small_part = {"d": t(64, 16, dtype=torch.float32), "g": t(64, 16, dtype=torch.float32)}
+        # ---------------- weights the GEMMs read: 16-bit mirrors in the SAME flat layout as the
+        # fp32 masters (TF layouts: HWIO conv, [kh,kw,out,in] deconv), written by the Adam kernel;
+        # fp32 runs read the masters themselves
+        if self.f32:
+            self.wbf_d, self.wbf_g = self.model.d, self.model.g
+        else:
+            self.wbf_d = self.model.d.like(self.edt)
+            self.wbf_g = self.model.g.like(self.edt)
         # fp16: dynamic loss scale state [scale, overflow flag, good steps] (device-resident, so
         # the whole step incl. skip / halve / grow stays inside the captured graphs)
         self.loss_scale = (torch.tensor([self.INIT_LOSS_SCALE, 0.0, 0.0], dtype=torch.float32, device=self.device)
                            if self.f16 else None)
+        # sampler zero-debias factor 1 / (1 - decay^t) (device scalar, set before each sampler run)
+        self._debias = torch.ones(1, dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------------ program build
     def _stats_buf(self, key, P, C):
@@ -186,71 +256,48 @@ class HipEngine:
         return buf
 
     def _build(self):
-        ext = self.ext
         self._keep: List[torch.Tensor] = []
-        self.progA = ext.Program(self.f16)
-        self.progB = ext.Program(self.f16)
-        self.progC = ext.Program(self.f16)
-        self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True, split_d=True)
+        self.progA = self._prog()
+        self.progB = self._prog()
+        self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
         self._a_fwd = self.progA.size()  # forward done: D's d_loss backward may start from here
         self._build_gloss_and_g_backward(self.progA)
-        self._join(self.progA)
-        # opt-in (single process): Adam(G) on the side stream, concurrently with D's backward,
-        # joined before Adam(D) / the step counter. Measured on MI355X at 64x64, B=128: 1.634 vs
-        # 1.556 ms/step serial -- the memory-bound Adam slows the GEMMs more than it hides.
-        self._adam_g_side = (self.world == 1 and not self.f16 and os.environ.get("DCGAN_CONCURRENT_ADAM") == "1")
-        if self._adam_g_side:
-            ev = self.progA.new_event()
-            self.progA.record(ev, 0)
-            self.progA.wait(ev, 1)
-            self._build_update(self.progA, first=True, stream=1)
         self._build_d_backward_dloss(self.progB)  # sets self._b_split (top layer done)
-        self._join(self.progB)
-        fused_adam = (not self._adam_g_side and self.world == 1 and not self.f16
-                      and os.environ.get("DCGAN_SEPARATE_ADAM") != "1")
-        if self._adam_g_side:
-            ev = self.progC.new_event()
-            self.progC.record(ev, 1)
-            self.progC.wait(ev, 0)
-            self._c_split = self.progC.size()
-            self._build_update(self.progC, first=False)
-        elif fused_adam:  # one launch: Adam(G), Adam(D), beta powers, global step
+        self._build_updates()
+        # D-gradient slice final after the D chain's first segment: the top conv layer (+ its BN)
+        # and the head, which the ParamSet lays out last
+        self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
+        self.progCast = self._prog()  # fp32 masters -> 16-bit mirrors (init / checkpoint load)
+        if not self.f32:
+            for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
+                self.progCast.cast_to_bf16("mirror", _p(ps.flat), 0, _p(pb.flat), ps.flat.numel(), 1.0, 0.0, 0)
+        self.progS = None  # sampler program, built lazily
+        self.progEval = None
+        self.progSum = None
+
+    def _build_updates(self):
+        """progC for the current schedule. The one-launch Adam over BOTH models is only used
+        where nothing else can be touching D's gradients or weights any more ("fused": after
+        the join of the two backward chains); every other schedule runs Adam(G) (segment
+        "adam_G", first _c_split ops) and Adam(D) + the step counter (segment "adam_D") apart."""
+        self.progC = self._prog()
+        if self._schedule() == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
             self._c_split = self.progC.size()
         else:
             self._build_update(self.progC, first=True)
             self._c_split = self.progC.size()
             self._build_update(self.progC, first=False)
-        # opt-in (single process, bf16): Adam(D) on the D chain's stream as soon as D's gradients
-        # are final AND the g_loss chain has left D (it reads the pre-update D weights); Adam(G) +
-        # the beta-power / step update after the join (see _run_fused). Measured on MI355X at
-        # 64x64, B=128: 1.325 vs 1.293 ms/step for the fused two-set Adam after the join -- the
-        # memory-bound Adam slows G's backward GEMMs more than it hides
-        # (profiles/ab_r1_early_adam_d.txt).
-        self._early_adam_d = (self.world == 1 and not self.f16 and not self._adam_g_side
-                              and os.environ.get("DCGAN_EARLY_ADAM_D") == "1")
-        if self._early_adam_d:
-            self.progCd = ext.Program(self.f16)
-            self.progCg = ext.Program(self.f16)
-            self._build_update_split(self.progCd, self.progCg)
-        # D-gradient slice final after segment B1: the top conv layer (+ its BN) and the head,
-        # which the ParamSet lays out last
-        self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
-        self.progCast = ext.Program(self.f16)  # fp32 masters -> bf16/fp16 mirrors (init / checkpoint load)
-        for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
-            self.progCast.cast_to_bf16("mirror", _p(ps.flat), 0, _p(pb.flat), ps.flat.numel(), 1.0, 0.0, 0)
-        self.progS = None  # sampler program, built lazily
-        self.progEval = None
 
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
                cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None, bkn=False, kb_valid=-1, bnb=None,
                stream=0):
-        """One conv-shaped GEMM. Bw is a bf16 weight-mirror view; bkn=True reads it as
-        [tap][K][N] (D forward, G dgrad, im2col'd layers), else as [tap][N][K]. bnb = (x, y,
-        mean, rstd, rows_per_group, act): the epilogue also emits the BN-backward partial sums of
+        """One conv-shaped GEMM. Bw is a weight view; bkn=True reads it as [tap][K][N] (D
+        forward, G dgrad, im2col'd layers), else as [tap][N][K]. bnb = (x, y, mean, rstd,
+        rows_per_group, act[, store_g]): the epilogue also emits the BN-backward partial sums of
         the layer whose dL/da this GEMM produces (see _dgrad_bnb)."""
-        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn)
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn, dtype=self.dt)
         if plan is None:
             raise RuntimeError("no igemm tile for %s (mode %d, N %d, bkn %d)" % (name, mode, N, bkn))
         cfg, splits = plan
@@ -265,22 +312,34 @@ class HipEngine:
                       bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak, bstore)
         return cfg
 
+    def _stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None, bkn=False):
+        """Number of partial-statistics rows a stats-emitting igemm writes (tiles x phases)."""
+        if mode == 1:
+            M, phases = Bn * (-(-Hout // 2)) * (-(-Wout // 2)), 4
+        else:
+            M, phases = Bn * Hout * Wout, 1
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn, dtype=self.dt)
+        if plan is None:
+            return None
+        bm, _ = H.tile_of(plan[0], self.dt)
+        return -(-M // bm) * phases
+
     def _dgrad_bnb(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, bn_name, x, y, groups, act, group_offset=0):
         """Fused BN-backward statistics for the data-gradient GEMM that writes dL/da of BN layer
         ``bn_name`` (x = its pre-BN input, y = its activation output, same layout as the GEMM
         output). Returns (igemm kwargs, partials, partials per group) or None when no tile keeps
-        the real/fake groups apart (odd sizes) -- the BN backward then runs its own stats pass."""
-        if os.environ.get("DCGAN_NO_FUSED_BNB") == "1":
+        the real/fake groups apart (odd sizes) or in fp32 -- the BN backward then runs its own
+        statistics pass."""
+        if self.f32:
             return None
         if mode == 1:
-            hq, wq, phases = -(-Hout // 2), -(-Wout // 2), 4
             if Hout % 2 or Wout % 2:
                 return None
-            M = Bn * hq * wq
+            M, phases = Bn * (Hout // 2) * (Wout // 2), 4
         else:
             M, phases = Bn * Hout * Wout, 1
         rpg = M // groups
-        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rpg, bkn)
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rpg, bkn, dtype=self.dt)
         if plan is None or N % 8 or not H.bnb_fits(plan[0]):
             return None
         bm, _ = H.tile_of(plan[0])
@@ -295,10 +354,10 @@ class HipEngine:
         """Fused activation backward for the data-gradient GEMM that produces dL/da of a layer
         WITHOUT BN: the GEMM stores dx = dL/da * act'(y) directly and emits per-tile partial
         column sums of dx (the bias gradient). Returns (igemm kwargs, partials, #partials) or
-        None (no vectorizable tile; the caller runs the separate act backward)."""
-        if os.environ.get("DCGAN_NO_FUSED_ACTG") == "1":
+        None (fp32, or no vectorizable tile: the caller runs the separate act backward)."""
+        if self.f32:
             return None
-        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, None, bkn)
+        plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, None, bkn, dtype=self.dt)
         if plan is None or N % 8 or not H.bnb_fits(plan[0]):
             return None
         bm, _ = H.tile_of(plan[0])
@@ -311,40 +370,28 @@ class HipEngine:
         return dict(stats=part, bnb=(y, y, None, None, 0, act, True)), part, P
 
     def _deconv_out(self, prog, name, x, w, y, B, L, pad, bias, act):
-        """G's output layer: the direct narrow kernel for RGB / gray outputs, else the igemm."""
-        if L.cout <= 4 and L.cin % 8 == 0 and L.cin <= 256:
+        """G's output layer: the direct narrow kernel for RGB / gray outputs (16-bit), else the
+        implicit GEMM."""
+        if not self.f32 and L.cout <= 4 and L.cin % 8 == 0 and L.cin <= 256:
             prog.narrow_deconv(name, _p(x), _p(w), _p(bias), _p(y), B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw,
                                L.cout, pad, act, self.cfg.lrelu_leak, 0)
         else:
             self._igemm(prog, name, 1, x, w, y, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad,
                         bias=bias, act=act)
 
-    def _igemm_stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None, bkn=False):
-        if mode == 1:
-            M = Bn * (-(-Hout // 2)) * (-(-Wout // 2))
-            phases = 4
-        else:
-            M = Bn * Hout * Wout
-            phases = 1
-        cfg, _ = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn)
-        bm, _ = H.tile_of(cfg)
-        return -(-M // bm) * phases
-
-    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema, slot=0, stream=0):
-        """BN finalize (+EMA) and apply+act over `groups` row groups whose statistics / EMA
-        shadows start at group slot `slot` (D's separate-half passes run groups=1, slot=half)."""
+    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema):
+        """BN finalize (+EMA) and apply+act over `groups` row groups."""
         cfgm = self.cfg
-        st = {k: v[slot:] for k, v in self.bn[name].items()}
+        st = self.bn[name]
         bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
         P = self.model.d if name.startswith("d_") else self.model.g
-        ema_m = bnstate.mean[name][slot:] if update_ema else None
-        ema_v = bnstate.var[name][slot:] if update_ema else None
-        tag = name if slot == 0 and groups > 1 or name.startswith("g_") else "%s.%d" % (name, slot)
-        prog.bn_finalize(tag + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
+        ema_m = bnstate.mean[name] if update_ema else None
+        ema_v = bnstate.var[name] if update_ema else None
+        prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
                          _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
-                         _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, stream)
-        prog.bn_apply_act(tag + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
-                          rows // groups, act, cfgm.lrelu_leak, stream)
+                         _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
+        prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
+                          rows // groups, act, cfgm.lrelu_leak, 0)
 
     @staticmethod
     def _rows_per_block(rows_per_group: int, C: int) -> int:
@@ -355,90 +402,28 @@ class HipEngine:
                 return rpb
         return 1
 
-    # ---- forward
-    def _d_forward_half(self, prog, half: int, update_ema: bool, stream: int):
-        """D's forward over ONE half of the [real | fake] batch (B rows at row offset half*B):
-        the reference's separate D(real) / D(fake) calls (image_train.py:82,85), each with its
-        own BN statistics and EMA slot. Used by the split forward, where D(real) runs on the
-        side stream concurrently with G's forward."""
-        cfg, B = self.cfg, self.B
-        Pd, Wd = self.model.d, self.wbf_d
-        hs = lambda t: t[half * B:(half + 1) * B]  # noqa: E731  one half of a [2B, ...] buffer
-        prev = hs(self.d_in)
-        tag = ".r" if half == 0 else ".f"
-        for i, L in enumerate(self.dl):
-            w = Wd[L.name + "/w"]  # HWIO [5,5,ci,co] = [tap][K][N]
-            pad = same_pads(L.in_hw)[0]
-            rows = B * L.out_hw ** 2
-            if i == 0 and L.cin % 8 != 0:
-                col = self.d0_col[half * rows:(half + 1) * rows]
-                prog.im2col_s2("d0.im2col" + tag, _p(prev), _p(col), B, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                               L.out_hw, pad, pad, self.kp_d0, stream)
-                self._igemm(prog, L.name + tag, 2, col, w, hs(self.d_a[L.name]), B, 1, 1, self.kp_d0, L.out_hw,
-                            L.out_hw, L.cout, 0, bias=Pd[L.name + "/biases"], act=LRELU, bkn=True,
-                            kb_valid=25 * L.cin, stream=stream)
-            elif not L.bn:
-                self._igemm(prog, L.name + tag, 0, prev, w, hs(self.d_a[L.name]), B, L.in_hw, L.in_hw, L.cin,
-                            L.out_hw, L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU, bkn=True,
-                            stream=stream)
-            else:
-                P = self._igemm_stats_tiles(0, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, None, True)
-                part = self._stats_buf(L.bn + tag, P, L.cout)
-                self._igemm(prog, L.name + tag, 0, prev, w, hs(self.d_x[L.name]), B, L.in_hw, L.in_hw, L.cin,
-                            L.out_hw, L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, bkn=True,
-                            stream=stream)
-                self._bn_fwd(prog, L.bn, hs(self.d_x[L.name]), hs(self.d_a[L.name]), rows, L.cout, 1, LRELU, part,
-                             P, update_ema, slot=half, stream=stream)
-            prev = hs(self.d_a[L.name])
-
     def _d0_direct(self) -> bool:
-        """D layer 0 forward on the direct conv3 kernel (Cin <= 4, Cout = 64) instead of
-        im2col + GEMM; DCGAN_D0_IM2COL=1 keeps the im2col forward."""
+        """D layer 0 forward on the direct conv3 kernel (16-bit, Cin <= 4, Cout = 64) instead of
+        im2col + GEMM."""
         L = self.dl[0]
-        return L.cin <= 4 and L.cout == 64 and os.environ.get("DCGAN_D0_IM2COL") != "1"
+        return not self.f32 and L.cin <= 4 and L.cout == 64
 
-    def _split_dfwd_ok(self) -> bool:
-        """Split forward (opt-in, DCGAN_SPLIT_DFWD=1): D(real) on the side stream beside G's
-        forward, D(fake) after G. Measured on MI355X at 64x64, B=128: 1.334 vs 1.321 ms/step
-        for the default single D pass over the stacked 2B batch -- G's forward GEMMs already
-        fill the CUs, and the half-batch GEMMs run at lower efficiency."""
-        if os.environ.get("DCGAN_SPLIT_DFWD") != "1":
-            return False
-        B = self.B
-        for L in self.dl:
-            if L.bn and H.igemm_cfg_for(0, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, None,
-                                        True) is None:
-                return False
-        return True
-
-    def _build_forward(self, prog, update_ema: bool, z, train_z: bool, split_d: bool = False):
+    # ---- forward
+    def _build_forward(self, prog, update_ema: bool, z, train_z: bool):
         cfg, B = self.cfg, self.B
         B2 = 2 * B
         Pg, Pd = self.model.g, self.model.d
-        split_d = split_d and self._split_dfwd_ok()
-        if prog is self.progA:
-            self.split_dfwd = split_d
-        if split_d:  # D(real) needs only the real batch and D's weights: start it at once
-            ev = prog.new_event()
-            prog.record(ev, 0)
-            prog.wait(ev, 1)
-            self._d_forward_half(prog, 0, update_ema, stream=1)
         zseed = self.seed * 1000003 + 17 + 7919 * self.rank * int(self.rank_seeded_z)
-        # train_z: z ~ U(-1,1) generated inside the projection kernel (Philox keyed by the device
-        # step counter; DCGAN_SEPARATE_PHILOX=1 keeps the standalone kernel for A/B)
-        gen_in_linear = train_z and os.environ.get("DCGAN_SEPARATE_PHILOX") != "1"
-        if train_z and not gen_in_linear:
-            prog.philox_uniform("z", _p(z), z.numel(), zseed, _p(self.step_counter), 0, -1.0, 1.0, 0)
-        # G projection + g_bn0 + relu
+        # G projection + g_bn0 + relu; train_z: z ~ U(-1,1) generated inside the projection kernel
+        # (Philox keyed by the device step counter); g_bn0 partial statistics straight from it:
+        # one partial row per (8-row block of z, spatial position) -- see linear_fwd_kernel
         C0 = cfg.g_base_ch
         rows0 = B * cfg.g_base_hw ** 2
-        # g_bn0 partial statistics straight from the projection kernel: one partial row per
-        # (8-row block of z, spatial position) -- see linear_fwd_kernel
         P0 = -(-B // 8) * (cfg.g_lin_out // C0)
         part0 = self._stats_buf("g_bn0", P0, C0)
         prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
                         B, cfg.z_dim, cfg.g_lin_out, 0, _p(part0), C0,
-                        _p(self.step_counter) if gen_in_linear else 0, zseed if gen_in_linear else 0)
+                        _p(self.step_counter) if train_z else 0, zseed if train_z else 0)
         self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, P0, update_ema)
         a_prev = self.g_h0
         Wg, Wd = self.wbf_g, self.wbf_d
@@ -446,7 +431,7 @@ class HipEngine:
             nat = Wg[L.name + "/w"]  # [5,5,co,ci] = [tap][N][K]
             pad = same_pads(L.out_hw)[0]
             if L.bn:
-                P = self._igemm_stats_tiles(1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout)
+                P = self._stats_tiles(1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout)
                 part = self._stats_buf(L.bn, P, L.cout)
                 self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
                             L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part)
@@ -456,16 +441,9 @@ class HipEngine:
                 a_prev = self.g_a[L.name]
             else:  # last: + bias, tanh, written into the fake half of D's input
                 self._deconv_out(prog, L.name, a_prev, nat, self.fake, B, L, pad, Pg[L.name + "/biases"], TANH)
-        if split_d:  # D(fake) behind G's forward, then join the D(real) branch for the head
-            self._d_forward_half(prog, 1, update_ema, stream=0)
-            ev = prog.new_event()
-            prog.record(ev, 1)
-            prog.wait(ev, 0)
-            prev = self.d_a[self.dl[-1].name]
         # D forward on [real | fake]
-        else:
-            prev = self.d_in
-        for i, L in enumerate(self.dl if not split_d else ()):
+        prev = self.d_in
+        for i, L in enumerate(self.dl):
             w = Wd[L.name + "/w"]  # HWIO [5,5,ci,co] = [tap][K][N]
             pad = same_pads(L.in_hw)[0]
             rows = B2 * L.out_hw ** 2
@@ -484,10 +462,10 @@ class HipEngine:
                             L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU, bkn=True)
             else:
                 rpg = B * L.out_hw ** 2
-                if H.igemm_cfg_for(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True) is not None:
+                P = self._stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True)
+                if P is not None:
                     # BN partial statistics straight from the conv epilogue (tiles never straddle
                     # the real/fake boundary)
-                    P = self._igemm_stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True)
                     part = self._stats_buf(L.bn, P, L.cout)
                     self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                 L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg,
@@ -504,15 +482,10 @@ class HipEngine:
                              update_ema)
             prev = self.d_a[L.name]
         lin = cfg.d_lin_name
-        if os.environ.get("DCGAN_SEPARATE_LOSS") == "1":
-            prog.gemv_head("d_head", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits), B2,
-                           cfg.d_lin_in, 0)
-            prog.gan_loss("loss", _p(self.logits), B, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob), 0,
-                          _p(self.loss_scale))
-        else:  # head GEMV + the fused 3-loss BCE in its last-arriving block
-            prog.gemv_head("d_head+loss", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits),
-                           B2, cfg.d_lin_in, 0, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob),
-                           _p(self.loss_scale))
+        # head GEMV + the fused 3-loss BCE in its last-arriving block
+        prog.gemv_head("d_head+loss", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits),
+                       B2, cfg.d_lin_in, 0, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob),
+                       _p(self.loss_scale))
 
     # ---- D backward for d_loss (2B rows, both groups) -> all D gradients
     def _build_d_backward_dloss(self, prog):
@@ -521,15 +494,8 @@ class HipEngine:
         Pd, gD = self.model.d, self.grad_d
         lin = cfg.d_lin_name
         last = self.dl[-1]
-        if os.environ.get("DCGAN_NO_HEAD_BWD") == "1":  # A/B: the unfused head backward
-            prog.head_wgrad("d_head.wgrad", _p(self.d_a[last.name]), _p(self.dl_d), _p(self.d_head_part), B2,
-                            cfg.d_lin_in, 16, _p(gD[lin + "/Matrix"]), _p(gD[lin + "/bias"]), 0)
-            prog.head_dgrad("d_head.dgrad", _p(self.dl_d), _p(Pd[lin + "/Matrix"]), _p(self.d_da[last.name]), B2,
-                            cfg.d_lin_in, 0)
-            fused_next = None
-        else:
-            fused_next = self._head_bwd(prog, "d_head.bwd", self.d_a[last.name], self.dl_d, self.d_da[last.name],
-                                        gD[lin + "/Matrix"], gD[lin + "/bias"], B2, last, 2, 0)
+        fused_next = self._head_bwd(prog, "d_head.bwd", self.d_a[last.name], self.dl_d, self.d_da[last.name],
+                                    gD[lin + "/Matrix"], gD[lin + "/bias"], B2, last, 2, 0)
         # fused_next: BN-backward partials emitted by the layer above (head / dgrad GEMM store pass)
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
@@ -543,7 +509,8 @@ class HipEngine:
                 part, Pn = fused_next
                 prog.sum_partials(L.name + ".dbias", _p(part), Pn, 2 * L.cout, L.cout, _p(gD[L.name + "/biases"]), 0)
             else:  # live bias (no BN after it): db = sum over rows of dx, fused with the act backward
-                self._act_bwd_dbias(prog, L.name + ".act_bwd", da, a, dx, rows, L.cout, LRELU, gD[L.name + "/biases"])
+                self._act_bwd_dbias(prog, L.name + ".act_bwd", da, a, dx, rows, L.cout, LRELU, gD[L.name + "/biases"],
+                                    "d")
             # weight gradient
             src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
             pad = same_pads(L.in_hw)[0]
@@ -560,7 +527,6 @@ class HipEngine:
             if i == len(self.dl) - 1:
                 # head + top layer gradients final: DDP splits the segment here so their
                 # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
-                self._join(prog)
                 self._b_split = prog.size()
             # data gradient into the previous activation (not needed below layer 0)
             fused_next = None
@@ -582,16 +548,15 @@ class HipEngine:
                 self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
                             L.in_hw, L.in_hw, L.cin, pad, **kw)
 
-    def _act_bwd_dbias(self, prog, name, dy, y, dx, rows, C, act, db):
+    def _act_bwd_dbias(self, prog, name, dy, y, dx, rows, C, act, db, chain):
         """dx = dy * act'(y) and the bias gradient db = column sums of dx: one fused launch
         when the channel count has a kernel variant, else act_bwd + a column-sum pass."""
         leak = self.cfg.lrelu_leak if act == LRELU else 0.0
-        fused_ok = os.environ.get("DCGAN_NO_FUSED_ACTB") != "1"
-        if fused_ok and (C in (1, 3) or (C % 8 == 0 and C <= 256 and 256 % (C // 8) == 0)):
+        if C in (1, 3) or (C % 8 == 0 and C <= 256 and 256 % (C // 8) == 0):
             prog.act_bwd_dbias(name, _p(dy), _p(y), _p(dx), rows, C, act, leak, _p(db), 0)
         else:
             prog.act_bwd(name, _p(dy), _p(y), _p(dx), dx.numel(), act, leak, 0)
-            self._colsum(prog, name + ".dbias", dx, rows, C, db)
+            self._colsum(prog, name + ".dbias", dx, rows, C, db, chain)
 
     def _head_bwd(self, prog, name, xa, dl, dx, dW, db, R, last, groups, group_offset):
         """D head backward (dx, optional dW / db) with the top BN layer's backward statistics
@@ -603,8 +568,7 @@ class HipEngine:
         lin = cfg.d_lin_name
         K = cfg.d_lin_in
         C = last.cout
-        ok = bool(last.bn) and C % 64 == 0 and K % C == 0 and os.environ.get("DCGAN_NO_HEAD_STATS") != "1"
-        if not ok:
+        if not (bool(last.bn) and C % 64 == 0 and K % C == 0):
             prog.head_bwd(name, _p(xa), _p(dl), _p(Pd[lin + "/Matrix"]), _p(dx), _p(dW), _p(db), R, K, 0)
             return None
         S = K // C
@@ -616,7 +580,7 @@ class HipEngine:
                       _p(st["rstd"][group_offset:]), C, R // groups, LRELU, cfg.lrelu_leak, _p(part))
         return part, S
 
-    def _colsum(self, prog, name, x, rows, C, dst):
+    def _colsum(self, prog, name, x, rows, C, dst, chain):
         if C % 8 == 0:
             rpb = self._rows_per_block(rows, C)
             part = self._stats_buf(name, rows // rpb, C)
@@ -624,51 +588,29 @@ class HipEngine:
             prog.sum_partials(name + ".sum", _p(part), rows // rpb, 2 * C, C, _p(dst), 0)
         else:
             blocks = 64
-            prog.colsum_small(name, _p(x), rows, C, _p(self.small_part), blocks, 0)
-            prog.sum_partials(name + ".sum", _p(self.small_part), blocks, C, C, _p(dst), 0)
+            sp = self.small_part[chain]
+            prog.colsum_small(name, _p(x), rows, C, _p(sp), blocks, 0)
+            prog.sum_partials(name + ".sum", _p(sp), blocks, C, C, _p(dst), 0)
 
     def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst):
         K = Bn * Hd * Wd
         taps = 1 if mode == 2 else 25
-        # weight gradients may run on a side stream, concurrently with the data-gradient chain
-        # on the main stream (both only read dx / the layer input); see _fork
-        self._fork(prog)
-        if mode == 0:  # 25-tap layers: LDS-DMA pipelined kernel, split-K reduced in-kernel
+        if mode == 0 and not self.f32:  # 25-tap layers: LDS-DMA pipelined kernel, split-K reduced in-kernel
             plan = H.wgrad3_cfg_for(Mc, Nc, Bn, Hd, Wd, Hg)
             if plan is not None:
                 prog.wgrad3(name + ".wgrad", _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, plan[0], plan[1],
-                            _p(dst), 1.0, self.SIDE)
+                            _p(dst), 1.0, 0)
                 return
-        cfg, splits = H.pick_wgrad(Mc, Nc, K, taps)
-        if mode == 0:
+        cfg, splits = H.pick_wgrad(Mc, Nc, K, taps, dtype=self.dt)
+        if mode == 0 and not self.f32:
             splits = H.wgrad_splits_for(Mc, Nc, Bn, Hd, Wd, Hg) or splits
         slabs = self._t(splits, taps, Mc, Nc, dtype=torch.float32)
         self._keep.append(slabs)
         prog.wgrad(name + ".wgrad", mode, _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(slabs),
-                   _p(dst), dst.numel(), 1.0, self.SIDE)
-
-    # ---- two-stream structure inside a segment: fork = side waits for main's progress so far,
-    # join = main waits for everything queued on side (every segment ends joined, so a segment
-    # captures into one hipGraph with parallel branches)
-    SIDE = 0
-
-    def _fork(self, prog):
-        # Weight gradients stay on the chain's own stream. Running them on a side stream beside
-        # the data-gradient chain was measured slower on MI355X (64x64, B=128): 69.4k vs 71.8k
-        # img/s with the serial step, and 1.332 vs 1.303 ms/step for G's weight gradients beside
-        # the concurrent G chain (profiles/ab_r1_concurrent_wgrad.txt) -- the two backward chains
-        # already fill the CUs. The side stream is used by the opt-in split forward only.
-        self.SIDE = 0
-
-    def _join(self, prog):
-        if getattr(self, "_side_open", False):
-            ev = prog.new_event()
-            prog.record(ev, 1)
-            prog.wait(ev, 0)
-            self._side_open = False
+                   _p(dst), dst.numel(), 1.0, 0)
 
     def _bn_bwd(self, prog, name, x, dy, y, dx, rows, C, groups, act, P, grads, coef, write_param_grads,
-                stats_key=None, row_offset_groups=None, fused=None):
+                row_offset_groups=None, fused=None):
         """BN + activation backward. fused = (partials, partials per group) when the producing
         data-gradient GEMM already emitted the statistics (else a column-stats pass here)."""
         st = self.bn[name]
@@ -697,7 +639,6 @@ class HipEngine:
     def _build_gloss_and_g_backward(self, prog):
         cfg, B = self.cfg, self.B
         Pd, Pg, gG = self.model.d, self.model.g, self.grad_g
-        lin = cfg.d_lin_name
         last = self.dl[-1]
         half = lambda t: t[B:]  # noqa: E731  fake half of a [2B, ...] buffer
         fused_next = self._head_bwd(prog, "g.d_head.dgrad", None, self.dl_g, self.gc_da[last.name], None, None,
@@ -731,18 +672,17 @@ class HipEngine:
                 self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, out, B, L.out_hw,
                             L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, **kw)
             else:
-                if L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
+                if not self.f32 and L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
                     prog.narrow_deconv("g." + L.name + ".dgrad_img", _p(dx), _p(nat), 0, _p(self.img_grad), B,
                                        L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, NONE, 0.0, 0)
                 else:
                     self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw,
                                 L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
-        # ---------------- G backward (reads no D state: Adam(D) may run from here on)
-        self._a_gd = prog.size()
+        # ---------------- G backward (reads no D state)
         n = len(self.gl)
         Lg = self.gl[-1]
         self._act_bwd_dbias(prog, "g_out.tanh_bwd", self.img_grad, self.fake, self.img_g, B * Lg.out_hw ** 2,
-                            Lg.cout, TANH, gG[Lg.name + "/biases"])
+                            Lg.cout, TANH, gG[Lg.name + "/biases"], "g")
         a_prev = self.g_a[self.gl[-2].name] if n > 1 else self.g_h0
         da_prev = self.g_da[self.gl[-2].name] if n > 1 else self.g_da0
         x_prev = self.g_x[self.gl[-2].name] if n > 1 else self.g_h0_pre
@@ -802,46 +742,33 @@ class HipEngine:
         prog.linear_wgrad("g_h0_lin.wgrad", _p(self.z), _p(self.g_dx0), _p(gG["g_h0_lin/Matrix"]),
                           _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
 
-    # ---- optimiser (+ bf16 weight mirrors)
-    def _build_update(self, prog, first: bool, stream: int = 0):
+    # ---- optimiser (+ 16-bit weight mirrors)
+    def _build_update(self, prog, first: bool):
         """TF-Adam for G (first part) and D + the step counter (last part); each Adam also
-        writes the bf16/fp16 mirror the conv GEMMs read. Under DDP the G all-reduce completes
-        first (it was issued before D's backward), so Adam(G) runs while D's last bucket is
-        still on the wire. fp16: one overflow check over both (all-reduced) gradients gates
-        both Adams, so everything runs in the last part."""
+        writes the 16-bit mirror the conv GEMMs read (fp32: none, the GEMMs read the masters).
+        Under DDP the G all-reduce completes first (it was issued before D's backward ends), so
+        Adam(G) runs while D's last bucket is still on the wire. fp16: one overflow check over
+        both (all-reduced) gradients gates both Adams, so everything runs in the last part."""
         gs = 1.0 / self.world
         od, og = self.opt_d, self.opt_g
         ls = _p(self.loss_scale)
         do_g = (first and not self.f16) or (not first and self.f16)
         do_d = not first
+        mg = 0 if self.f32 else _p(self.wbf_g.flat)
+        md = 0 if self.f32 else _p(self.wbf_d.flat)
         if self.f16 and do_d:
             prog.nonfinite_check("ls.check_d", _p(self.grad_d.flat), self.grad_d.flat.numel(), ls, 0)
             prog.nonfinite_check("ls.check_g", _p(self.grad_g.flat), self.grad_g.flat.numel(), ls, 0)
         if do_g:
-            prog.adam_bf("adam_g", _p(self.model.g.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
+            prog.adam_bf("adam_g", _p(self.model.g.flat), mg, _p(self.grad_g.flat), _p(og.m.flat),
                          _p(og.v.flat), _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
-                         gs, stream, ls)
+                         gs, 0, ls)
         if do_d:
-            prog.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
+            prog.adam_bf("adam_d", _p(self.model.d.flat), md, _p(self.grad_d.flat), _p(od.m.flat),
                          _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
                          gs, 0, ls)
             prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
                           _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
-
-    def _build_update_split(self, prog_d, prog_g):
-        """Single-process bf16: TF-Adam(D) alone (prog_d, run beside G's backward), then
-        TF-Adam(G) + the beta-power / global-step update (prog_g) -- the same kernels and
-        arithmetic as _build_update."""
-        od, og = self.opt_d, self.opt_g
-        ls = _p(self.loss_scale)
-        prog_d.adam_bf("adam_d", _p(self.model.d.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat),
-                       _p(od.v.flat), _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps,
-                       1.0, 0, ls)
-        prog_g.adam_bf("adam_g", _p(self.model.g.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
-                       _p(og.v.flat), _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
-                       1.0, 0, ls)
-        prog_g.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
-                        _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
 
     def _build_update_fused(self, prog):
         """Single-process bf16: both TF-Adams + the beta-power / global-step update in one launch
@@ -854,41 +781,18 @@ class HipEngine:
                    od.beta1, od.beta2, od.eps, 1.0 / self.world, _p(self.step_counter), 0)
 
     def _repack_weights_now(self):
-        H.run(self.progCast)
+        if self.progCast.size():
+            H.run(self.progCast)
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ execution
-    def _streams(self):
-        if not hasattr(self, "_side_stream"):
-            self._side_stream = torch.cuda.Stream(device=self.device)
-        return [torch.cuda.current_stream(self.device), self._side_stream]
-
-    # Schedules:
-    #   "fused"       single process: ONE graph; D's d_loss backward (progB) on its own streams
-    #                 concurrently with the g_loss chain + G's backward (progA tail)
-    #   "concurrent"  DDP (and the timed single-process step): the same two concurrent chains,
-    #                 cut into 6 graphs so the collectives can be issued between them from the
-    #                 host: D's top layer + head (76 % of D's bytes) is all-reduced as soon as the
-    #                 D chain has produced it, G's gradients as soon as G's backward ends, the
-    #                 rest of D's when the D chain ends; Adam(G) / Adam(D) wait for their own
-    #                 collectives only
-    #   "serial"      DCGAN_SERIAL_DBWD=1: fwd + G backward, then D's backward, as 5 segments
-    #                 (G all-reduce overlaps D's backward)
     MAIN, ALT = 0, 1
 
     def _schedule(self) -> str:
-        if self.world == 1 and not self._timing:
-            return "fused"
-        if os.environ.get("DCGAN_SERIAL_DBWD") == "1" or self._adam_g_side:
-            return "serial"
-        return "concurrent"
-
-    @property
-    def _hybrid(self) -> bool:
-        """Concurrent schedule variant (DCGAN_DDP_SCHEDULE=hybrid): only D's top layer + head
-        run beside the G chain; the rest of D's backward starts when the G chain ends, so it
-        overlaps G's all-reduce (the largest one, 20.5 MB fp32) instead of delaying it."""
-        return os.environ.get("DCGAN_DDP_SCHEDULE", "concurrent") == "hybrid"
+        req = self._sched_req
+        if self.world > 1 or self._timing:  # collectives / phase timers need the segmented step
+            return req if req in ("concurrent", "serial") else "concurrent"
+        return req or "fused"
 
     def _segments(self):
         """The step as a list of (name, [(program, begin, end)], stream) segments."""
@@ -909,10 +813,12 @@ class HipEngine:
         """Per-phase GPU timers: the step runs as segments with events between
         them. Call before the first train_step (graphs are captured per segment). Concurrent
         schedule: each phase is reported as ms from the step start to the END of that phase
-        (the D and G chains overlap); serial schedule: phase durations."""
-        if self._graphs:
+        (the D and G chains overlap); serial schedule: phase durations. The update program is
+        rebuilt for the segmented schedule (Adam(G) and Adam(D) apart)."""
+        if self._graphs or self._step_host:
             raise RuntimeError("enable_timing() must precede the first train_step")
         self._timing = True
+        self._build_updates()
         self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self._segments()) + 1)]
 
     def phase_times(self) -> Dict[str, float]:
@@ -926,123 +832,100 @@ class HipEngine:
             return {n + "@end": ev[0].elapsed_time(ev[i + 1]) for i, (n, _, _) in enumerate(segs)}
         return {n: ev[i].elapsed_time(ev[i + 1]) for i, (n, _, _) in enumerate(segs)}
 
-    def _concurrent_dbwd(self) -> bool:
-        """D's d_loss backward runs on its own streams concurrently with the g_loss chain + G's
-        backward (independent buffers; two chains of GEMMs and small latency-bound BN kernels
-        fill each other's gaps). Measured on MI355X at 64x64, B=128, single process: 1.32 vs
-        1.50 ms/step. DCGAN_SERIAL_DBWD=1 serialises."""
-        return self._schedule() != "serial"
+    def _tick(self, i, stream) -> None:
+        if self._timing and not self.dry:
+            self._ev[i].record(stream)
 
-    def _alt(self):
-        if not hasattr(self, "_alt_streams"):
-            self._alt_streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
-        return self._alt_streams
+    def _get_exec(self):
+        if self._exec is None:
+            self._exec = _TorchExec(self)
+        return self._exec
 
-    def _run_fused(self, cs):
-        """The "fused" schedule issued onto cs (+ forked alt streams); also what gets captured.
+    def _run_fused(self, ex, cs):
+        """The "fused" schedule issued onto cs (+ the alt streams); also what gets captured.
         D's backward starts right after the forward: holding it until the g_loss chain has left
         D (so it overlaps only G's backward) measured 1.314 vs 1.297 ms/step on MI355X."""
-        side = self._streams()[1]
-        alt = self._alt()
-        H.run(self.progA, [cs, side], 0, self._a_fwd)
-        fork = torch.cuda.Event()
-        fork.record(cs)
-        alt[0].wait_event(fork)
-        H.run(self.progB, alt)
-        if self._early_adam_d:
-            H.run(self.progA, [cs, side], self._a_fwd, self._a_gd)   # g_loss chain through D(fake)
-            left_d = torch.cuda.Event()
-            left_d.record(cs)
-            alt[0].wait_event(left_d)
-            H.run(self.progCd, alt)                                   # Adam(D) beside G's backward
-            H.run(self.progA, [cs, side], self._a_gd, -1)            # G's backward
-        else:
-            H.run(self.progA, [cs, side], self._a_fwd, -1)
-        join = torch.cuda.Event()
-        join.record(alt[0])
-        cs.wait_event(join)
-        H.run(self.progCg if self._early_adam_d else self.progC, [cs, side])
+        ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
+        ex.wait(ex.alt[0], cs)
+        ex.run(self.progB, ex.alt)
+        ex.run(self.progA, [cs, ex.side], self._a_fwd, -1)
+        ex.wait(cs, ex.alt[0])
+        ex.run(self.progC, [cs, ex.side])
 
-    def _seg(self, i, stream):
+    def _seg(self, ex, i, stream):
         """Run segment i on `stream` (graph replay, or eager replay of its program ranges)."""
         if self.graph_enabled:
             g = self._graphs[i]
             if g is not None:
-                with torch.cuda.stream(stream):
-                    g.replay()
+                ex.replay(g, stream)
             return
         _, parts, which = self._segments()[i]
-        sec = self._streams()[1] if which == self.MAIN else self._alt()[1]
+        sec = ex.side if which == self.MAIN else ex.alt[1]
         for prog, b, e in parts:
-            H.run(prog, [stream, sec], b, e)
+            ex.run(prog, [stream, sec], b, e)
 
-    def _run_step(self):
-        st = self._streams()
-        cs = st[0]
+    def _ar_launch(self, ex, which: str, src) -> None:
+        """All-reduce one gradient slice ("g", "dtop", "drest") on the comm stream once `src`'s
+        queued work is done."""
+        if self.world > 1:
+            ex.wait(ex.comm, src)
+            ex.collective(getattr(self, "_ar_" + which), ex.comm)
+
+    def _ar_join(self, ex, dst) -> None:
+        """dst waits for every collective issued so far (the 1/W scale is folded into Adam)."""
+        if self.world > 1:
+            ex.wait(dst, ex.comm)
+
+    def _run_step(self, ex):
+        cs = ex.main()
         sch = self._schedule()
         if sch == "fused":
             if self.graph_enabled:
-                self._seg(0, cs)
+                self._seg(ex, 0, cs)
             else:
-                self._run_fused(cs)
+                self._run_fused(ex, cs)
             return
-        tick = (lambda i, s: self._ev[i].record(s)) if self._timing else (lambda i, s: None)
-        ddp = self.world > 1
         if sch == "concurrent":
-            alt = self._alt()[0]
-            tick(0, cs)
-            self._seg(0, cs)              # z, G fwd, D fwd (real | fake), losses
-            tick(1, cs)
-            alt.wait_stream(cs)
-            self._seg(1, alt)             # D chain: head + top layer gradients
-            tick(2, alt)
-            if ddp:
-                with torch.cuda.stream(alt):
-                    self._ar_dtop.launch()
-            self._seg(2, cs)              # G chain: g_loss through D(fake), G backward -> grad_g final
-            tick(3, cs)
-            if ddp:
-                with torch.cuda.stream(cs):
-                    self._ar_g.launch()
-            if self._hybrid:              # the rest of D's backward overlaps G's all-reduce instead
-                alt.wait_stream(cs)
-            self._seg(3, alt)             # D chain: rest of D's backward -> grad_d final
-            tick(4, alt)
-            if ddp:
-                with torch.cuda.stream(cs):
-                    self._ar_g.wait(scale_in_place=False)   # cs waits for dtop + G on the comm stream
-            self._seg(4, cs)              # Adam G -> G mirror (overlaps the last D all-reduce)
-            tick(5, cs)
-            if ddp:
-                with torch.cuda.stream(alt):
-                    self._ar_drest.launch()
-                with torch.cuda.stream(cs):
-                    self._ar_drest.wait(scale_in_place=False)
-            cs.wait_stream(alt)
-            self._seg(5, cs)              # Adam D, step counter, D mirror
-            tick(6, cs)
+            alt = ex.alt[0]
+            self._tick(0, cs)
+            self._seg(ex, 0, cs)               # z, G fwd, D fwd (real | fake), losses
+            self._tick(1, cs)
+            ex.wait(alt, cs)
+            self._seg(ex, 1, alt)              # D chain: head + top layer gradients
+            self._tick(2, alt)
+            self._ar_launch(ex, "dtop", alt)
+            self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward -> grad_g final
+            self._tick(3, cs)
+            self._ar_launch(ex, "g", cs)
+            self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
+            self._tick(4, alt)
+            self._ar_join(ex, cs)              # cs waits for the dtop + G collectives
+            self._seg(ex, 4, cs)               # Adam G -> G mirror (overlaps the last D all-reduce)
+            self._tick(5, cs)
+            self._ar_launch(ex, "drest", alt)
+            self._ar_join(ex, cs)
+            ex.wait(cs, alt)                   # (W = 1, timed: the D chain itself)
+            self._seg(ex, 5, cs)               # Adam D, step counter, D mirror
+            self._tick(6, cs)
             return
-        tick(0, cs)
-        self._seg(0, cs)                  # fwd, g_loss chain through D(fake), G backward -> grad_g final
-        tick(1, cs)
-        if ddp:
-            self._ar_g.launch()
-        self._seg(1, cs)                  # D backward: head + top layer (overlaps the G all-reduce)
-        tick(2, cs)
-        if ddp:
-            self._ar_dtop.launch()
-        self._seg(2, cs)                  # rest of D's backward -> grad_d final
-        tick(3, cs)
-        if ddp:
-            self._ar_drest.launch()
-            self._ar_g.wait(scale_in_place=False)
-        self._seg(3, cs)                  # Adam G -> G mirror (overlaps the last D all-reduce)
-        tick(4, cs)
-        if ddp:
-            self._ar_dtop.wait(scale_in_place=False)
-            self._ar_drest.wait(scale_in_place=False)
-        self._seg(4, cs)                  # Adam D, step counter, D mirror
-        tick(5, cs)
+        self._tick(0, cs)
+        self._seg(ex, 0, cs)                   # fwd, g_loss chain through D(fake), G backward -> grad_g final
+        self._tick(1, cs)
+        self._ar_launch(ex, "g", cs)
+        g_done = ex.mark(ex.comm) if self.world > 1 else None
+        self._seg(ex, 1, cs)                   # D backward: head + top layer (overlaps the G all-reduce)
+        self._tick(2, cs)
+        self._ar_launch(ex, "dtop", cs)
+        self._seg(ex, 2, cs)                   # rest of D's backward -> grad_d final
+        self._tick(3, cs)
+        self._ar_launch(ex, "drest", cs)
+        if g_done is not None:
+            ex.wait_mark(cs, g_done)           # G's collective only
+        self._seg(ex, 3, cs)                   # Adam G -> G mirror (overlaps the D all-reduces)
+        self._tick(4, cs)
+        self._ar_join(ex, cs)
+        self._seg(ex, 4, cs)                   # Adam D, step counter, D mirror
+        self._tick(5, cs)
 
     def _ensure_comm(self):
         if self.world > 1 and not hasattr(self, "_ar_g"):
@@ -1057,23 +940,24 @@ class HipEngine:
         between replays on the comm stream). Capturing does not execute anything; it is
         attempted only after one eager step has loaded every code object, and any failure
         falls back to eager replay of the recorded programs."""
+        ex = self._get_exec()
         try:
             torch.cuda.synchronize(self.device)
             graphs = []
             fused = self._schedule() == "fused"
             for name, parts, which in self._segments():
                 if all((p.size() if e < 0 else e) <= b for p, b, e in parts):
-                    graphs.append(None)  # empty segment (fp16: no separate D update)
+                    graphs.append(None)  # empty segment (fp16: no separate G update)
                     continue
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     cs = torch.cuda.current_stream(self.device)
                     if fused:
-                        self._run_fused(cs)
+                        self._run_fused(ex, cs)
                     else:
-                        sec = self._streams()[1] if which == self.MAIN else self._alt()[1]
+                        sec = ex.side if which == self.MAIN else ex.alt[1]
                         for prog, b, e in parts:
-                            H.run(prog, [cs, sec], b, e)
+                            ex.run(prog, [cs, sec], b, e)
                 graphs.append(g)
             self._graphs = graphs
             return True
@@ -1083,13 +967,19 @@ class HipEngine:
             return False
 
     def train_step(self) -> None:
+        if self.dry:
+            raise RuntimeError("a dry-run engine only records the step (engine.schedule_check)")
         self._ensure_comm()
         if (self.graph_requested and not self.graph_enabled and self._step_host >= 1
                 and not getattr(self, "_cap_tried", 0)):
             self._cap_tried = 1
             self.graph_enabled = self._capture()
-        self._run_step()
+        self._run_step(self._get_exec())
         self._step_host += 1
+        # one EMA update per BN slot per step (zero-debias bookkeeping, host-side counters)
+        self.model.g_bn.count_step(0)
+        for s in range(self.model.d_bn.slots):
+            self.model.d_bn.count_step(s)
 
     @property
     def global_step(self) -> int:
@@ -1118,7 +1008,6 @@ class HipEngine:
 
     def activations(self) -> "Dict[str, torch.Tensor]":
         """Views of the last step's tensors for summaries (no extra compute)."""
-        from collections import OrderedDict
         B = self.B
         a = OrderedDict()
         a["z"] = self.z
@@ -1134,34 +1023,69 @@ class HipEngine:
         a[self.cfg.d_lin_name] = self.logits[:B]
         return a
 
+    # ------------------------------------------------------------------ device-side summaries
+    def device_summaries(self) -> "OrderedDict[str, object]":
+        """Zero fraction + TF-bucket histogram statistics of every summarised tensor, computed on
+        the device (summary.hip) in ONE program; only the per-tensor statistics rows (a few KB
+        each) are copied to the host. Returns name -> numpy row [min, max, n, sum, sumsq, zeros,
+        counts...] (obs.summaries turns them into TensorBoard protos)."""
+        from ..obs.events import BUCKET_EDGES
+        if self.progSum is None:
+            names, tensors = [], []
+            for name, t in self.activations().items():
+                if name != "G":
+                    names.append(name + ("/activations" if name not in ("z", "d", "d_") else ""))
+                    tensors.append(t)
+            for name, t in self.model.all_named_variables().items():
+                names.append(name)
+                tensors.append(t)
+            nb = len(BUCKET_EDGES) + 1
+            self._sum_edges = torch.tensor(BUCKET_EDGES, dtype=torch.float64, device=self.device)
+            self._sum_out = torch.zeros(len(tensors), nb + 6, dtype=torch.float64, device=self.device)
+            prog = self._prog()
+            for i, t in enumerate(tensors):
+                xd = 0 if t.dtype == torch.float32 else 1
+                if xd == 1 and t.dtype != self.edt:
+                    raise TypeError("summary of %s: dtype %s" % (names[i], t.dtype))
+                prog.tensor_summary("sum." + names[i], _p(t), xd, t.numel(), _p(self._sum_edges), nb,
+                                    _p(self._sum_out[i]), 0)
+            self.progSum, self._sum_names = prog, names
+        H.run(self.progSum)
+        rows = self._sum_out.cpu().numpy()
+        return OrderedDict(zip(self._sum_names, rows))
+
     # ------------------------------------------------------------------ sampling / eval
     def sampler(self, z: torch.Tensor) -> torch.Tensor:
-        """G with inference-mode BN (moving averages) -- distriubted_model.py:131-153."""
+        """G with inference-mode BN (moving averages) -- distriubted_model.py:131-153. With
+        --bn_zero_debias the moving averages are divided by 1 - decay^t (t = EMA updates so far,
+        as in the reference engine's BNState.averages)."""
         if self.progS is None:
             self._build_sampler()
+        bn = self.model.g_bn
+        t = float(bn.steps[0])
+        corr = 1.0 - bn.decay ** t if (bn.zero_debias and t > 0) else 1.0
+        self._debias.fill_(1.0 / corr)
         self.sample_z.copy_(z.to(self.device, torch.float32))
         H.run(self.progS)
         return self._s_out.float().clone()
 
     def _build_sampler(self):
         cfg, B = self.cfg, self.B
-        prog = self.ext.Program(self.f16)
+        prog = self._prog()
         Pg = self.model.g
         t = self._t
-        self._s_bufs = {}
         h0p, h0 = t(B, cfg.g_lin_out), t(B, cfg.g_lin_out)
         self._s_out = t(B, cfg.output_size, cfg.output_size, cfg.c_dim)
         sc = {name: (t(C, dtype=torch.float32), t(C, dtype=torch.float32)) for name, C in cfg.g_bn_layers()}
         self._s_keep = [h0p, h0, sc]
         bnst = self.model.g_bn
-        debias = 1.0
         prog.linear_fwd("s.lin", _p(self.sample_z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(h0p), B,
                         cfg.z_dim, cfg.g_lin_out, 0)
 
-        def coef(name, C):
-            # zero-debias (if enabled) is applied host-side at build; BN state is read live
+        def coef(name, C):  # BN state and the debias factor are read live (device pointers)
             prog.bn_coef_eval("s." + name, C, _p(Pg[name + "/gamma"]), _p(Pg[name + "/beta"]), cfg.bn_eps,
-                              _p(bnst.mean[name]), _p(bnst.var[name]), debias, _p(sc[name][0]), _p(sc[name][1]), 0)
+                              _p(bnst.mean[name]), _p(bnst.var[name]), 1.0, _p(sc[name][0]), _p(sc[name][1]), 0,
+                              _p(self._debias))
 
         C0 = cfg.g_base_ch
         coef("g_bn0", C0)
@@ -1189,7 +1113,7 @@ class HipEngine:
         """Sample-time d_loss / g_loss (image_train.py:181-184) in train-mode BN but WITHOUT
         mutating the moving averages (documented deviation)."""
         if self.progEval is None:
-            prog = self.ext.Program(self.f16)
+            prog = self._prog()
             self._ev_z = self._t(self.B, self.cfg.z_dim, dtype=torch.float32)
             self._build_forward(prog, update_ema=False, z=self._ev_z, train_z=False)
             self.progEval = prog
@@ -1212,7 +1136,7 @@ class HipEngine:
         D.all_reduce_mean_(self.model.d_bn.flat)
 
     def after_state_load(self) -> None:
-        """Call after loading weights/slots from a checkpoint: refresh packed bf16 weights."""
+        """Call after loading weights/slots from a checkpoint: refresh the 16-bit weight mirrors."""
         self._repack_weights_now()
 
     def op_names(self) -> List[str]:
@@ -1220,3 +1144,10 @@ class HipEngine:
         for p in (self.progA, self.progB, self.progC):
             out += [p.name(i) for i in range(p.size())]
         return out
+
+    def kernel_count(self) -> int:
+        """Kernel launches per training step (events excluded)."""
+        n = 0
+        for p in (self.progA, self.progB, self.progC):
+            n += sum(1 for i in range(p.size()) if p.op_info(i)[2] == self.ext.OP_LAUNCH)
+        return n

@@ -31,7 +31,8 @@ def _default_buckets() -> List[float]:
     return [-x for x in reversed(pos)] + [0.0] + pos
 
 
-_BUCKETS = np.array(_default_buckets())
+BUCKET_EDGES = _default_buckets()
+_BUCKETS = np.array(BUCKET_EDGES)
 
 
 def histogram_proto(values: np.ndarray) -> bytes:
@@ -48,6 +49,21 @@ def histogram_proto(values: np.ndarray) -> bytes:
     return (wire.f_double(1, float(v.min())) + wire.f_double(2, float(v.max())) + wire.f_double(3, float(v.size)) +
             wire.f_double(4, float(v.sum())) + wire.f_double(5, float((v * v).sum())) +
             wire.f_packed_doubles(6, limits) + wire.f_packed_doubles(7, buckets))
+
+
+def histogram_proto_from_stats(row: Sequence[float]) -> bytes:
+    """HistogramProto from a device statistics row (summary.hip: [min, max, n, sum, sumsq,
+    zeros, counts over BUCKET_EDGES...]) -- the same proto histogram_proto builds on the host."""
+    row = np.asarray(row, dtype=np.float64)
+    E = len(_BUCKETS)
+    counts = row[6:6 + E].copy()
+    if row.size > 6 + E:
+        counts[-1] += row[6 + E:].sum()  # values above the last edge (inf): the last bucket
+    nz = np.nonzero(counts)[0]
+    lo, hi = (nz[0], nz[-1] + 1) if nz.size else (0, 1)
+    return (wire.f_double(1, float(row[0])) + wire.f_double(2, float(row[1])) + wire.f_double(3, float(row[2])) +
+            wire.f_double(4, float(row[3])) + wire.f_double(5, float(row[4])) +
+            wire.f_packed_doubles(6, _BUCKETS[lo:hi].tolist()) + wire.f_packed_doubles(7, counts[lo:hi].tolist()))
 
 
 class SummaryWriter:
@@ -76,6 +92,10 @@ class SummaryWriter:
     @staticmethod
     def histogram(tag: str, values: np.ndarray) -> bytes:
         return wire.f_bytes(1, wire.f_bytes(1, tag) + wire.f_bytes(5, histogram_proto(values)))
+
+    @staticmethod
+    def histogram_from_stats(tag: str, row: Sequence[float]) -> bytes:
+        return wire.f_bytes(1, wire.f_bytes(1, tag) + wire.f_bytes(5, histogram_proto_from_stats(row)))
 
     @staticmethod
     def image(tag: str, img: np.ndarray) -> bytes:

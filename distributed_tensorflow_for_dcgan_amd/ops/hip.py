@@ -66,16 +66,38 @@ def _p(t: Optional[torch.Tensor]) -> int:
 
 
 # --------------------------------------------------------------------------- tile policy
+CU_COUNT = 256
 IGEMM_CFGS = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (32, 64), 5: (64, 32),
               6: (32, 32), 7: (128, 16), 8: (64, 16), 9: (256, 64)}
 IGEMM3_TILES = {0: (128, 128), 1: (256, 64), 2: (64, 256), 3: (128, 64), 4: (64, 128), 5: (64, 64)}
+# fp32 build (igemm_f32.hip): the only tile family of that element type, cfg 200..203
+IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)}
 
 
-def tile_of(cfg: int) -> Tuple[int, int]:
-    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..219 igemm3.hip."""
+def tile_of(cfg: int, dtype: int = 0) -> Tuple[int, int]:
+    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..219 igemm3.hip; dtype 2
+    (fp32): igemm_f32.hip."""
+    if dtype == 2:
+        return IGEMM_F32_TILES[cfg]
     if cfg >= 200:
         return IGEMM3_TILES[cfg % 10]
     return IGEMM_CFGS[cfg % 100]
+
+
+def pick_igemm_f32(M: int, N: int, phases: int = 1, rows_per_group: Optional[int] = None,
+                   target_blocks: int = 2 * CU_COUNT) -> Optional[Tuple[int, int]]:
+    """(cfg, 1) for the fp32 implicit GEMM: the largest tile that still gives ~target_blocks
+    workgroups (narrow 64x16 tile for N <= 16, e.g. the RGB layers); no split-K."""
+    order = [202] if N <= 16 else ([203, 201, 200] if N >= 128 else [201, 200])
+    best = None
+    for c in order:
+        bm, bn = IGEMM_F32_TILES[c]
+        if rows_per_group is not None and rows_per_group % bm:
+            continue
+        best = c
+        if -(-M // bm) * -(-N // bn) * phases >= target_blocks:
+            break
+    return None if best is None else (best, 1)
 
 
 def bnb_fits(cfg: int) -> bool:
@@ -86,7 +108,6 @@ def bnb_fits(cfg: int) -> bool:
 
 
 WGRAD_CFGS = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64), 4: (32, 64), 5: (64, 32), 6: (32, 32)}
-CU_COUNT = 256
 
 
 def pick_igemm_cfg(M: int, N: int, phases: int = 1, rows_per_group: Optional[int] = None,
@@ -160,14 +181,20 @@ def tuned_table() -> dict:
 
 
 def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wout: int, N: int,
-                  rows_per_group: Optional[int] = None, bkn: bool = False) -> Optional[Tuple[int, int]]:
+                  rows_per_group: Optional[int] = None, bkn: bool = False,
+                  dtype: int = 0) -> Optional[Tuple[int, int]]:
     """(cfg, splits) for one implicit-GEMM launch: the tuned entry when present and legal
     (weight layout, BN-statistics grouping), else the heuristics. None when no tile can
-    produce group-aligned statistics (caller computes them in a separate pass)."""
+    produce group-aligned statistics (caller computes them in a separate pass). dtype 2 =
+    the fp32 build (its own tile family, no tuned table)."""
     if mode == 1:
         M, phases, taps = Bn * (-(-Hout // 2)) * (-(-Wout // 2)), 4, 9
     else:
         M, phases, taps = Bn * Hout * Wout, 1, (25 if mode == 0 else 1)
+    if dtype == 2:
+        if mode == 1 and rows_per_group is not None:
+            return None
+        return pick_igemm_f32(M, N, phases, rows_per_group)
     ent = tuned_table().get("%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N))
     if ent is not None:
         cfg, sp = ent
@@ -184,8 +211,14 @@ def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wo
     return None if c is None else (c, 1)
 
 
-def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_COUNT) -> Tuple[int, int]:
-    """(cfg, splits) for a weight-gradient GEMM of Mc x Nc per tap over K pixels."""
+def pick_wgrad(Mc: int, Nc: int, K: int, taps: int, target_blocks: int = 4 * CU_COUNT,
+               dtype: int = 0) -> Tuple[int, int]:
+    """(cfg, splits) for a weight-gradient GEMM of Mc x Nc per tap over K pixels (dtype 2:
+    the fp32 kernel, one 64x64 tile for every cfg)."""
+    if dtype == 2:
+        tiles = -(-Mc // 64) * -(-Nc // 64) * taps
+        kt = -(-K // 64)
+        return 3, max(1, min(-(-target_blocks // tiles), max(1, kt // (16 if taps == 1 else 4))))
     if Mc >= 128 and Nc >= 128:
         cfg = 0
     elif Mc < 128 and Nc >= 128:

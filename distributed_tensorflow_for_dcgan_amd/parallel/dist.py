@@ -182,14 +182,28 @@ class GradAllReducer:
         else:
             ctx = _nullctx()
         with ctx:
-            for s, e in self.buckets:
-                if self.wire is not None:
-                    w = self.wire[s:e]
-                    w.copy_(self.flat[s:e])
-                    dist.all_reduce(w, op=dist.ReduceOp.SUM)
-                    self.flat[s:e].copy_(w)
-                else:
-                    dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM)
+            self.issue()
+
+    def issue(self) -> None:
+        """The bucket collectives on the CURRENT stream (the caller has ordered it after the
+        producers of the gradients; the HIP engine's executor does this)."""
+        if self.world <= 1:
+            return
+        for s, e in self.buckets:
+            if self.wire is not None:
+                w = self.wire[s:e]
+                w.copy_(self.flat[s:e])
+                dist.all_reduce(w, op=dist.ReduceOp.SUM)
+                self.flat[s:e].copy_(w)
+            else:
+                dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM)
+
+    def accesses(self):
+        """(ptr, bytes, is_write) ranges one issue() touches (schedule checker)."""
+        out = [(self.flat.data_ptr(), self.flat.numel() * self.flat.element_size(), True)]
+        if self.wire is not None:
+            out.append((self.wire.data_ptr(), self.wire.numel() * self.wire.element_size(), True))
+        return out
 
     def wait(self, scale_in_place: bool = True) -> None:
         if self.world <= 1:

@@ -68,8 +68,9 @@ def run(flags: Flags, out=None) -> int:
     cfg = config_from_flags(flags)
     B = int(flags.batch_size)
     shape = (cfg.output_size, cfg.output_size, cfg.c_dim)
-    if flags.verbose and chief:
-        print("device %s rank %d/%d engine %s" % (device, rank, world, flags.engine), file=out)
+    if flags.verbose:
+        print("device %s rank %d/%d local_rank %d (%s) engine %s" % (device, rank, world, cl["local_rank"],
+                                                                   cl["source"], flags.engine), file=out, flush=True)
 
     engine = build_engine(cfg, B, device, engine=flags.engine, dtype=flags.dtype, seed=int(flags.seed), rank=rank,
                           world=world, graph=bool(flags.graph), allreduce_dtype=flags.allreduce_dtype,

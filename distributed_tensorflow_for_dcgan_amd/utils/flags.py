@@ -44,7 +44,7 @@ REFERENCE_FLAGS: List[Tuple[str, str, Any, str]] = [
 
 # Additive flags of this framework (not in the reference).
 EXTRA_FLAGS: List[Tuple[str, str, Any, str]] = [
-    ("dtype", "str", "bf16", "compute dtype: bf16 | fp16 (dynamic loss scaling) | fp32 (reference engine)"),
+    ("dtype", "str", "bf16", "compute dtype: bf16 | fp16 (dynamic loss scaling) | fp32 (reference precision)"),
     ("device", "str", "auto", "auto | cpu | cuda (cuda == the local MI355X via HIP)"),
     ("synthetic", "bool", False, "use synthetic images of the configured shape instead of TFRecords"),
     ("max_steps", "int", 1200000, "stop after this many global steps (reference hard-codes 1,200,000)"),
@@ -192,15 +192,19 @@ def cluster_from_flags(flags: Flags) -> Dict[str, Any]:
             "master_port": int(env.get("MASTER_PORT", "29500")),
             "source": "env",
         }
-    workers = [w for w in flags.worker_hosts.split(",") if w.strip()] if flags.worker_hosts else []
+    workers = [w.strip() for w in flags.worker_hosts.split(",") if w.strip()] if flags.worker_hosts else []
     if len(workers) > 1:
         host, _, port = workers[0].rpartition(":")
         if flags.task_index < 0 or flags.task_index >= len(workers):
             raise ValueError("--task_index=%d out of range for %d workers" % (flags.task_index, len(workers)))
+        # one process per GPU: this worker's GPU is its index among the workers listed for the
+        # same host (reference launches N workers on one box as N --worker_hosts entries)
+        my_host = workers[flags.task_index].rpartition(":")[0]
+        local = sum(1 for w in workers[:flags.task_index] if w.rpartition(":")[0] == my_host)
         return {
             "rank": flags.task_index,
             "world_size": len(workers),
-            "local_rank": int(env.get("LOCAL_RANK", "0")),
+            "local_rank": int(env.get("LOCAL_RANK", str(local))),
             "master_addr": host or "127.0.0.1",
             "master_port": int(port or 29500),
             "source": "worker_hosts",

@@ -125,3 +125,27 @@ def test_launcher_restarts_after_fault_and_resumes(tmp_path):
     assert "[launch] restart 1/2" in p.stdout
     assert "global_step 10" in p.stdout  # resumed
     assert os.path.exists(tmp_path / "ck" / "model.ckpt-14.index")
+
+
+def test_reference_style_worker_hosts_launch(tmp_path):
+    """The reference's own launch form (image_train.py:52-66): one process per worker, cluster
+    given by --worker_hosts/--task_index, no torchrun environment. Both workers train together
+    (gloo on CPU here) and worker 1 maps to local GPU index 1."""
+    p0, p1 = _free_port(), _free_port()
+    hosts = "127.0.0.1:%d,127.0.0.1:%d" % (p0, p1)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, OMP_NUM_THREADS="2")
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+            env.pop(k, None)
+        cmd = [sys.executable, os.path.join(ROOT, "image_train.py"), "--job_name=worker", "--task_index=%d" % r,
+               "--worker_hosts=" + hosts, "--ps_hosts=127.0.0.1:%d" % _free_port(), "--synthetic",
+               "--output_size=28", "--c_dim=1", "--batch_size=4", "--max_steps=2", "--device=cpu", "--verbose",
+               "--checkpoint_dir=%s" % (tmp_path / "ck"), "--sample_dir=%s" % (tmp_path / "s"),
+               "--save_summaries_secs=1000", "--sample_every=0", "--check_sync_every=1"]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=600)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "rank 0/2 local_rank 0 (worker_hosts)" in outs[0]
+    assert "rank 1/2 local_rank 1 (worker_hosts)" in outs[1]
+    assert "Epoch: [ 0] step: [ 2]" in outs[0]

@@ -45,6 +45,11 @@ def test_cluster_mapping(monkeypatch):
                         "--ps_hosts=127.0.0.1:2221"])
     c = F.cluster_from_flags(fl)
     assert c["world_size"] == 2 and c["rank"] == 1 and c["master_port"] == 2222
+    assert c["local_rank"] == 1  # second worker listed for this host -> second GPU
+    fl2 = F.parse_flags(["--task_index=2", "--worker_hosts=hostA:1,hostB:1,hostA:2,hostB:2"])
+    assert F.cluster_from_flags(fl2)["local_rank"] == 1
+    fl3 = F.parse_flags(["--task_index=1", "--worker_hosts=hostA:1,hostB:1,hostA:2,hostB:2"])
+    assert F.cluster_from_flags(fl3)["local_rank"] == 0
     monkeypatch.setenv("RANK", "3")
     monkeypatch.setenv("WORLD_SIZE", "8")
     monkeypatch.setenv("LOCAL_RANK", "3")

@@ -1,0 +1,83 @@
+"""CPU tests of the stream-hazard checker (engine/schedule_check.py): every schedule of the HIP
+engine, for every element type, single process and DDP, is free of unordered overlapping
+accesses -- and the checker does find the round-1 race when it is re-introduced."""
+import pytest
+import torch
+
+from distributed_tensorflow_for_dcgan_amd.engine import schedule_check as SC
+from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+
+CASES = [(1, None, False), (1, None, True), (1, "serial", False), (2, None, False), (2, "serial", False)]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("world,schedule,timing", CASES)
+def test_schedule_has_no_stream_hazards(dtype, world, schedule, timing):
+    sched, hz, n = SC.check(DCGANConfig(), 4, dtype, world, schedule, timing)
+    expect = schedule or ("fused" if world == 1 and not timing else "concurrent")
+    assert sched == expect
+    assert n > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+@pytest.mark.parametrize("size", [28, 128])
+def test_other_resolutions_have_no_stream_hazards(size):
+    c = 1 if size == 28 else 3
+    for world, schedule, timing in ((1, None, False), (2, None, False)):
+        _, hz, _ = SC.check(DCGANConfig(output_size=size, c_dim=c), 2, "bf16", world, schedule, timing)
+        assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def _dry(world=1, timing=False):
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=world, dry_run=True, graph=False)
+    if timing:
+        eng._timing = True
+        eng._build_updates()
+    return eng
+
+
+def test_checker_finds_the_round1_adam_race():
+    """Round 1: at W=1 with --timing the concurrent schedule kept the fused two-model Adam in
+    its "adam_G" segment, which runs before the main stream joins the D chain."""
+    eng = _dry(timing=True)
+    assert eng._schedule() == "concurrent"
+    hz, _ = SC.check_engine(eng)
+    assert hz == []
+    eng.progC = eng._prog()
+    eng._build_update_fused(eng.progC)   # the round-1 program
+    eng._c_split = eng.progC.size()      # ... all of it in "adam_G"
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed the Adam(D) / D-backward race"
+    txt = "\n".join(map(str, hz))
+    assert "adam_gd" in txt and "alt0" in txt
+
+
+def test_checker_finds_a_missing_join():
+    """Dropping the join of the D chain before the update is reported."""
+    eng = _dry()
+
+    def bad_fused(ex, cs):
+        ex.run(eng.progA, [cs, ex.side], 0, eng._a_fwd)
+        ex.wait(ex.alt[0], cs)
+        ex.run(eng.progB, ex.alt)
+        ex.run(eng.progA, [cs, ex.side], eng._a_fwd, -1)
+        ex.run(eng.progC, [cs, ex.side])  # no ex.wait(cs, alt0)
+
+    eng._run_fused = bad_fused
+    hz, _ = SC.check_engine(eng)
+    assert any("adam" in h.a or "adam" in h.b for h in hz)
+
+
+def test_op_accesses_are_recorded():
+    eng = _dry()
+    names = set()
+    for p in (eng.progA, eng.progB, eng.progC):
+        for i in range(p.size()):
+            name, slot, kind, ev, acc = p.op_info(i)
+            names.add(name)
+            if kind == eng.ext.OP_LAUNCH:
+                assert acc, "op %s records no accesses" % name
+                assert all(n > 0 for _, n, _ in acc)
+    assert "adam_gd" in names and "d_head+loss" in names
+    assert eng.kernel_count() == sum(p.size() for p in (eng.progA, eng.progB, eng.progC))
