@@ -49,10 +49,13 @@ def shapes(cfg: DCGANConfig, B: int):
     return out
 
 
+V1 = False  # --v1: also time the first-generation igemm.hip tiles
+
+
 def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     """[(cfg, splits)] worth timing for one GEMM."""
     out = []
-    if not bkn:  # igemm.hip reads k-contiguous weights only
+    if not bkn and V1:  # igemm.hip reads k-contiguous weights only
         for c, (bm, bn) in H.IGEMM_CFGS.items():
             if (N <= 16) != (bn == 16):
                 continue
@@ -64,8 +67,8 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     phases = 4 if mode == 1 else 1
     M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
     kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
-    for c in range(200, 216):
-        if c % 10 not in H.IGEMM3_TILES:
+    for c in range(200, 240):
+        if c % 10 not in H.IGEMM3_TILES or H.igemm3_lds(c) > 160 * 1024:
             continue
         bm, bn = H.IGEMM3_TILES[c % 10]
         if bn > N:
@@ -93,9 +96,14 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--inner", type=int, default=8, help="launches per timed event pair")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--v1", action="store_true", help="also time igemm.hip (v1) tiles")
+    ap.add_argument("--out", default="", help="also write this run's table (JSON) here")
     a = ap.parse_args()
+    global V1
+    V1 = a.v1
     cfg = DCGANConfig(output_size=a.size)
     ext = H.ext()
     dev = torch.device("cuda", 0)
@@ -113,6 +121,9 @@ def main():
         stats = torch.empty(1 << 22, device=dev)
         fl = flops(mode, Bn, Hin, Win, Kc, Hout, Wout, N)
         cands = candidates(mode, Bn, Hout, Wout, Kc, N, bkn)
+        if not cands:
+            print("%-22s (no igemm3 tile: N=%d)" % (name, N))
+            continue
         progs = {}
         for (c, sp) in cands:
             p = ext.Program()
@@ -127,15 +138,19 @@ def main():
         torch.cuda.synchronize()
         for _ in range(a.reps):
             for c in cands:
+                # `inner` back-to-back launches per event pair: the host launch latency of the
+                # first one is not counted against the kernel (the queue stays full after it)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
                 H.run(progs[c])
+                e0.record(s)
+                for _ in range(a.inner):
+                    H.run(progs[c])
                 e1.record(s)
                 times[c].append((e0, e1))
         torch.cuda.synchronize()
         res = []
         for c in cands:
-            ts = sorted(e0.elapsed_time(e1) for e0, e1 in times[c])
+            ts = sorted(e0.elapsed_time(e1) / a.inner for e0, e1 in times[c])
             med = ts[len(ts) // 2] * 1e3
             res.append((med, c))
         res.sort()
@@ -146,6 +161,8 @@ def main():
                H.tile_of(bc), best[0], fl / best[0] / 1e6) +
               " ".join("%d:%d:%.0f" % (c[0], c[1], t) for t, c in res[:6]), flush=True)
         table["%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N)] = "%d:%d" % (bc, bsp)
+    if a.out:
+        json.dump(table, open(a.out, "w"), indent=1, sort_keys=True)
     if a.write:
         path = os.path.join(os.path.dirname(H.__file__), "igemm_tuned.json")
         old = {}

@@ -121,7 +121,9 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   const int kt1 = min(KT, kt0 + kps);
   const int nk = max(0, kt1 - kt0);
 
-  // ablation (timing only, outputs wrong): a zero-size descriptor drops every load through it
+  // ablation (timing only, outputs wrong): bit 0 / 1 a zero-size descriptor drops every A / B
+  // fetch (the LDS-DMA still writes zeros), bit 2 skips fragment reads + MFMAs, bit 3 skips the
+  // LDS-DMA issue altogether
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, (p.ablate & 1) ? 0u : p.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, (p.ablate & 2) ? 0u : p.b_bytes);
 
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(s);
+    if (s < nk && !(p.ablate & 8)) issue(s);
 
   const int fr = lane & 15, fq = lane >> 4;
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
@@ -225,7 +227,8 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     // younger DMA tiles and flattens the pipeline (LDS reads of the previous tile have all
     // returned: their values fed the MFMAs already).
     asm volatile("s_barrier" ::: "memory");
-    if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS);
+    if (kt + NS - 1 < nk && !(p.ablate & 8)) issue((kt + NS - 1) % NS);
+    if (p.ablate & 4) continue;  // timing study: no fragment reads / MFMAs
     const char* sa = lds + (kt % NS) * STAGE;
     const char* sb = sa + A_BYTES;
     // all fragments of the k-tile first (both k32 halves: the second half's LDS reads are in
@@ -400,16 +403,22 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 }  // namespace dcg
 
 // ---------------------------------------------------------------------------- host launch
-// v3 configs: cfg = 200 + 10 * (3 - NS) + id  (NS = 3 -> 200..209, NS = 2 -> 210..219)
+// v3 configs: cfg = 200 + 10 * k + id, LDS stages NS = {3, 2, 4, 5}[k]  (NS = 3 -> 200..209,
+// NS = 2 -> 210..219, NS = 4 -> 220..229, NS = 5 -> 230..239). Deeper rings keep more k-tiles of
+// LDS-DMA in flight (issue -> landed is ~1.1 us, several k-tiles of MFMA work), at the cost of
+// workgroups per CU (160 KiB of LDS per CU).
 #define DCG_IGEMM3_TILES(X) \
   X(0, 128, 128, 2, 2) X(1, 256, 64, 4, 1) X(2, 64, 256, 1, 4) X(3, 128, 64, 2, 2) \
   X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2)
 
+static constexpr int kIgemm3Stages[4] = {3, 2, 4, 5};
+
 extern "C" int DCG_API(dcg_igemm3_tile)(int cfg, int* bm, int* bn, int* ns) {
-  if (cfg < 200 || cfg >= 220) return -1;
+  if (cfg < 200 || cfg >= 240) return -1;
   const int id = cfg % 10;
-  *ns = cfg < 210 ? 3 : 2;
-#define X(id_, BM_, BN_, WM_, WN_) if (id == id_) { *bm = BM_; *bn = BN_; return 0; }
+  *ns = kIgemm3Stages[(cfg - 200) / 10];
+#define X(id_, BM_, BN_, WM_, WN_) \
+  if (id == id_) { *bm = BM_; *bn = BN_; return (size_t)*ns * (BM_ + BN_) * 128 <= 160 * 1024 ? 0 : -1; }
   DCG_IGEMM3_TILES(X)
 #undef X
   return -1;
@@ -433,12 +442,24 @@ extern "C" int DCG_API(dcg_igemm3_launch)(const dcg::IGemmArgs* a, int cfg, int 
   int bm, bn, ns;
   if (DCG_API(dcg_igemm3_tile)(cfg, &bm, &bn, &ns)) return -1;
   const int id = cfg % 10;
-#define X(id_, BM_, BN_, WM_, WN_)                                              \
-  if (id == id_) {                                                              \
-    if (ns == 3) return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 3>(a, blocks, s)   \
-                            : launch3<BM_, BN_, WM_, WN_, 0, 3>(a, blocks, s);  \
-    return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 2>(a, blocks, s)                \
-               : launch3<BM_, BN_, WM_, WN_, 0, 2>(a, blocks, s);               \
+#define X(id_, BM_, BN_, WM_, WN_)                                                              \
+  if (id == id_) {                                                                              \
+    if (ns == 3) return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 3>(a, blocks, s)                   \
+                            : launch3<BM_, BN_, WM_, WN_, 0, 3>(a, blocks, s);                  \
+    if (ns == 4) {                                                                              \
+      if constexpr ((size_t)4 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
+        return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 4>(a, blocks, s)                            \
+                   : launch3<BM_, BN_, WM_, WN_, 0, 4>(a, blocks, s);                           \
+      return -1;                                                                                \
+    }                                                                                           \
+    if (ns == 5) {                                                                              \
+      if constexpr ((size_t)5 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
+        return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 5>(a, blocks, s)                            \
+                   : launch3<BM_, BN_, WM_, WN_, 0, 5>(a, blocks, s);                           \
+      return -1;                                                                                \
+    }                                                                                           \
+    return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 2>(a, blocks, s)                                \
+               : launch3<BM_, BN_, WM_, WN_, 0, 2>(a, blocks, s);                               \
   }
   DCG_IGEMM3_TILES(X)
 #undef X

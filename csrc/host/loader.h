@@ -4,11 +4,13 @@
 // self-test (tests/native/host_selftest.cpp) drives it directly under ASan/UBSan and TSan.
 //
 // * reader threads pull file names from an epoch-shuffled list (infinite epochs when `loop`),
-//   read TFRecords (CRC-checked), extract the `image_raw` bytes feature, decode raw float64 /
-//   float32 / uint8 pixels and convert them ONCE into the output dtype (fp32 or bf16, uint8
-//   rescaled by scale/shift) into a slot of a fixed-capacity example pool;
+//   read TFRecords (CRC-checked), extract the `image_raw` bytes feature, and decode raw float64 /
+//   float32 / uint8 pixels ONCE, straight into a reserved slot of a fixed-capacity example pool,
+//   in the training dtype (fp32, bf16 or fp16; uint8 rescaled by scale/shift) -- so a bf16 run
+//   ships half the bytes over H2D;
 // * next_batch() waits until min_after_dequeue + batch examples are pooled (RandomShuffleQueue
-//   semantics), then draws `batch` uniformly random slots into the caller's buffer.
+//   semantics), then draws `batch` uniformly random slots and copies them into the caller's
+//   buffer outside the lock.
 // With threads == 1 the order is a deterministic function of the seed.
 #pragma once
 #include <algorithm>
@@ -39,6 +41,34 @@ static inline uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// IEEE binary16, round to nearest even (images are in [-1, 1]: no overflow handling needed
+// beyond saturation to inf)
+static inline uint16_t f2h(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const int32_t e = (int32_t)((u >> 23) & 0xFF) - 127 + 15;
+  uint32_t m = u & 0x7FFFFFu;
+  if (((u >> 23) & 0xFF) == 0xFF) return (uint16_t)(sign | 0x7C00u | (m ? 0x200u : 0u));
+  if (e >= 31) return (uint16_t)(sign | 0x7C00u);
+  if (e <= 0) {  // subnormal half
+    if (e < -10) return (uint16_t)sign;
+    m |= 0x800000u;
+    const int shift = 14 - e;
+    uint32_t h = m >> shift;
+    const uint32_t rem = m & ((1u << shift) - 1), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+  }
+  uint32_t h = ((uint32_t)e << 10) | (m >> 13);
+  const uint32_t rem = m & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+
+enum SrcType { SRC_AUTO = 0, SRC_F64, SRC_F32, SRC_U8 };
+enum OutType { OUT_F32 = 0, OUT_BF16, OUT_F16 };
+
 class Loader {
  public:
   Loader(std::vector<std::string> files, std::string feature, int H, int W, int C, int batch, int capacity,
@@ -48,10 +78,15 @@ class Loader {
         min_after_(std::max(0, min_after_dequeue)), loop_(loop), verify_(verify_crc), u8_scale_(u8_scale),
         u8_shift_(u8_shift), rng_(seed), file_rng_(seed ^ 0x9E3779B97F4A7C15ull) {
     if (files_.empty()) throw std::runtime_error("Loader: no input files");
-    if (out_dtype == "f32") out_bytes_ = 4;
-    else if (out_dtype == "bf16") out_bytes_ = 2;
-    else throw std::runtime_error("out_dtype must be f32 or bf16");
-    src_ = src_dtype;
+    if (out_dtype == "f32") { out_bytes_ = 4; out_ = OUT_F32; }
+    else if (out_dtype == "bf16") { out_bytes_ = 2; out_ = OUT_BF16; }
+    else if (out_dtype == "f16") { out_bytes_ = 2; out_ = OUT_F16; }
+    else throw std::runtime_error("out_dtype must be f32, bf16 or f16");
+    if (src_dtype == "auto") src_ = SRC_AUTO;
+    else if (src_dtype == "f64") src_ = SRC_F64;
+    else if (src_dtype == "f32") src_ = SRC_F32;
+    else if (src_dtype == "u8") src_ = SRC_U8;
+    else throw std::runtime_error("src_dtype must be auto, f64, f32 or u8");
     capacity_ = std::max(capacity, min_after_ + batch_);
     pool_.resize((size_t)capacity_ * elems_ * out_bytes_);
     free_.reserve(capacity_);
@@ -83,19 +118,24 @@ class Loader {
              (done_workers_ == (int)workers_.size());
     });
     if (!error_.empty()) throw std::runtime_error(error_);
-    int n = 0;
-    const size_t ebytes = elems_ * out_bytes_;
-    while (n < batch_ && !filled_.empty()) {
+    // draw the batch's slots under the lock (RandomShuffleQueue semantics), copy them out with
+    // the lock released (the readers keep decoding meanwhile), then hand the slots back
+    std::vector<int>& taken = taken_;
+    taken.clear();
+    while ((int)taken.size() < batch_ && !filled_.empty()) {
       std::uniform_int_distribution<size_t> dist(0, filled_.size() - 1);
       const size_t k = dist(rng_);
-      const int slot = filled_[k];
+      taken.push_back(filled_[k]);
       filled_[k] = filled_.back();
       filled_.pop_back();
-      std::memcpy(dst + (size_t)n * ebytes, pool_.data() + (size_t)slot * ebytes, ebytes);
-      free_.push_back(slot);
-      ++n;
     }
+    const int n = (int)taken.size();
     dequeued_ += n;
+    lk.unlock();
+    const size_t ebytes = elems_ * out_bytes_;
+    for (int i = 0; i < n; ++i) std::memcpy(dst + (size_t)i * ebytes, pool_.data() + (size_t)taken[i] * ebytes, ebytes);
+    lk.lock();
+    for (int i = 0; i < n; ++i) free_.push_back(taken[i]);
     lk.unlock();
     cv_.notify_all();
     return n;
@@ -127,37 +167,47 @@ class Loader {
     return true;
   }
 
-  void decode_into(const uint8_t* raw, size_t len, uint8_t* dst) {
-    std::string src = src_;
-    if (src == "auto") {
-      if (len == elems_ * 8) src = "f64";
-      else if (len == elems_ * 4) src = "f32";
-      else if (len == elems_) src = "u8";
+  // raw pixels -> output dtype, one tight loop per (source, output) pair; the source type is
+  // resolved per record from the payload size when "auto" (float64 is the reference's format,
+  // image_input.py:48)
+  template <typename Src>
+  void emit(const uint8_t* raw, uint8_t* dst, Src src) const {
+    const size_t n = elems_;
+    if (out_ == OUT_F32) {
+      float* o = reinterpret_cast<float*>(dst);
+      for (size_t i = 0; i < n; ++i) o[i] = src(raw, i);
+    } else if (out_ == OUT_BF16) {
+      uint16_t* o = reinterpret_cast<uint16_t*>(dst);
+      for (size_t i = 0; i < n; ++i) o[i] = f2bf(src(raw, i));
+    } else {
+      uint16_t* o = reinterpret_cast<uint16_t*>(dst);
+      for (size_t i = 0; i < n; ++i) o[i] = f2h(src(raw, i));
+    }
+  }
+  void decode_into(const uint8_t* raw, size_t len, uint8_t* dst) const {
+    SrcType src = src_;
+    if (src == SRC_AUTO) {
+      if (len == elems_ * 8) src = SRC_F64;
+      else if (len == elems_ * 4) src = SRC_F32;
+      else if (len == elems_) src = SRC_U8;
       else throw std::runtime_error("image_raw has " + std::to_string(len) + " bytes, expected " +
                                     std::to_string(elems_) + " x {1,4,8}");
+    } else if (len != elems_ * (src == SRC_F64 ? 8 : src == SRC_F32 ? 4 : 1)) {
+      throw std::runtime_error("image_raw has " + std::to_string(len) + " bytes, not the declared dtype's size");
     }
-    for (size_t i = 0; i < elems_; ++i) {
-      float v;
-      if (src == "f64") {
-        double d;
-        std::memcpy(&d, raw + 8 * i, 8);
-        v = (float)d;
-      } else if (src == "f32") {
-        std::memcpy(&v, raw + 4 * i, 4);
-      } else {
-        v = raw[i] * u8_scale_ + u8_shift_;
-      }
-      if (out_bytes_ == 4) std::memcpy(dst + 4 * i, &v, 4);
-      else {
-        const uint16_t b = f2bf(v);
-        std::memcpy(dst + 2 * i, &b, 2);
-      }
+    if (src == SRC_F64) {
+      emit(raw, dst, [](const uint8_t* r, size_t i) { double d; std::memcpy(&d, r + 8 * i, 8); return (float)d; });
+    } else if (src == SRC_F32) {
+      emit(raw, dst, [](const uint8_t* r, size_t i) { float f; std::memcpy(&f, r + 4 * i, 4); return f; });
+    } else {
+      const float sc = u8_scale_, sh = u8_shift_;
+      emit(raw, dst, [sc, sh](const uint8_t* r, size_t i) { return r[i] * sc + sh; });
     }
   }
 
   void work() {
     std::string fname, rec;
-    std::vector<uint8_t> tmp(elems_ * out_bytes_);
+    const size_t ebytes = elems_ * out_bytes_;
     try {
       while (take_file(&fname)) {
         RecordReader rr(fname, verify_);
@@ -166,19 +216,29 @@ class Loader {
           size_t len = 0;
           if (!example_bytes_feature(reinterpret_cast<const uint8_t*>(rec.data()), rec.size(), feature_, &p, &len))
             throw std::runtime_error("record without bytes feature '" + feature_ + "' in " + fname);
-          decode_into(p, len, tmp.data());
-          std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [this] { return stop_ || !free_.empty(); });
-          if (stop_) {
-            lk.unlock();
-            return finish();
+          int slot;
+          {  // reserve a free slot, decode into it with the lock released
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [this] { return stop_ || !free_.empty(); });
+            if (stop_) {
+              lk.unlock();
+              return finish();
+            }
+            slot = free_.back();
+            free_.pop_back();
           }
-          const int slot = free_.back();
-          free_.pop_back();
-          std::memcpy(pool_.data() + (size_t)slot * tmp.size(), tmp.data(), tmp.size());
-          filled_.push_back(slot);
-          ++records_;
-          lk.unlock();
+          try {
+            decode_into(p, len, pool_.data() + (size_t)slot * ebytes);
+          } catch (...) {
+            std::lock_guard<std::mutex> g(mu_);
+            free_.push_back(slot);
+            throw;
+          }
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            filled_.push_back(slot);
+            ++records_;
+          }
           cv_.notify_all();
         }
       }
@@ -198,7 +258,10 @@ class Loader {
   }
 
   std::vector<std::string> files_;
-  std::string feature_, src_;
+  std::string feature_;
+  SrcType src_ = SRC_AUTO;
+  OutType out_ = OUT_F32;
+  std::vector<int> taken_;
   size_t elems_;
   int batch_, min_after_, capacity_;
   bool loop_, verify_;

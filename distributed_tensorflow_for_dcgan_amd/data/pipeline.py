@@ -22,6 +22,16 @@ import torch
 from . import tfrecord as TR
 
 NUM_EXAMPLES_PER_EPOCH_FOR_TRAIN = 107766  # reference image_input.py:14
+LOADER_DTYPE = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16"}
+ENGINE_DTYPE = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def batch_dtype(flags, device) -> torch.dtype:
+    """The dtype batches are decoded into: the training compute dtype on a GPU (bf16 batches
+    halve the H2D bytes and need no on-device cast), fp32 on the CPU."""
+    if torch.device(device).type != "cuda":
+        return torch.float32
+    return ENGINE_DTYPE.get(str(getattr(flags, "dtype", "bf16")), torch.float32)
 
 
 class SyntheticSource:
@@ -75,7 +85,7 @@ class TFRecordSource:
         self.loader = native.ext().Loader(self.files, feature, H, W, C, batch, cap, shuffle_buffer, threads,
                                           int(seed) * 1000003 + rank, out_dtype, "auto", loop, True,
                                           1.0 / 127.5, -1.0)
-        tdtype = torch.float32 if out_dtype == "f32" else torch.bfloat16
+        tdtype = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[out_dtype]
         pin = self.device.type == "cuda"
         self._host = [torch.empty((batch,) + self.shape, dtype=tdtype, pin_memory=pin) for _ in range(prefetch)]
         self._dev = [torch.empty((batch,) + self.shape, dtype=tdtype, device=self.device) for _ in range(prefetch)]
@@ -179,8 +189,8 @@ class DeviceCachedSource:
         self.data = torch.empty((n,) + self.shape, dtype=dtype, device=self.device)
         chunk = max(batch, 256)
         loader = native.ext().Loader(self.files, feature, H, W, C, chunk, chunk, 0, threads, int(seed) + rank,
-                                     "f32", "auto", False, True, 1.0 / 127.5, -1.0)
-        host = torch.empty((chunk,) + self.shape, dtype=torch.float32, pin_memory=self.device.type == "cuda")
+                                     LOADER_DTYPE[dtype], "auto", False, True, 1.0 / 127.5, -1.0)
+        host = torch.empty((chunk,) + self.shape, dtype=dtype, pin_memory=self.device.type == "cuda")
         filled = 0
         try:
             while filled < n:
@@ -278,9 +288,11 @@ def make_source(flags, batch: int, shape, device, rank: int = 0, world: int = 1,
             return ImageFolderSource(d, batch, shape, device, is_crop=bool(flags.is_crop),
                                      image_size=int(flags.image_size), rank=rank, world=world,
                                      shard=bool(flags.shard_data), seed=seed)
+    dt = batch_dtype(flags, device)
     if bool(getattr(flags, "cache_on_device", False)) and data_dir is None:
         return DeviceCachedSource(d, batch, shape, device, rank=rank, world=world, shard=bool(flags.shard_data),
-                                  seed=seed, threads=int(flags.loader_threads))
+                                  seed=seed, threads=int(flags.loader_threads), dtype=dt)
     sb = int(flags.shuffle_buffer) if shuffle_buffer is None else shuffle_buffer
     return TFRecordSource(d, batch, shape, device, rank=rank, world=world, shard=bool(flags.shard_data),
-                          shuffle_buffer=sb, threads=int(flags.loader_threads), seed=seed, loop=loop)
+                          shuffle_buffer=sb, threads=int(flags.loader_threads), seed=seed, loop=loop,
+                          out_dtype=LOADER_DTYPE[dt])

@@ -70,6 +70,14 @@ CU_COUNT = 256
 IGEMM_CFGS = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (32, 64), 5: (64, 32),
               6: (32, 32), 7: (128, 16), 8: (64, 16), 9: (256, 64)}
 IGEMM3_TILES = {0: (128, 128), 1: (256, 64), 2: (64, 256), 3: (128, 64), 4: (64, 128), 5: (64, 64)}
+IGEMM3_STAGES = (3, 2, 4, 5)  # LDS stages of igemm3 cfg 200+10k+id
+
+
+def igemm3_lds(cfg: int) -> int:
+    bm, bn = IGEMM3_TILES[cfg % 10]
+    return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
+
+
 # fp32 build (igemm_f32.hip): the only tile family of that element type, cfg 200..203
 IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)}
 
@@ -103,7 +111,7 @@ def pick_igemm_f32(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
 def bnb_fits(cfg: int) -> bool:
     """True when the tile's LDS can hold the fused BN-backward statistics scratch (epilogue.h)."""
     bm, bn = tile_of(cfg)
-    ns = (3 if cfg < 210 else 2) if cfg >= 200 else 2
+    ns = IGEMM3_STAGES[(cfg - 200) // 10] if cfg >= 200 else 2
     return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= ns * (bm + bn) * 128
 
 

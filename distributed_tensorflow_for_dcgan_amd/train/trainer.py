@@ -35,6 +35,54 @@ from ..utils.flags import Flags, cluster_from_flags
 
 STEP_LINE = "Epoch: [%2d] step: [%2d] time: %4.4f, d_loss: %.8f, g_loss: %.8f"
 SYNC_EVERY = 10  # steps between collective checks of the chief's time-based save decision
+LOSS_KEYS = ("d_loss_real", "d_loss_fake", "g_loss", "d_loss")
+
+
+class AsyncLossLog:
+    """The reference prints its step line after every ``sess.run`` (image_train.py:160-162),
+    which on a GPU engine means a host sync per step. Here the device loss vector is copied into
+    a small ring of pinned host buffers without blocking (``non_blocking`` copy + event); a line
+    is printed once its copy has landed -- normally one step later -- so the training stream
+    never waits for the host. Engines without a device loss tensor are read synchronously."""
+
+    def __init__(self, engine, device, depth: int = 8):
+        self.engine = engine
+        self.async_ = device.type == "cuda" and hasattr(engine, "losses_tensor")
+        self.pending = []   # (meta, event, pinned buffer), oldest first
+        self.landed = []    # (meta, values) taken out of a full ring
+        self.free = ([torch.empty(4, dtype=torch.float32, pin_memory=True) for _ in range(depth)]
+                     if self.async_ else [])
+
+    def push(self, meta) -> None:
+        if not self.async_:
+            L = self.engine.last_losses()
+            self.landed.append((meta, [L[k] for k in LOSS_KEYS]))
+            return
+        if not self.free:  # ring full (the GPU is far behind): retire the oldest copy
+            m, ev, buf = self.pending.pop(0)
+            ev.synchronize()
+            self.landed.append((m, buf.tolist()))
+            self.free.append(buf)
+        buf = self.free.pop()
+        buf.copy_(self.engine.losses_tensor(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((meta, ev, buf))
+
+    def ready(self, flush: bool = False):
+        """(meta, losses dict) of every landed entry, oldest first (all of them when flush)."""
+        out = [(m, dict(zip(LOSS_KEYS, v))) for m, v in self.landed]
+        self.landed = []
+        while self.pending:
+            meta, ev, buf = self.pending[0]
+            if flush:
+                ev.synchronize()
+            elif not ev.query():
+                break
+            self.pending.pop(0)
+            out.append((meta, dict(zip(LOSS_KEYS, buf.tolist()))))
+            self.free.append(buf)
+        return out
 
 
 def _device(flags: Flags, local_rank: int) -> torch.device:
@@ -125,6 +173,13 @@ def run(flags: Flags, out=None) -> int:
     start_time = time.time()
     next_summary = start_time + float(flags.save_summaries_secs)
     last_rate_t, last_rate_step = start_time, step
+    losslog = AsyncLossLog(engine, device)
+
+    def emit(entries):
+        for (st, t, ips), L in entries:
+            print(STEP_LINE % (st // step_per_epoch, st % step_per_epoch, t, L["d_loss"], L["g_loss"]) +
+                  ", images/sec: %.1f" % ips, file=out, flush=True)
+
     try:
         while step < max_steps:
             if prof_range and step == prof_range[0] and prof is None:
@@ -141,14 +196,14 @@ def run(flags: Flags, out=None) -> int:
             now = time.time()
             summary_due = chief and writer is not None and now >= next_summary
             if step % max(1, int(flags.log_every)) == 0 or summary_due or step == max_steps:
-                L = engine.last_losses()
                 ips = B * world * (step - last_rate_step) / max(1e-9, now - last_rate_t) if step > last_rate_step else 0.0
-                print(STEP_LINE % (step // step_per_epoch, step % step_per_epoch, now - start_time,
-                                   L["d_loss"], L["g_loss"]) + ", images/sec: %.1f" % ips, file=out, flush=True)
+                losslog.push((step, now - start_time, ips))
+                emit(losslog.ready(flush=summary_due or step == max_steps or bool(flags.timing)))
                 if flags.timing and hasattr(engine, "phase_times"):
                     print("phase ms: " + ", ".join("%s %.3f" % kv for kv in engine.phase_times().items()),
                           file=out, flush=True)
                 if summary_due:
+                    L = engine.last_losses()
                     print("Running Summary operation on the chief.", file=out)
                     rate = (step - last_rate_step) / max(1e-9, now - last_rate_t)
                     vals = SUM.collect(engine, L, steps_per_sec=rate, loader_stats=source.stats())
@@ -180,6 +235,7 @@ def run(flags: Flags, out=None) -> int:
                 print("DCGAN_FAULT_AT_STEP=%d: simulated failure" % fault_at, file=out, flush=True)
                 out.flush()
                 os._exit(3)
+        emit(losslog.ready(flush=True))
         if world > 1:
             engine.sync_bn_state()
         if chief:

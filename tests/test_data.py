@@ -101,6 +101,28 @@ def test_native_loader_bf16_and_uint8(tmp_path):
     assert vals == [-100, -99, -98, -97, -96, -95]
 
 
+@pytest.mark.parametrize("out", ["f32", "bf16", "f16"])
+def test_native_loader_float64_decode_matches_numpy(tmp_path, out):
+    """The reference's float64 records decoded straight into the training dtype, rounded exactly
+    like torch's cast (round to nearest even), including fp16 subnormals."""
+    d = str(tmp_path / "f64")
+    os.makedirs(d)
+    rng = np.random.default_rng(3)
+    imgs = rng.uniform(-1, 1, (4, 8, 8, 3))
+    imgs[0, 0, 0] = [1e-6, -3e-8, 6.1e-5]  # fp16 subnormal range
+    TR.write_image_records(os.path.join(d, "a.tfrecord"), imgs, "float64")
+    L = native.ext().Loader(TR.list_record_files(d), "image_raw", 8, 8, 3, 4, 4, 0, 1, 1, out, "f64", False, True,
+                            1 / 127.5, -1.0)
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[out]
+    buf = torch.empty(4, 8, 8, 3, dtype=dt)
+    assert L.next_batch(buf.data_ptr()) == 4
+    exp = torch.from_numpy(imgs).float().to(dt)
+    got = sorted(buf.unbind(0), key=lambda t: float(t.float().sum()))
+    ref = sorted(exp.unbind(0), key=lambda t: float(t.float().sum()))
+    for g, r in zip(got, ref):
+        assert torch.equal(g, r)
+
+
 def test_shuffle_buffer_min_after_dequeue(tmp_path):
     """RandomShuffleQueue semantics: the first batch is drawn from >= min_after_dequeue pooled."""
     d = str(tmp_path / "s")
