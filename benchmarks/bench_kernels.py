@@ -3,7 +3,8 @@
 
 For every conv-shaped GEMM of the DCGAN training step (D forward on 2B, D dgrads, G forward,
 G dgrads, at per-GPU batch B) time every tile configuration -- igemm.hip (both staging
-variants) and igemm3.hip (every tile, 2/3 LDS stages, split-K 1..8) with the weight layout
+variants), igemm3.hip (every tile, 2..5 LDS stages, split-K 1..8) and igemmh.hip (halo window,
+every tile that fits) with the weight layout
 the engine reads for that GEMM -- in ONE process, interleaved (guide §5.4 rule 24), and
 report TF/s. ``--write`` stores the fastest "cfg:splits" per shape in ops/igemm_tuned.json,
 which the engine's tile policy consults first.
@@ -67,6 +68,13 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     phases = 4 if mode == 1 else 1
     M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
     kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
+    if mode in (0, 1) and N % 64 == 0:  # igemmh: halo window in LDS
+        for c in range(400, 430):
+            if H.igemmh_shm(c, mode, Hout, Wout, Kc) is None:
+                continue
+            if H.IGEMMH_TILES[c % 10][1] > N:
+                continue
+            out.append((c, 1))
     for c in range(200, 240):
         if c % 10 not in H.IGEMM3_TILES or H.igemm3_lds(c) > 160 * 1024:
             continue
@@ -101,6 +109,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--v1", action="store_true", help="also time igemm.hip (v1) tiles")
     ap.add_argument("--out", default="", help="also write this run's table (JSON) here")
+    ap.add_argument("--top", type=int, default=6, help="candidates listed per shape")
+    ap.add_argument("--cfgs", default="", help="comma-separated cfg prefix filter, e.g. 4,21")
     a = ap.parse_args()
     global V1
     V1 = a.v1
@@ -121,6 +131,8 @@ def main():
         stats = torch.empty(1 << 22, device=dev)
         fl = flops(mode, Bn, Hin, Win, Kc, Hout, Wout, N)
         cands = candidates(mode, Bn, Hout, Wout, Kc, N, bkn)
+        if a.cfgs:
+            cands = [c for c in cands if any(str(c[0]).startswith(f) for f in a.cfgs.split(","))]
         if not cands:
             print("%-22s (no igemm3 tile: N=%d)" % (name, N))
             continue
@@ -129,7 +141,7 @@ def main():
             p = ext.Program()
             p.igemm_ex(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad,
                        pad, c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn if c >= 200 else 0,
-                       kb if c >= 200 else -1, sp)
+                       kb if 200 <= c < 400 else -1, sp)
             progs[(c, sp)] = p
         times = {c: [] for c in cands}
         s = torch.cuda.current_stream()
@@ -159,7 +171,7 @@ def main():
         print("%-22s M/ph=%7d N=%4d K=%5d  best %3d:%d %-10s %7.1f us %6.0f TF/s | " %
               (name, Bn * Hout * Wout // (4 if mode == 1 else 1), N, Kc * (25 if mode == 0 else 1), bc, bsp,
                H.tile_of(bc), best[0], fl / best[0] / 1e6) +
-              " ".join("%d:%d:%.0f" % (c[0], c[1], t) for t, c in res[:6]), flush=True)
+              " ".join("%d:%d:%.0f" % (c[0], c[1], t) for t, c in res[:a.top]), flush=True)
         table["%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N)] = "%d:%d" % (bc, bsp)
     if a.out:
         json.dump(table, open(a.out, "w"), indent=1, sort_keys=True)

@@ -174,10 +174,17 @@ class Program {
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
                int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
     int bm = 0, bn = 0, ns = 0;
-    const bool v3 = cfg >= 200;
-    if (v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
+    const bool hh = cfg >= 400;          // igemmh.hip (halo window in LDS)
+    const bool v3 = cfg >= 200 && !hh;
+    if (hh && dt_ == 2) throw std::runtime_error("igemmh: 16-bit builds only");
+    if (hh ? KF(dcg_igemmh_tile)(cfg, &bm, &bn, &ns)
+           : v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
       throw std::runtime_error("bad igemm cfg " + std::to_string(cfg) + " for this element type");
-    if (!v3 && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
+    if (hh && (mode == 2 || splits != 1 || (Kc != 64 && Kc != 128 && Kc != 256 && Kc != 512) ||
+               (kb_valid >= 0 && kb_valid != Kc)))
+      throw std::runtime_error("igemmh: conv / deconv with Kc in {64,128,256,512}, no split-K");
+    if (!hh && !v3 && cfg >= 200) throw std::runtime_error("bad igemm cfg");
+    if (!v3 && !hh && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
     if (splits < 1) throw std::runtime_error("splits must be >= 1");
     const int kal = (int)(16 / es_);  // 16-byte A rows
     if (Kc % kal) throw std::runtime_error("igemm needs 16-byte A rows (Kc % " + std::to_string(kal) + " == 0)");
@@ -250,6 +257,45 @@ class Program {
       k.oy_off = q.oy_off; k.ox_off = q.ox_off; k.ntaps = q.ntaps; k.fd_hw = q.fd_hw; k.fd_w = q.fd_w;
       for (int t = 0; t < 25; ++t) k.tap[t] = q.tap[t];
     }
+    size_t h_shm = 0;
+    if (hh) {  // per-phase input window of a tile and tap offsets inside it (igemmh.hip header)
+      int wp_max = 0, tb = 0;
+      for (int i = 0; i < a.nphases; ++i) {
+        const IGemmPhase& q = ph[i];
+        IGemmPhaseK& k = a.phk[i];
+        const int hwq = q.Hq * q.Wq;
+        int TB, TH;
+        if (bm % q.Wq) throw std::runtime_error("igemmh: tile rows must be whole grid rows");
+        if (bm <= hwq) {
+          if (hwq % bm) throw std::runtime_error("igemmh: tile rows must divide the image grid");
+          TB = 1; TH = bm / q.Wq;
+        } else {
+          if (bm % hwq) throw std::runtime_error("igemmh: tile rows must be whole images");
+          TB = bm / hwq; TH = q.Hq;
+        }
+        if (tb && TB != tb) throw std::runtime_error("igemmh: phases with different tile geometry");
+        tb = TB;
+        int dymin = 1 << 20, dymax = -(1 << 20), dxmin = 1 << 20, dxmax = -(1 << 20);
+        for (int t = 0; t < q.ntaps; ++t) {
+          dymin = std::min(dymin, (int)q.dy[t]); dymax = std::max(dymax, (int)q.dy[t]);
+          dxmin = std::min(dxmin, (int)q.dx[t]); dxmax = std::max(dxmax, (int)q.dx[t]);
+        }
+        k.win_h = a.sstride * (TH - 1) + dymax - dymin + 1;
+        k.win_w = a.sstride * (q.Wq - 1) + dxmax - dxmin + 1;
+        k.win_oy = q.iy0_off + dymin; k.win_ox = q.ix0_off + dxmin;
+        k.fd_whw = fastdiv_make(k.win_h * k.win_w); k.fd_ww = fastdiv_make(k.win_w);
+        for (int t = 0; t < q.ntaps; ++t)
+          k.tap[t] = ((q.dy[t] - dymin) * k.win_w + (q.dx[t] - dxmin)) | ((int)q.wtap[t] << 16);
+        wp_max = std::max(wp_max, TB * k.win_h * k.win_w);
+      }
+      a.h_tb = tb;
+      a.h_wbytes = (int)((((size_t)wp_max * (Kc / 8) + 63) / 64) * 1024);
+      h_shm = (size_t)a.h_wbytes + (size_t)ns * bn * 128;
+      const size_t epi = (size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + (bnb_x ? 16384 : 0);
+      h_shm = std::max(h_shm, epi);
+      if (h_shm > 160 * 1024)
+        throw std::runtime_error("igemmh: window + B ring need " + std::to_string(h_shm) + " B of LDS (> 160 KiB)");
+    }
     int maxM = 0;
     for (auto& p : ph) maxM = std::max(maxM, p.M);
     const int mtiles = (maxM + bm - 1) / bm, ntiles = (N + bn - 1) / bn;
@@ -265,7 +311,7 @@ class Program {
         .w(C, (c_rows - 1) * ldc * out_es + (size_t)(cofs + N) * out_es)
         .w(stats, (size_t)mtiles * a.nphases * 2 * N * 4);
     if (bnb_x) {
-      const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
+      const size_t lds = hh ? h_shm : (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
       if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 16384 > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
@@ -289,6 +335,12 @@ class Program {
     }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
     if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
+    if (hh) {
+      const unsigned blocks = (unsigned)((size_t)mtiles * ntiles * a.nphases);
+      return add(name, stream, [this, a, cfg, bkn, blocks, h_shm](hipStream_t s) {
+        return KF(dcg_igemmh_launch)(&a, cfg, bkn, blocks, h_shm, s);
+      }, acc.v);
+    }
     if (!v3)
       return add(name, stream, [this, a, cfg, mtiles, ntiles](hipStream_t s) {
         return KF(dcg_igemm_launch)(&a, cfg, mtiles, ntiles, s);
@@ -744,7 +796,8 @@ static py::tuple igemm_tile(int cfg, int dtype) {
   int bm = 0, bn = 0, ns = 0;
   int rc;
 #define DT(fn) (dtype == 2 ? fn##_f32 : dtype == 1 ? fn##_f16 : fn)
-  if (cfg >= 200) rc = DT(dcg_igemm3_tile)(cfg, &bm, &bn, &ns);
+  if (cfg >= 400) rc = DT(dcg_igemmh_tile)(cfg, &bm, &bn, &ns);
+  else if (cfg >= 200) rc = DT(dcg_igemm3_tile)(cfg, &bm, &bn, &ns);
   else rc = DT(dcg_igemm_tile)(cfg, &bm, &bn);
 #undef DT
   if (rc) throw std::runtime_error("bad cfg");

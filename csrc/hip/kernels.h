@@ -23,6 +23,11 @@ struct IGemmPhaseK {
   int Hq, Wq, M, iy0_off, ix0_off, oy_off, ox_off, ntaps;
   FastDiv fd_hw, fd_w;
   int tap[25];              // packed (dy & 0xff) | (dx & 0xff) << 8 | wtap << 16
+                            // (igemmh: window pixel offset of the tap | wtap << 16)
+  // igemmh (halo) only: the input window of a tile -- row / column of window pixel 0 relative
+  // to (sstride * first tile row, 0), window height / width, and their fast divisors
+  int win_oy, win_ox, win_h, win_w;
+  FastDiv fd_whw, fd_ww;
 };
 
 struct IGemmArgs {
@@ -54,6 +59,9 @@ struct IGemmArgs {
   // activation-only backward (layer without BN): store g = dL/da * act'(y) instead of dL/da and
   // emit (sum g, 0) per channel -- the bias gradient partials. bnb_x aliases y, mean/rstd unused.
   int bnb_store_g;
+  // igemmh (halo): LDS bytes reserved for the input window (whole 1 KiB DMA pieces, max over
+  // phases) and images per tile (1 when a tile is a band of rows of one image)
+  int h_wbytes, h_tb;
 };
 
 struct WGradArgs {

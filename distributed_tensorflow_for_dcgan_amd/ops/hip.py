@@ -78,6 +78,58 @@ def igemm3_lds(cfg: int) -> int:
     return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
 
 
+# igemmh.hip (halo window in LDS, only the weights stream): cfg 400 + 10k + id, NS = (3, 2, 4)[k]
+IGEMMH_TILES = {0: (128, 128), 1: (128, 64), 2: (256, 64), 3: (64, 128), 4: (64, 64)}
+IGEMMH_STAGES = (3, 2, 4)
+
+
+def igemmh_shm(cfg: int, mode: int, Hout: int, Wout: int, Kc: int, pad_y: int = 1, pad_x: int = 1,
+               bnb: bool = False) -> Optional[int]:
+    """Dynamic LDS bytes of an igemmh launch (window of the largest phase + B ring, at least
+    the epilogue scratch), or None when the tile geometry is illegal for the shape or the LDS
+    exceeds 160 KiB. Mirrors the host checks of Program.igemm_ex (csrc/bindings.cpp)."""
+    if cfg < 400 or cfg % 10 not in IGEMMH_TILES or (cfg - 400) // 10 >= len(IGEMMH_STAGES):
+        return None
+    if mode not in (0, 1) or Kc not in (64, 128, 256, 512):
+        return None
+    bm, bn = IGEMMH_TILES[cfg % 10]
+    ns = IGEMMH_STAGES[(cfg - 400) // 10]
+    if mode == 0:
+        phases = [(Hout, Wout, 5, 5)]
+        ss = 2
+    else:
+        phases = []
+        for py in range(2):
+            for px in range(2):
+                hq, wq = (Hout - py + 1) // 2, (Wout - px + 1) // 2
+                if hq * wq == 0:
+                    continue
+                spy = 3 if (py + pad_y) % 2 == 0 else 2
+                spx = 3 if (px + pad_x) % 2 == 0 else 2
+                phases.append((hq, wq, spy, spx))
+        ss = 1
+    wp, tb = 0, None
+    for hq, wq, spy, spx in phases:
+        hw = hq * wq
+        if bm % wq:
+            return None
+        if bm <= hw:
+            if hw % bm:
+                return None
+            t_b, th = 1, bm // wq
+        else:
+            if bm % hw:
+                return None
+            t_b, th = bm // hw, hq
+        if tb is not None and t_b != tb:
+            return None
+        tb = t_b
+        wp = max(wp, t_b * (ss * (th - 1) + spy) * (ss * (wq - 1) + spx))
+    shm = -(-wp * (Kc // 8) // 64) * 1024 + ns * bn * 128
+    shm = max(shm, (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + (16384 if bnb else 0))
+    return shm if shm <= 160 * 1024 else None
+
+
 # fp32 build (igemm_f32.hip): the only tile family of that element type, cfg 200..203
 IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)}
 
@@ -87,6 +139,8 @@ def tile_of(cfg: int, dtype: int = 0) -> Tuple[int, int]:
     (fp32): igemm_f32.hip."""
     if dtype == 2:
         return IGEMM_F32_TILES[cfg]
+    if cfg >= 400:
+        return IGEMMH_TILES[cfg % 10]
     if cfg >= 200:
         return IGEMM3_TILES[cfg % 10]
     return IGEMM_CFGS[cfg % 100]
@@ -110,6 +164,8 @@ def pick_igemm_f32(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
 
 def bnb_fits(cfg: int) -> bool:
     """True when the tile's LDS can hold the fused BN-backward statistics scratch (epilogue.h)."""
+    if cfg >= 400:  # igemmh sizes its LDS per launch (the host rejects a launch that cannot fit)
+        return True
     bm, bn = tile_of(cfg)
     ns = IGEMM3_STAGES[(cfg - 200) // 10] if cfg >= 200 else 2
     return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= ns * (bm + bn) * 128
@@ -174,7 +230,7 @@ TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "igemm_tun
 def tuned_table() -> dict:
     """Per-layer tile choices measured on MI355X by ``benchmarks/bench_kernels.py --write``
     (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> "cfg:splits" (or a bare cfg): cfg < 200 is
-    igemm.hip (+100 = LDS-DMA staging), 200..219 igemm3.hip)."""
+    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip, 400..429 igemmh.hip)."""
     global _TUNED
     if _TUNED is None:
         _TUNED = {}
