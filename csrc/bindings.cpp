@@ -313,7 +313,8 @@ class Program {
     if (bnb_x) {
       const size_t lds = hh ? h_shm : (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
-      if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 16384 > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
+      const size_t nt = v3 ? (size_t)KF(dcg_igemm3_threads)(cfg) : 256;
+      if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 64 * nt > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
       const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
       if (bnb_store_g) {  // activation backward only (no BN): x, mean, rstd and groups unused

@@ -113,11 +113,11 @@ __device__ __forceinline__ void frag_epilogue_dispatch(const f32x4 (&acc)[FM][FN
 
 // Pairwise tree over the RL row lanes of red2[RL][BN][2] (fixed order: deterministic; log2(RL)
 // LDS rounds instead of an RL-long dependent chain of LDS reads). Result in red2[0][BN][2].
-template <int RL, int BN>
+template <int RL, int BN, int NT = 256>
 __device__ __forceinline__ void lane_tree(float* red2) {
 #pragma unroll
   for (int h = RL / 2; h > 0; h >>= 1) {
-    for (int q = threadIdx.x; q < h * BN * 2; q += 256) red2[q] += red2[q + h * BN * 2];
+    for (int q = threadIdx.x; q < h * BN * 2; q += NT) red2[q] += red2[q + h * BN * 2];
     __syncthreads();
   }
 }
@@ -128,11 +128,12 @@ __device__ __forceinline__ void lane_tree(float* red2) {
 // the BN backward needs, without a separate pass over three tensors. Each thread owns one fixed
 // 8-channel chunk; row lanes are reduced through LDS scratch (red2, 16 KiB) in a fixed order.
 // Requires elem_t output with N % 8 == 0 (the caller checks) and a tile inside one BN group.
-template <int BM, int BN>
+// NT threads per workgroup; red2 holds 64 * NT bytes.
+template <int BM, int BN, int NT = 256>
 __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* rowoff, const elem_t* ctile,
                                               float* red2, int n0, int m0, float* dst) {
-  constexpr int CPAD = BN + 8, CPR = BN / 8, RL = 256 / CPR;
-  static_assert(256 % CPR == 0, "chunks per row");
+  constexpr int CPAD = BN + 8, CPR = BN / 8, RL = NT / CPR;
+  static_assert(NT % CPR == 0, "chunks per row");
   const int tid = threadIdx.x, c = tid % CPR, rl = tid / CPR;
   const int N = p.N, n = n0 + 8 * c;
   const bool nok = n < N;
@@ -161,8 +162,8 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
 #pragma unroll
     for (int i = 0; i < 8; ++i) red2[(rl * BN + 8 * c + i) * 2 + 0] = s[i];
     __syncthreads();
-    lane_tree<RL, BN>(red2);
-    for (int nl = tid; nl < BN; nl += 256) {
+    lane_tree<RL, BN, NT>(red2);
+    for (int nl = tid; nl < BN; nl += NT) {
       if (n0 + nl >= N) continue;
       dst[n0 + nl] = red2[nl * 2 + 0];
       dst[N + n0 + nl] = 0.f;
@@ -200,8 +201,8 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
     red2[(rl * BN + 8 * c + i) * 2 + 1] = s2[i];
   }
   __syncthreads();
-  lane_tree<RL, BN>(red2);
-  for (int nl = tid; nl < BN; nl += 256) {
+  lane_tree<RL, BN, NT>(red2);
+  for (int nl = tid; nl < BN; nl += NT) {
     if (n0 + nl >= N) continue;
     dst[n0 + nl] = red2[nl * 2 + 0];
     dst[N + n0 + nl] = red2[nl * 2 + 1];

@@ -58,19 +58,20 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 template <int BM, int BN, int WM, int WN, int BKN, int NS>
-__global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
+__global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NW = WM * WN, NT = 64 * NW;                   // 4 or 8 waves
   constexpr int NPA = A_BYTES / 1024, NPB = B_BYTES / 1024;  // 1 KiB DMA pieces per stage
-  constexpr int PPW_A = NPA / 4, PPW_B = NPB / 4;             // per wave
+  constexpr int PPW_A = NPA / NW, PPW_B = NPB / NW;           // per wave
   constexpr int LPT = PPW_A + PPW_B;                          // DMA instructions per wave per tile
   constexpr int SB = BN * 2;                                  // k-major B row stride (bytes)
   constexpr int B_ROWS_PER_PIECE = BKN ? 1024 / SB : 8;
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(NPA % 4 == 0 && NPB % 4 == 0, "every wave issues the same DMA count");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(NPA % NW == 0 && NPB % NW == 0, "every wave issues the same DMA count");
   static_assert(FM >= 1 && FN >= 1, "tile");
   static_assert(!BKN || (SB <= 1024 && 1024 % SB == 0), "k-major B rows");
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   if (m0 >= M) {  // phase with fewer rows (odd output sizes): its stats slot must still be defined
     if (p.stats && split == 0) {
       float* dst = p.stats + (size_t)(mt * p.nphases + phase) * 2 * p.N;
-      for (int nl = tid; nl < BN; nl += 256)
+      for (int nl = tid; nl < BN; nl += NT)
         if (n0 + nl < p.N) { dst[n0 + nl] = 0.f; dst[p.N + n0 + nl] = 0.f; }
     }
     return;
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   bool a_ok[PPW_A];
 #pragma unroll
   for (int i = 0; i < PPW_A; ++i) {
-    const int r = 8 * (wave + 4 * i) + (lane >> 3);
+    const int r = 8 * (wave + NW * i) + (lane >> 3);
     const int m = m0 + r;
     a_ok[i] = m < M;
     if (p.plain) {
@@ -179,11 +180,11 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
         if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
           off = (uint32_t)(a_base[i] + tap_delta + cc) * 2u;
       }
-      dma16_asm(ra, sa + (wave + 4 * i) * 1024, off);
+      dma16_asm(ra, sa + (wave + NW * i) * 1024, off);
     }
 #pragma unroll
     for (int i = 0; i < PPW_B; ++i) {
-      const int q = wave + 4 * i;
+      const int q = wave + NW * i;
       uint32_t off = OOB;
       if constexpr (BKN) {
         const int rr = q * B_ROWS_PER_PIECE + lane / (SB / 16);
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) store16_sc1(rw, own_base + (uint32_t)(((i * FN + j) * 256 + tid) * 16), acc[i][j]);
+      for (int j = 0; j < FN; ++j) store16_sc1(rw, own_base + (uint32_t)(((i * FN + j) * NT + tid) * 16), acc[i][j]);
     wait_vmcnt<0>();
     __syncthreads();
     if (tid == 0) {
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            tot[i][j] += load16_sc1(rw, base + (uint32_t)(((i * FN + j) * 256 + tid) * 16));
+            tot[i][j] += load16_sc1(rw, base + (uint32_t)(((i * FN + j) * NT + tid) * 16));
       }
     }
 #pragma unroll
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   constexpr int CPAD = BN + 8;
   elem_t* ctile = reinterpret_cast<elem_t*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
   static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= NS * STAGE, "epilogue LDS");
-  for (int r = tid; r < BM; r += 256) {
+  for (int r = tid; r < BM; r += NT) {
     const int m = m0 + r;
     int off = -1;
     if (m < M) {
@@ -359,11 +360,11 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   frag_epilogue_dispatch<FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats, vec, m0);
   if (stamp && tid == 0) stamp[5] = __builtin_amdgcn_s_memtime();
   if (p.bnb_x) {  // BN-backward statistics fused into the store pass (epilogue.h)
-    constexpr bool kFits = (BM + 2 * WM * BN) * 4 + BM * CPAD * 2 + 16384 <= NS * STAGE;
+    constexpr bool kFits = (BM + 2 * WM * BN) * 4 + BM * CPAD * 2 + 64 * NT <= NS * STAGE;
     if constexpr (kFits) {
       __syncthreads();
       float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + BM * CPAD * 2);
-      vec_store_bnb<BM, BN>(p, rowoff, ctile, red2, n0, m0, p.stats + (size_t)(mt * p.nphases + phase) * 2 * N);
+      vec_store_bnb<BM, BN, NT>(p, rowoff, ctile, red2, n0, m0, p.stats + (size_t)(mt * p.nphases + phase) * 2 * N);
     } else {
       __builtin_trap();  // the host only requests fused statistics on tiles with the LDS for them
     }
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
   if (vec) {
     constexpr int CPR = BN / 8;
     elem_t* C = reinterpret_cast<elem_t*>(p.C);
-    for (int q = tid; q < BM * CPR; q += 256) {
+    for (int q = tid; q < BM * CPR; q += NT) {
       const int r = q / CPR, c = q - r * CPR;
       const int off = rowoff[r];
       const int n = n0 + 8 * c;
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
     }
   }
   if (do_stats) {
-    for (int nl = tid; nl < BN; nl += 256) {
+    for (int nl = tid; nl < BN; nl += NT) {
       const int n = n0 + nl;
       if (n >= N) continue;
       float s = 0.f, s2 = 0.f;
@@ -407,9 +408,11 @@ __global__ __launch_bounds__(256) void igemm3_kernel(IGemmArgs p) {
 // NS = 2 -> 210..219, NS = 4 -> 220..229, NS = 5 -> 230..239). Deeper rings keep more k-tiles of
 // LDS-DMA in flight (issue -> landed is ~1.1 us, several k-tiles of MFMA work), at the cost of
 // workgroups per CU (160 KiB of LDS per CU).
+// ids 6..8: 8-wave workgroups (512 threads, 64x64 per wave): bigger tiles load fewer operand
+// bytes per MFMA (the K loop is bound by the LDS-DMA fill rate, profiles/r2/igemm3_ablations_r2.txt)
 #define DCG_IGEMM3_TILES(X) \
   X(0, 128, 128, 2, 2) X(1, 256, 64, 4, 1) X(2, 64, 256, 1, 4) X(3, 128, 64, 2, 2) \
-  X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2)
+  X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2) X(6, 256, 128, 4, 2) X(7, 128, 256, 2, 4) X(8, 512, 64, 8, 1)
 
 static constexpr int kIgemm3Stages[4] = {3, 2, 4, 5};
 
@@ -434,8 +437,16 @@ static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), shm, s, *a);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), shm, s, *a);
   return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_igemm3_threads)(int cfg) {
+  const int id = cfg % 10;
+#define X(id_, BM_, BN_, WM_, WN_) if (id == id_) return 64 * WM_ * WN_;
+  DCG_IGEMM3_TILES(X)
+#undef X
+  return 256;
 }
 
 extern "C" int DCG_API(dcg_igemm3_launch)(const dcg::IGemmArgs* a, int cfg, int bkn, unsigned blocks, hipStream_t s) {
@@ -444,8 +455,12 @@ extern "C" int DCG_API(dcg_igemm3_launch)(const dcg::IGemmArgs* a, int cfg, int 
   const int id = cfg % 10;
 #define X(id_, BM_, BN_, WM_, WN_)                                                              \
   if (id == id_) {                                                                              \
-    if (ns == 3) return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 3>(a, blocks, s)                   \
-                            : launch3<BM_, BN_, WM_, WN_, 0, 3>(a, blocks, s);                  \
+    if (ns == 3) {                                                                              \
+      if constexpr ((size_t)3 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
+        return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 3>(a, blocks, s)                            \
+                   : launch3<BM_, BN_, WM_, WN_, 0, 3>(a, blocks, s);                           \
+      return -1;                                                                                \
+    }                                                                                           \
     if (ns == 4) {                                                                              \
       if constexpr ((size_t)4 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
         return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 4>(a, blocks, s)                            \

@@ -53,9 +53,12 @@ def main():
             span = (last[-1][9] + last[-1][1] - last[0][9]) / 1e3
             busy = sum(r[1] for r in last) / 1e3
             print("\nlast full step: %d kernels, busy %.1f us, span %.1f us" % (len(last), busy, span))
+            t0 = last[0][9]
+            print("  start_us   dur_us  grid / resources / kernel")
             for r in last:
-                print("%8.1f us  grid(%d,%d,%d) vgpr %d lds %d  %s" % (r[1] / 1e3, r[2] // max(1, r[5]), r[3], r[4],
-                                                                     r[6], r[8], short(r[0])))
+                print("%9.1f %8.1f  grid(%d,%d,%d) vgpr %d lds %d  %s" % ((r[9] - t0) / 1e3, r[1] / 1e3,
+                                                                       r[2] // max(1, r[5]), r[3], r[4], r[6], r[8],
+                                                                       short(r[0])))
 
 
 if __name__ == "__main__":

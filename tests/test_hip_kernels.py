@@ -133,7 +133,7 @@ def test_im2col_exact(B, Hs, C, kpad):
     assert not col[:, 25 * C:].float().any()
 
 
-IG3 = [200, 201, 202, 203, 204, 205, 210, 211, 212, 213, 214, 215]
+IG3 = [200, 201, 202, 203, 204, 205, 210, 211, 212, 213, 214, 215, 206, 207, 216, 217, 218]  # 2x6..2x8: 8 waves
 
 
 @pytest.mark.parametrize("bkn", [0, 1])
@@ -167,7 +167,7 @@ def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
     w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=43))  # deconv [5,5,out,in] = [25][N][Kc] (bt layout)
     bias = rnd(Co, scale=0.1, seed=44)
     ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
-    for cfg in (200, 203, 205, 212, 215):
+    for cfg in (200, 203, 205, 212, 215, 206, 217, 218):
         for splits in (1, 2, 5):
             y = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True, cfg=cfg,
                                         splits=splits)
@@ -177,10 +177,47 @@ def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
     yd = R.conv2d_transpose_same(xd, w.float(), (Ho, Ho))
     dy = bf(rnd(B, Ho, Ho, Co, seed=46))
     (gx,) = torch.autograd.grad(yd, xd, dy.float())
-    for cfg in (200, 205, 213):
+    for cfg in (200, 205, 213, 216, 207):
         for splits in (1, 4):
             out = h.conv2d_same(dy, w.reshape(25, Co, Ci), Ci, out_f32=True, cfg=cfg, bkn=True, splits=splits)
             close(out, gx, 2e-3, "G dgrad cfg%d s%d" % (cfg, splits))
+
+
+@pytest.mark.parametrize("cfg", [200, 211, 213, 206, 218, 403, 414])
+def test_igemm_fused_bn_backward_stats(cfg):
+    """Data-gradient GEMM with the BN-backward statistics fused into its store pass (epilogue.h
+    vec_store_bnb): stored dL/da == the plain GEMM's, partials sum to (sum g, sum g * xhat) with
+    g = dL/da * lrelu'(y), for 4- and 8-wave igemm3 tiles and igemmh."""
+    h = H()
+    B, Hi, Ci, Co = 4, 16, 128, 64
+    Ho = 2 * Hi
+    dy = bf(rnd(B, Hi, Hi, Ci, seed=60))
+    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=61)).reshape(25, Co, Ci).contiguous()
+    x = bf(rnd(B, Ho, Ho, Co, seed=62))
+    y = bf(rnd(B, Ho, Ho, Co, seed=63) - 0.3)
+    mean = rnd(1, Co, scale=0.2, seed=64)
+    rstd = rnd(1, Co, seed=65).abs() + 0.5
+    if cfg >= 400 and h.igemmh_shm(cfg, 1, Ho, Ho, Ci, bnb=True) is None:
+        pytest.skip("tile does not fit this shape")
+    if cfg < 400 and not h.bnb_fits(cfg):
+        pytest.skip("tile has no LDS for the fused statistics")
+    bm = h.tile_of(cfg)[0]
+    mph = B * Hi * Hi
+    da_ref = h.conv2d_transpose_same(dy, w, Co, (Ho, Ho), cfg=200)
+    da = torch.empty_like(da_ref)
+    mt = -(-mph // bm)
+    st = torch.empty(mt * 4, 2, Co, device=dev)
+    prog = h.ext().Program()
+    prog.igemm_ex("bnb", 1, h._p(dy), h._p(w), h._p(da), B, Hi, Hi, Ci, Ho, Ho, Co, 1, 1, cfg, 0, Co, 0, 0, 0, 0.2,
+                  h._p(st), 0, 0, -1, 1, h._p(x), h._p(y), h._p(mean), h._p(rstd), mph, 2, 0.2, 0)
+    h.run(prog)
+    torch.cuda.synchronize()
+    assert torch.equal(da, da_ref)
+    g = da.float() * torch.where(y.float() > 0, 1.0, 0.2)
+    xh = (x.float() - mean.reshape(Co)) * rstd.reshape(Co)
+    s = st.sum(0)
+    close(s[0], g.reshape(-1, Co).sum(0), 2e-3, "sum g cfg%d" % cfg)
+    close(s[1], (g * xh).reshape(-1, Co).sum(0), 2e-3, "sum g xhat cfg%d" % cfg)
 
 
 def test_igemm3_plain_im2col_bkn():
