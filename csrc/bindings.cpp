@@ -172,7 +172,7 @@ class Program {
                int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
                uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
-               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
+               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0, int fin = -1) {
     int bm = 0, bn = 0, ns = 0;
     const bool hh = cfg >= 400;          // igemmh.hip (halo window in LDS)
     const bool v3 = cfg >= 200 && !hh;
@@ -336,25 +336,88 @@ class Program {
     }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
     if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
+    if (fin >= 0 && hh) throw std::runtime_error("igemm fin: igemm / igemm3 tiles only");
     if (hh) {
       const unsigned blocks = (unsigned)((size_t)mtiles * ntiles * a.nphases);
       return add(name, stream, [this, a, cfg, bkn, blocks, h_shm](hipStream_t s) {
         return KF(dcg_igemmh_launch)(&a, cfg, bkn, blocks, h_shm, s);
       }, acc.v);
     }
-    if (!v3)
+    if (!v3) {
+      if (fin >= 0) attach_fin(a, fin, ntiles, acc);
       return add(name, stream, [this, a, cfg, mtiles, ntiles](hipStream_t s) {
         return KF(dcg_igemm_launch)(&a, cfg, mtiles, ntiles, s);
       }, acc.v);
+    }
     const size_t tiles = (size_t)mtiles * ntiles * a.nphases;
     if (splits > 1) {  // per-op workspace + zeroed arrival counters (reset by the kernel itself)
       a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * (size_t)bm * bn * sizeof(float)));
       a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
       acc.w((uintptr_t)a.ws, tiles * splits * (size_t)bm * bn * sizeof(float)).w((uintptr_t)a.counters, tiles * 4);
     }
+    if (fin >= 0) attach_fin(a, fin, ntiles, acc);
     const unsigned blocks = (unsigned)(tiles * splits);
     return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); },
                acc.v);
+  }
+
+  // ------------------------------------------------------------------ fused BN finalize (finalize.h)
+  // A spec recorded here is attached to ONE igemm_ex op (fin=<handle>): that GEMM's workgroups
+  // reduce the partial rows they write and evaluate the finalize, instead of a separate
+  // bn_finalize / bn_bwd_finalize / sum_partials launch. Returns the handle.
+  int bn_fin_fwd(int groups, int ppg, int C, double count, uintptr_t gamma, uintptr_t beta, float eps,
+                 uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift, uintptr_t ema_mean,
+                 uintptr_t ema_var, float decay) {
+    BnFin f{};
+    f.mode = 1; f.groups = groups; f.ppg = ppg; f.C = C; f.count = count; f.eps = eps; f.decay = decay;
+    f.gamma = P<const float>(gamma); f.beta = P<const float>(beta);
+    f.mean = P<float>(mean); f.rstd = P<float>(rstd); f.scale = P<float>(scale); f.shift = P<float>(shift);
+    f.ema_mean = P<float>(ema_mean); f.ema_var = P<float>(ema_var);
+    const size_t gc = (size_t)groups * C * 4;
+    AccList acc;
+    acc.r(gamma, (size_t)C * 4).r(beta, (size_t)C * 4).w(mean, gc).w(rstd, gc).w(scale, gc).w(shift, gc)
+        .w(ema_mean, gc).w(ema_var, gc);
+    fins_.push_back({f, acc.v});
+    return (int)fins_.size() - 1;
+  }
+  int bn_fin_bwd(int groups, int ppg, int C, float count, uintptr_t gamma, uintptr_t mean, uintptr_t rstd,
+                 uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef) {
+    BnFin f{};
+    f.mode = 2; f.groups = groups; f.ppg = ppg; f.C = C; f.count = count;
+    f.gamma = P<const float>(gamma); f.mean_in = P<const float>(mean); f.rstd_in = P<const float>(rstd);
+    f.dgamma = P<float>(dgamma); f.dbeta = P<float>(dbeta); f.coef = P<float>(coef);
+    const size_t gc = (size_t)groups * C * 4;
+    AccList acc;
+    acc.r(gamma, (size_t)C * 4).r(mean, gc).r(rstd, gc).w(dgamma, (size_t)C * 4).w(dbeta, (size_t)C * 4)
+        .w(coef, 3 * gc);
+    fins_.push_back({f, acc.v});
+    return (int)fins_.size() - 1;
+  }
+  int bn_fin_sum(int groups, int ppg, int C, uintptr_t dst) {
+    BnFin f{};
+    f.mode = 3; f.groups = groups; f.ppg = ppg; f.C = C; f.count = 1.0;
+    f.dbeta = P<float>(dst);
+    fins_.push_back({f, AccList().w(dst, (size_t)C * 4).v});
+    return (int)fins_.size() - 1;
+  }
+  void attach_fin(IGemmArgs& a, int fin, int ntiles, AccList& acc) {
+    if (fin >= (int)fins_.size()) throw std::runtime_error("igemm: bad fin handle");
+    if (dt_ == 2 || !a.stats) throw std::runtime_error("igemm fin: 16-bit igemm3 with statistics only");
+    BnFin f = fins_[fin].first;
+    const int rows = a.mtiles * a.nphases;
+    if (f.groups < 1 || f.ppg < 1 || f.groups * f.ppg != rows || f.C != a.N)
+      throw std::runtime_error("igemm fin: groups x rows-per-group must equal the GEMM's partial rows");
+    int F = 1;  // rows per level-1 group: a power of two dividing ppg, ~sqrt(ppg), <= 32
+    while (F * F < f.ppg && f.ppg % (2 * F) == 0 && F < 32) F *= 2;
+    f.F = F;
+    f.ntn = ntiles;
+    f.part = a.stats;
+    const size_t nl1 = (size_t)f.groups * (f.ppg / F);
+    f.l1 = reinterpret_cast<double*>(dev_alloc(nl1 * 2 * f.C * sizeof(double)));
+    f.ctr = reinterpret_cast<unsigned*>(dev_alloc((nl1 + 1) * ntiles * sizeof(unsigned), nullptr, true));
+    a.fin = reinterpret_cast<const BnFin*>(dev_alloc(sizeof(BnFin), &f));
+    acc.w((uintptr_t)f.l1, nl1 * 2 * f.C * 8).w((uintptr_t)f.ctr, (nl1 + 1) * ntiles * 4);
+    for (auto& x : fins_[fin].second) acc.v.push_back(x);
   }
   int last_mtiles() const { return last_mtiles_; }
   int last_nphases() const { return last_nphases_; }
@@ -788,6 +851,7 @@ class Program {
   std::vector<void*> dev_allocs_;
   std::vector<hipEvent_t> events_;
   int last_mtiles_ = 0, last_nphases_ = 0;
+  std::vector<std::pair<BnFin, std::vector<Acc>>> fins_;  // fused-finalize specs (bn_fin_*)
   int dt_ = 0;       // element type of every activation / weight-mirror pointer
   size_t es_ = 2;    // its size in bytes
   bool dry_ = false;
@@ -853,7 +917,10 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("bias"), py::arg("act"), py::arg("leak"), py::arg("stats"), py::arg("stream"), py::arg("bkn"),
            py::arg("kb_valid"), py::arg("splits"), py::arg("bnb_x") = 0, py::arg("bnb_y") = 0,
            py::arg("bnb_mean") = 0, py::arg("bnb_rstd") = 0, py::arg("bnb_rpg") = 0, py::arg("bnb_act") = 0,
-           py::arg("bnb_leak") = 0.f, py::arg("bnb_store_g") = 0)
+           py::arg("bnb_leak") = 0.f, py::arg("bnb_store_g") = 0, py::arg("fin") = -1)
+      .def("bn_fin_fwd", &Program::bn_fin_fwd)
+      .def("bn_fin_bwd", &Program::bn_fin_bwd)
+      .def("bn_fin_sum", &Program::bn_fin_sum)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)

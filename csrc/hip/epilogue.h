@@ -163,10 +163,11 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
     for (int i = 0; i < 8; ++i) red2[(rl * BN + 8 * c + i) * 2 + 0] = s[i];
     __syncthreads();
     lane_tree<RL, BN, NT>(red2);
-    for (int nl = tid; nl < BN; nl += NT) {
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(dst, (uint32_t)(2 * N * 4));
+    for (int nl = tid; nl < BN; nl += NT) {  // write-through (sc1): a fused finalize may read it on another CU
       if (n0 + nl >= N) continue;
-      dst[n0 + nl] = red2[nl * 2 + 0];
-      dst[N + n0 + nl] = 0.f;
+      st_sc1_f32(rd, (uint32_t)(n0 + nl) * 4u, red2[nl * 2 + 0]);
+      st_sc1_f32(rd, (uint32_t)(N + n0 + nl) * 4u, 0.f);
     }
     return;
   }
@@ -202,10 +203,11 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
   }
   __syncthreads();
   lane_tree<RL, BN, NT>(red2);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(dst, (uint32_t)(2 * N * 4));
   for (int nl = tid; nl < BN; nl += NT) {
     if (n0 + nl >= N) continue;
-    dst[n0 + nl] = red2[nl * 2 + 0];
-    dst[N + n0 + nl] = red2[nl * 2 + 1];
+    st_sc1_f32(rd, (uint32_t)(n0 + nl) * 4u, red2[nl * 2 + 0]);
+    st_sc1_f32(rd, (uint32_t)(N + n0 + nl) * 4u, red2[nl * 2 + 1]);
   }
 }
 

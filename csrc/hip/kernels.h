@@ -30,6 +30,21 @@ struct IGemmPhaseK {
   FastDiv fd_whw, fd_ww;
 };
 
+// BN finalize fused into the statistics-producing GEMM (finalize.h). mode 1 forward (mean /
+// rstd / scale / shift / EMA), 2 backward (dx coefficients, dgamma, dbeta), 3 bias-gradient sum.
+struct BnFin {
+  int mode, groups, ppg, F, C, ntn;       // partial rows per group, rows per L1 group, channels, column tiles
+  double count;                           // rows per group
+  float eps, decay;
+  const float* part;                      // the partial rows [groups * ppg][2][C] (= IGemmArgs::stats)
+  double* l1;                             // [groups * ppg / F][2][C]
+  unsigned* ctr;                          // [(groups * ppg / F + 1) * ntn], zero between launches
+  const float* gamma; const float* beta;
+  float* mean; float* rstd; float* scale; float* shift; float* ema_mean; float* ema_var;  // forward out
+  const float* mean_in; const float* rstd_in;                                            // backward in
+  float* dgamma; float* dbeta; float* coef;                                              // backward out
+};
+
 struct IGemmArgs {
   const elem_t* A; int Bn, H, W, Kc, sstride, plain;
   const elem_t* Bw; int N;
@@ -62,6 +77,7 @@ struct IGemmArgs {
   // igemmh (halo): LDS bytes reserved for the input window (whole 1 KiB DMA pieces, max over
   // phases) and images per tile (1 when a tile is a band of rows of one image)
   int h_wbytes, h_tb;
+  const BnFin* fin;         // igemm3: BN finalize fused into the epilogue (nullptr = separate kernel)
 };
 
 struct WGradArgs {

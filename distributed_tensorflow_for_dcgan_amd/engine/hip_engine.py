@@ -292,11 +292,12 @@ class HipEngine:
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
                cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None, bkn=False, kb_valid=-1, bnb=None,
-               stream=0):
+               stream=0, fin=None):
         """One conv-shaped GEMM. Bw is a weight view; bkn=True reads it as [tap][K][N] (D
         forward, G dgrad, im2col'd layers), else as [tap][N][K]. bnb = (x, y, mean, rstd,
         rows_per_group, act[, store_g]): the epilogue also emits the BN-backward partial sums of
-        the layer whose dL/da this GEMM produces (see _dgrad_bnb)."""
+        the layer whose dL/da this GEMM produces (see _dgrad_bnb). fin: callable cfg -> handle of a
+        fused-finalize spec (Program.bn_fin_*) or -1 (see _fin_ok)."""
         plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn, dtype=self.dt)
         if plan is None:
             raise RuntimeError("no igemm tile for %s (mode %d, N %d, bkn %d)" % (name, mode, N, bkn))
@@ -307,10 +308,35 @@ class HipEngine:
             bx, by, bm, br = _p(bnb[0]), _p(bnb[1]), _p(bnb[2]), _p(bnb[3])
             brpg, bact = bnb[4], bnb[5]
             bstore = int(len(bnb) > 6 and bnb[6])
+        fh = fin(cfg) if fin is not None else -1
         prog.igemm_ex(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
                       ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), stream, int(bkn), kb_valid, splits,
-                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak, bstore)
+                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak, bstore, fh)
         return cfg
+
+    def _fin_ok(self, cfg: int) -> bool:
+        """DCGAN_FUSED_FIN=1: the BN finalize (or bias-gradient sum) runs inside the statistics GEMM
+        (csrc/hip/finalize.h, 16-bit igemm / igemm3 tiles) instead of a separate launch. Off by
+        default: measured 1.389 vs 1.321 ms/step (profiles/r2/ab_fused_finalize_r2.txt) -- the
+        per-workgroup arrival (vmcnt(0) on the C-tile stores + one agent-scope atomic round trip)
+        costs more than the 14 launches it removes."""
+        return (not self.f32 and cfg < 400 and os.environ.get("DCGAN_FUSED_FIN") == "1")
+
+    def _fin_fwd(self, prog, name, rows, C, groups, P, update_ema, holder):
+        """fin callable for the GEMM producing BN ``name``'s forward statistics."""
+        def make(cfg):
+            if not self._fin_ok(cfg):
+                return -1
+            cfgm, st = self.cfg, self.bn[name]
+            bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
+            Pm = self.model.d if name.startswith("d_") else self.model.g
+            ema_m = bnstate.mean[name] if update_ema else None
+            ema_v = bnstate.var[name] if update_ema else None
+            holder["fused"] = True
+            return prog.bn_fin_fwd(groups, P // groups, C, float(rows // groups), _p(Pm[name + "/gamma"]),
+                                   _p(Pm[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]),
+                                   _p(st["scale"]), _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum)
+        return make
 
     def _stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None, bkn=False):
         """Number of partial-statistics rows a stats-emitting igemm writes (tiles x phases)."""
@@ -324,12 +350,14 @@ class HipEngine:
         bm, _ = H.tile_of(plan[0], self.dt)
         return -(-M // bm) * phases
 
-    def _dgrad_bnb(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, bn_name, x, y, groups, act, group_offset=0):
+    def _dgrad_bnb(self, prog, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, bn_name, x, y, groups, act,
+                   group_offset=0, fin=None):
         """Fused BN-backward statistics for the data-gradient GEMM that writes dL/da of BN layer
         ``bn_name`` (x = its pre-BN input, y = its activation output, same layout as the GEMM
         output). Returns (igemm kwargs, partials, partials per group) or None when no tile keeps
         the real/fake groups apart (odd sizes) or in fp32 -- the BN backward then runs its own
-        statistics pass."""
+        statistics pass. fin = (param set, grads or None, coef buffer): also fuse the BN-backward
+        finalize into the GEMM where the tile allows (the returned holder then says "fused")."""
         if self.f32:
             return None
         if mode == 1:
@@ -348,13 +376,28 @@ class HipEngine:
         st = self.bn[bn_name]
         mean, rstd = st["mean"][group_offset:], st["rstd"][group_offset:]
         kw = dict(stats=part, rows_per_group=rpg, bnb=(x, y, mean, rstd, rpg, act))
-        return kw, part, P // groups
+        hold = {}
+        if fin is not None:
+            Pm, grads, coef = fin
 
-    def _dgrad_actb(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, name, y, act):
+            def make(cfg):
+                if not self._fin_ok(cfg):
+                    return -1
+                hold["fused"] = True
+                dg = grads[bn_name + "/gamma"] if grads is not None else None
+                db = grads[bn_name + "/beta"] if grads is not None else None
+                # BN count = ALL rows of a group (a deconv-shaped dgrad's rpg counts one phase)
+                return prog.bn_fin_bwd(groups, P // groups, N, float(M * phases // groups),
+                                       _p(Pm[bn_name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef))
+            kw["fin"] = make
+        return kw, part, P // groups, hold
+
+    def _dgrad_actb(self, prog, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, name, y, act, db=None):
         """Fused activation backward for the data-gradient GEMM that produces dL/da of a layer
         WITHOUT BN: the GEMM stores dx = dL/da * act'(y) directly and emits per-tile partial
         column sums of dx (the bias gradient). Returns (igemm kwargs, partials, #partials) or
-        None (fp32, or no vectorizable tile: the caller runs the separate act backward)."""
+        None (fp32, or no vectorizable tile: the caller runs the separate act backward). db: the
+        bias-gradient buffer -- the column sum is then fused into the GEMM where the tile allows."""
         if self.f32:
             return None
         plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, None, bkn, dtype=self.dt)
@@ -367,7 +410,16 @@ class HipEngine:
             M, phases = Bn * Hout * Wout, 1
         P = -(-M // bm) * phases
         part = self._stats_buf(name + ".actb", P, N)
-        return dict(stats=part, bnb=(y, y, None, None, 0, act, True)), part, P
+        kw = dict(stats=part, bnb=(y, y, None, None, 0, act, True))
+        hold = {}
+        if db is not None:
+            def make(cfg):
+                if not self._fin_ok(cfg):
+                    return -1
+                hold["fused"] = True
+                return prog.bn_fin_sum(1, P, N, _p(db))
+            kw["fin"] = make
+        return kw, part, P, hold
 
     def _deconv_out(self, prog, name, x, w, y, B, L, pad, bias, act):
         """G's output layer: the direct narrow kernel for RGB / gray outputs (16-bit), else the
@@ -379,17 +431,19 @@ class HipEngine:
             self._igemm(prog, name, 1, x, w, y, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad,
                         bias=bias, act=act)
 
-    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema):
-        """BN finalize (+EMA) and apply+act over `groups` row groups."""
+    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema, fused=False):
+        """BN finalize (+EMA) -- unless the statistics GEMM already ran it (fused) -- and
+        apply+act over `groups` row groups."""
         cfgm = self.cfg
         st = self.bn[name]
         bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
         P = self.model.d if name.startswith("d_") else self.model.g
         ema_m = bnstate.mean[name] if update_ema else None
         ema_v = bnstate.var[name] if update_ema else None
-        prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
-                         _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
-                         _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
+        if not fused:
+            prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
+                             _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
+                             _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
         prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
                           rows // groups, act, cfgm.lrelu_leak, 0)
 
@@ -433,11 +487,13 @@ class HipEngine:
             if L.bn:
                 P = self._stats_tiles(1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout)
                 part = self._stats_buf(L.bn, P, L.cout)
-                self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part)
                 rows = B * L.out_hw ** 2
+                hold = {}
+                self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
+                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part,
+                            fin=self._fin_fwd(prog, L.bn, rows, L.cout, 1, P, update_ema, hold))
                 self._bn_fwd(prog, L.bn, self.g_x[L.name], self.g_a[L.name], rows, L.cout, 1, RELU, part, P,
-                             update_ema)
+                             update_ema, fused=bool(hold))
                 a_prev = self.g_a[L.name]
             else:  # last: + bias, tanh, written into the fake half of D's input
                 self._deconv_out(prog, L.name, a_prev, nat, self.fake, B, L, pad, Pg[L.name + "/biases"], TANH)
@@ -463,13 +519,14 @@ class HipEngine:
             else:
                 rpg = B * L.out_hw ** 2
                 P = self._stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True)
+                hold = {}
                 if P is not None:
                     # BN partial statistics straight from the conv epilogue (tiles never straddle
                     # the real/fake boundary)
                     part = self._stats_buf(L.bn, P, L.cout)
                     self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                 L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg,
-                                bkn=True)
+                                bkn=True, fin=self._fin_fwd(prog, L.bn, rows, L.cout, 2, P, update_ema, hold))
                 else:  # odd sizes: no tile divides the group -> separate group-aligned stats pass
                     self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                 L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], bkn=True)
@@ -479,7 +536,7 @@ class HipEngine:
                     prog.colstats(L.bn + ".stats", 0, _p(self.d_x[L.name]), 0, 0, 0, 0, 0, 0.0, rows, L.cout, rpb,
                                   rpg, _p(part), 0)
                 self._bn_fwd(prog, L.bn, self.d_x[L.name], self.d_a[L.name], rows, L.cout, 2, LRELU, part, P // 2,
-                             update_ema)
+                             update_ema, fused=bool(hold))
             prev = self.d_a[L.name]
         lin = cfg.d_lin_name
         # head GEMV + the fused 3-loss BCE in its last-arriving block
@@ -506,8 +563,9 @@ class HipEngine:
                 self._bn_bwd(prog, L.bn, self.d_x[L.name], da, a, dx, rows, L.cout, 2, LRELU, Pd, gD,
                              self.coef[L.bn], write_param_grads=True, fused=fused_next)
             elif fused_next is not None:  # dx already stored by the upper dgrad GEMM; db from its partials
-                part, Pn = fused_next
-                prog.sum_partials(L.name + ".dbias", _p(part), Pn, 2 * L.cout, L.cout, _p(gD[L.name + "/biases"]), 0)
+                part, Pn = fused_next[0], fused_next[1]
+                if not (len(fused_next) > 2 and fused_next[2].get("fused")):  # (else summed by the GEMM)
+                    prog.sum_partials(L.name + ".dbias", _p(part), Pn, 2 * L.cout, L.cout, _p(gD[L.name + "/biases"]), 0)
             else:  # live bias (no BN after it): db = sum over rows of dx, fused with the act backward
                 self._act_bwd_dbias(prog, L.name + ".act_bwd", da, a, dx, rows, L.cout, LRELU, gD[L.name + "/biases"],
                                     "d")
@@ -536,15 +594,16 @@ class HipEngine:
                 kw = {}
                 out = self.d_da[P_.name]
                 if P_.bn:
-                    r = self._dgrad_bnb(1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.bn,
-                                        self.d_x[P_.name], self.d_a[P_.name], 2, LRELU)
+                    r = self._dgrad_bnb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                                        P_.bn, self.d_x[P_.name], self.d_a[P_.name], 2, LRELU,
+                                        fin=(Pd, gD, self.coef[P_.bn]))
                     if r is not None:
-                        kw, fused_next = r[0], (r[1], r[2])
+                        kw, fused_next = r[0], (r[1], r[2], r[3])
                 else:
-                    r = self._dgrad_actb(1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.name,
-                                         self.d_a[P_.name], LRELU)
+                    r = self._dgrad_actb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                                         P_.name, self.d_a[P_.name], LRELU, db=gD[P_.name + "/biases"])
                     if r is not None:
-                        kw, fused_next, out = r[0], (r[1], r[2]), self.d_dx[P_.name]
+                        kw, fused_next, out = r[0], (r[1], r[2], r[3]), self.d_dx[P_.name]
                 self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
                             L.in_hw, L.in_hw, L.cin, pad, **kw)
 
@@ -619,8 +678,10 @@ class HipEngine:
             mean = mean[row_offset_groups:row_offset_groups + 1]
             rstd = rstd[row_offset_groups:row_offset_groups + 1]
         rpg = rows // groups
+        done = False
         if fused is not None:
-            part, ppg = fused
+            part, ppg = fused[0], fused[1]
+            done = len(fused) > 2 and bool(fused[2].get("fused"))  # finalize ran inside the GEMM
             Pn = ppg * groups
         else:
             rpb = self._rows_per_block(rpg, C)
@@ -630,8 +691,9 @@ class HipEngine:
                           self.cfg.lrelu_leak, rows, C, rpb, rpg, _p(part), 0)
         dg = grads[name + "/gamma"] if write_param_grads else None
         db = grads[name + "/beta"] if write_param_grads else None
-        prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg), _p(P[name + "/gamma"]),
-                             _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
+        if not done:
+            prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg),
+                                 _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
         prog.bn_bwd_apply(name + ".bwd_apply", _p(dy), _p(y), _p(x), _p(coef), _p(dx), rows, C, rpg, act,
                           self.cfg.lrelu_leak, 0)
 
@@ -660,15 +722,16 @@ class HipEngine:
                 kw = {}
                 out = self.gc_da[P_.name]
                 if P_.bn:
-                    r = self._dgrad_bnb(1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False, P_.bn,
-                                        half(self.d_x[P_.name]), half(self.d_a[P_.name]), 1, LRELU, group_offset=1)
+                    r = self._dgrad_bnb(prog, 1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                                        P_.bn, half(self.d_x[P_.name]), half(self.d_a[P_.name]), 1, LRELU,
+                                        group_offset=1, fin=(Pd, None, self.coef_g[P_.bn]))
                     if r is not None:
-                        kw, fused_next = r[0], (r[1], r[2])
+                        kw, fused_next = r[0], (r[1], r[2], r[3])
                 else:
-                    r = self._dgrad_actb(1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                    r = self._dgrad_actb(prog, 1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
                                          "g." + P_.name, half(self.d_a[P_.name]), LRELU)
                     if r is not None:
-                        kw, fused_next, out = r[0], (r[1], r[2]), self.gc_dx[P_.name]
+                        kw, fused_next, out = r[0], (r[1], r[2], r[3]), self.gc_dx[P_.name]
                 self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, out, B, L.out_hw,
                             L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, **kw)
             else:
@@ -694,23 +757,23 @@ class HipEngine:
                            Lg.in_hw, Lg.in_hw, padL, padL, self.kp_g, 0)
             self._wgrad(prog, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
                         0, gG[Lg.name + "/w"])
-            r = self._dgrad_bnb(2, B, 1, 1, self.kp_g, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev, a_prev, 1,
-                                RELU)
+            r = self._dgrad_bnb(prog, 2, B, 1, 1, self.kp_g, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev,
+                                a_prev, 1, RELU, fin=(Pg, gG, self.coef[bn_prev]))
             fused_next = None
             kw = {}
             if r is not None:
-                kw, fused_next = r[0], (r[1], r[2])
+                kw, fused_next = r[0], (r[1], r[2], r[3])
             self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, wL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
                         Lg.in_hw, Lg.cin, 0, bkn=True, kb_valid=25 * Lg.cout, **kw)
         else:
             self._wgrad(prog, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
                         Lg.cin, padL, gG[Lg.name + "/w"])
-            r = self._dgrad_bnb(0, B, Lg.out_hw, Lg.out_hw, Lg.cout, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev,
-                                a_prev, 1, RELU)
+            r = self._dgrad_bnb(prog, 0, B, Lg.out_hw, Lg.out_hw, Lg.cout, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev,
+                                x_prev, a_prev, 1, RELU, fin=(Pg, gG, self.coef[bn_prev]))
             fused_next = None
             kw = {}
             if r is not None:
-                kw, fused_next = r[0], (r[1], r[2])
+                kw, fused_next = r[0], (r[1], r[2], r[3])
             self._igemm(prog, Lg.name + ".dgrad", 0, self.img_g, wL, da_prev, B, Lg.out_hw, Lg.out_hw, Lg.cout,
                         Lg.in_hw, Lg.in_hw, Lg.cin, padL, bkn=True, **kw)
         for j in range(n - 2, -1, -1):
@@ -726,12 +789,12 @@ class HipEngine:
             pad = same_pads(L.out_hw)[0]
             self._wgrad(prog, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
                         gG[L.name + "/w"])
-            r = self._dgrad_bnb(0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc, src, 1,
-                                RELU)
+            r = self._dgrad_bnb(prog, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc,
+                                src, 1, RELU, fin=(Pg, gG, self.coef[bsrc]))
             fused_next = None
             kw = {}
             if r is not None:
-                kw, fused_next = r[0], (r[1], r[2])
+                kw, fused_next = r[0], (r[1], r[2], r[3])
             self._igemm(prog, L.name + ".dgrad", 0, dx, self.wbf_g[L.name + "/w"], dsrc, B, L.out_hw, L.out_hw,
                         L.cout, L.in_hw, L.in_hw, L.cin, pad, bkn=True, **kw)
         # g_bn0 backward + projection gradients
