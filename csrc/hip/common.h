@@ -102,6 +102,12 @@ __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t o
 
 constexpr uint32_t OOB = 0xF8000000u;  // any offset past the descriptor size (operands < OOB bytes)
 
+// offset, or past the descriptor's range when !ok (a buffer load then returns zeros): arithmetic,
+// not a select, so hipcc emits no exec-mask branch per load (valid offsets < OOB by host checks)
+__device__ __forceinline__ uint32_t oob_unless(bool ok, uint32_t off) {
+  return off | (((uint32_t)ok - 1u) & OOB);
+}
+
 // 16-byte LDS-DMA: buffer_load_dwordx4 ... lds. The wave's 64 lanes write 1 KiB contiguously at
 // `lds` (wave-uniform) + 16 * lane; the global offset is per lane (out of range -> zeros).
 __device__ __forceinline__ void buf_load16_lds(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t off) {
@@ -110,12 +116,27 @@ __device__ __forceinline__ void buf_load16_lds(__amdgpu_buffer_rsrc_t r, void* l
 #endif
 }
 
+// 32-bit LDS address space (ds_* addressing: no generic-pointer null checks)
+typedef __attribute__((address_space(3))) char lds_char;
+
 // The same 16-byte LDS-DMA as inline asm. hipcc cannot tell which LDS bytes a DMA writes, so
 // after the builtin form it waits vmcnt(0) before the next ds_read of ANY LDS address -- which
 // drains the tile just issued for the NEXT k-step and serialises load and compute. Hidden in
 // asm, the DMA is invisible to its waitcnt pass; the caller orders it with explicit counted
 // `s_waitcnt vmcnt(N)` + barrier (and must not mix it with compiler-visible vector loads in
 // the same pipelined span). M0 write -> LDS-DMA needs one wait state (s_nop 0).
+// variant taking the wave-uniform LDS byte address directly (keeps per-piece addressing in SGPRs)
+__device__ __forceinline__ void dma16_asm_la(__amdgpu_buffer_rsrc_t r, uint32_t la_in, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t la = __builtin_amdgcn_readfirstlane(la_in);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(la), "v"(off), "s"(r) : "memory", "m0");
+#pragma clang diagnostic pop
+#endif
+}
+
 __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t off) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);

@@ -46,8 +46,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   static_assert(WM * WN == 4, "4 waves");
   static_assert(FM >= 1 && FN >= 1, "tile");
   __shared__ __attribute__((aligned(16))) u32x4 lds[2 * STAGE];
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_char*)lds;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int phase = blockIdx.z;
   const IGemmPhase* ph = p.ph + phase;
@@ -99,15 +100,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   }
 
   auto a_offset = [&](int i, int dy, int dx, int cc, bool kval) -> uint32_t {
-    uint32_t off = OOB;
-    if (p.plain) {
-      if (a_ok[i] && kval) off = (uint32_t)(a_bh[i] * Kc + cc) * 2u;
-    } else {
-      const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
-      if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
-        off = (uint32_t)(((a_bh[i] + iy) * p.W + ix) * Kc + cc) * 2u;
-    }
-    return off;
+    if (p.plain) return oob_unless(a_ok[i] && kval, (uint32_t)(a_bh[i] * Kc + cc) * 2u);
+    const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
+    return oob_unless(a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W,
+                      (uint32_t)(((a_bh[i] + iy) * p.W + ix) * Kc + cc) * 2u);
   };
 
   u32x4 ra_reg[STAGING ? 1 : A_PT], rb_reg[STAGING ? 1 : B_PT];
@@ -120,21 +116,22 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     int dy = 0, dx = 0, wt = 0;
     if (!p.plain) { dy = ph->dy[ti]; dx = ph->dx[ti]; wt = ph->wtap[ti]; }
     if constexpr (STAGING) {
-      u32x4* sa = lds + buf * STAGE;
-      u32x4* sb = sa + BM * 8;
+      // asm LDS-DMA (common.h dma16_asm): the compiler-visible builtin made hipcc wait
+      // vmcnt before every further DMA (measured: s_waitcnt vmcnt(3) between pieces)
+      const uint32_t sa = lds_base + buf * STAGE * 16;
+      const uint32_t sb = sa + BM * 128;
 #pragma unroll
       for (int i = 0; i < PPW_A; ++i) {
         const int q = wave + 4 * i;
         if (NPA % 4 == 0 || q < NPA)
-          buf_load16_lds(ra, sa + q * 64, a_offset(i, dy, dx, cc, kval));
+          dma16_asm_la(ra, sa + q * 1024, a_offset(i, dy, dx, cc, kval));
       }
 #pragma unroll
       for (int i = 0; i < PPW_B; ++i) {
         const int q = wave + 4 * i;
         if (NPB % 4 == 0 || q < NPB) {
           const int n = n0 + 8 * q + (lane >> 3);
-          const uint32_t off = (n < N && kval) ? (uint32_t)((wt * N + n) * Kc + cc) * 2u : OOB;
-          buf_load16_lds(rb, sb + q * 64, off);
+          dma16_asm_la(rb, sb + q * 1024, oob_unless(n < N && kval, (uint32_t)((wt * N + n) * Kc + cc) * 2u));
         }
       }
     } else {

@@ -53,13 +53,20 @@ __device__ __forceinline__ f32x4 load16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t o
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CPOL_SC1));
 }
 
+// Timing studies (DCGAN_IGEMM_ABLATE / DCGAN_IGEMM_STAMPS) need a build with
+// -DDCG_IGEMM_STUDY=1; production kernels carry no runtime study branches.
+#ifndef DCG_IGEMM_STUDY
+#define DCG_IGEMM_STUDY 0
+#endif
+
 template <int N_>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int BKN, int NS>
+template <int BM, int BN, int WM, int WN, int BKN, int NS, int PL>
 __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
+  constexpr bool kStudy = DCG_IGEMM_STUDY != 0;
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -76,11 +83,14 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   static_assert(FM >= 1 && FN >= 1, "tile");
   static_assert(!BKN || (SB <= 1024 && 1024 % SB == 0), "k-major B rows");
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  lds_char* const lds3 = (lds_char*)lds;            // LDS address space: 32-bit ds_* addressing
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds3;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: every per-wave LDS / DMA address below stays in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  // diagnostics: [start, K loop start, K loop end, end] per workgroup (off in production)
-  unsigned long long* stamp = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  // diagnostics: [start, K loop start, K loop end, end] per workgroup (study builds only)
+  unsigned long long* stamp = (kStudy && p.stamps) ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
   if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memtime();
 
   // ---- tile decode (XCD-aware): t -> (phase, mt, nt, split), split fastest
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     return;
   }
   const int Kc = p.Kc, N = p.N;
-  const int ntaps = p.plain ? 1 : ph.ntaps;
+  const int ntaps = PL ? 1 : ph.ntaps;
   const int kt_per_tap = (Kc + BK - 1) / BK;
   const int KT = ntaps * kt_per_tap;
   const int kps = (KT + S - 1) / S;  // per phase: deconv phases have 9 / 6 / 6 / 4 taps
@@ -128,8 +138,9 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   // ablation (timing only, outputs wrong): bit 0 / 1 a zero-size descriptor drops every A / B
   // fetch (the LDS-DMA still writes zeros), bit 2 skips fragment reads + MFMAs, bit 3 skips the
   // LDS-DMA issue altogether
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, (p.ablate & 1) ? 0u : p.a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, (p.ablate & 2) ? 0u : p.b_bytes);
+  const int ablate = kStudy ? p.ablate : 0;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, (ablate & 1) ? 0u : p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, (ablate & 2) ? 0u : p.b_bytes);
 
   // ---- A rows of this lane: piece q = wave + 4 i, row = 8 q + lane / 8, slot = lane & 7,
   //      global 16-byte chunk = slot ^ (row & 7)
@@ -141,7 +152,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     const int r = 8 * (wave + NW * i) + (lane >> 3);
     const int m = m0 + r;
     a_ok[i] = m < M;
-    if (p.plain) {
+    if constexpr (PL) {
       a_base[i] = m * Kc; a_iy[i] = 0; a_ix[i] = 0;
     } else {
       const uint32_t b = fdiv((uint32_t)m, ph.fd_hw);
@@ -161,10 +172,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   int cur_c0 = (kt0 - cur_ti * kt_per_tap) * BK;
 
   auto issue = [&](int slot) {
-    char* sa = lds + slot * STAGE;
-    char* sb = sa + A_BYTES;
+    const uint32_t sa = lds_base + slot * STAGE;
+    const uint32_t sb = sa + A_BYTES;
     int dy = 0, dx = 0, wt = 0;
-    if (!p.plain) {
+    if constexpr (!PL) {
       const int ti = ph.tap[cur_ti];  // scalar load (kernarg): no vector load inside the pipelined loop
       dy = (int)(signed char)(ti & 0xff);
       dx = (int)(signed char)((ti >> 8) & 0xff);
@@ -172,34 +183,33 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     }
     const int cc = cur_c0 + a_chunk * 8;
     const bool kval = cc < Kc;
-    const int tap_delta = (dy * p.W + dx) * Kc;
+    const int tap_delta = (dy * p.W + dx) * Kc + cc;
+    // branch-free: every lane computes its offset, a select turns invalid ones into OOB (zero fill)
 #pragma unroll
     for (int i = 0; i < PPW_A; ++i) {
-      uint32_t off = OOB;
-      if (p.plain) {
-        if (a_ok[i] && kval) off = (uint32_t)(a_base[i] + cc) * 2u;
-      } else {
+      bool ok = a_ok[i] && kval;
+      if constexpr (!PL) {
         const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
-        if (a_ok[i] && kval && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
-          off = (uint32_t)(a_base[i] + tap_delta + cc) * 2u;
+        ok = ok && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
       }
-      dma16_asm(ra, sa + (wave + NW * i) * 1024, off);
+      const uint32_t off = oob_unless(ok, (uint32_t)(a_base[i] + (PL ? cc : tap_delta)) * 2u);
+      dma16_asm_la(ra, sa + (wave + NW * i) * 1024, off);
     }
 #pragma unroll
     for (int i = 0; i < PPW_B; ++i) {
       const int q = wave + NW * i;
-      uint32_t off = OOB;
+      uint32_t off;
       if constexpr (BKN) {
         const int rr = q * B_ROWS_PER_PIECE + lane / (SB / 16);
         const int k = cur_c0 + rr;
         const int n = n0 + ((lane % (SB / 16)) ^ (kn_swz<SB>(rr) >> 1)) * 8;
-        if (k < p.kb_valid && n < N) off = (uint32_t)((wt * Kc + k) * N + n) * 2u;
+        off = oob_unless(k < p.kb_valid && n < N, (uint32_t)((wt * Kc + k) * N + n) * 2u);
       } else {
         const int n = n0 + 8 * q + (lane >> 3);
         const int c = cur_c0 + a_chunk * 8;
-        if (n < N && c < Kc && c < p.kb_valid) off = (uint32_t)((wt * N + n) * Kc + c) * 2u;
+        off = oob_unless(n < N && c < Kc && c < p.kb_valid, (uint32_t)((wt * N + n) * Kc + c) * 2u);
       }
-      dma16_asm(rb, sb + q * 1024, off);
+      dma16_asm_la(rb, sb + q * 1024, off);
     }
     cur_c0 += BK;
     if (cur_c0 >= Kc) { cur_c0 = 0; ++cur_ti; }
@@ -213,7 +223,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
 
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nk && !(p.ablate & 8)) issue(s);
+    if (s < nk && !(ablate & 8)) issue(s);
 
   const int fr = lane & 15, fq = lane >> 4;
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
@@ -231,10 +241,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     // younger DMA tiles and flattens the pipeline (LDS reads of the previous tile have all
     // returned: their values fed the MFMAs already).
     asm volatile("s_barrier" ::: "memory");
-    if (kt + NS - 1 < nk && !(p.ablate & 8)) issue((kt + NS - 1) % NS);
-    if (p.ablate & 4) continue;  // timing study: no fragment reads / MFMAs
-    const char* sa = lds + (kt % NS) * STAGE;
-    const char* sb = sa + A_BYTES;
+    if (kt + NS - 1 < nk && !(ablate & 8)) issue((kt + NS - 1) % NS);
+    if (ablate & 4) continue;  // timing study: no fragment reads / MFMAs
+    const lds_char* sa = lds3 + (kt % NS) * STAGE;
+    const lds_char* sb = sa + A_BYTES;
     // all fragments of the k-tile first (both k32 halves: the second half's LDS reads are in
     // flight while the first half's MFMAs run), then one prioritised MFMA cluster
     elem8 af[2][FM], bfr[2][FN];
@@ -244,7 +254,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * TM + i * 16 + fr;
-        af[ks][i] = *reinterpret_cast<const elem8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
+        af[ks][i] = *reinterpret_cast<const __attribute__((address_space(3))) elem8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
       }
       if constexpr (BKN) {
 #pragma unroll
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int r = wn * TN + j * 16 + fr;
-          bfr[ks][j] = *reinterpret_cast<const elem8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
+          bfr[ks][j] = *reinterpret_cast<const __attribute__((address_space(3))) elem8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
         }
       }
     }
@@ -342,7 +352,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     const int m = m0 + r;
     int off = -1;
     if (m < M) {
-      if (p.plain) {
+      if constexpr (PL) {
         off = m * p.ldc;
       } else {
         const uint32_t b = fdiv((uint32_t)m, ph.fd_hw);
@@ -436,7 +446,23 @@ extern "C" int DCG_API(dcg_igemm3_tile)(int cfg, int* bm, int* bn, int* ns) {
 template <int BM, int BN, int WM, int WN, int BKN, int NS>
 static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
   constexpr size_t shm = (size_t)NS * (BM + BN) * 64 * 2;
-  auto k = dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS>;
+  // plain (im2col'd) GEMMs read their weight k-major only (the host never asks otherwise)
+  if constexpr (BKN) {
+    if (a->plain) {
+      auto k = dcg::igemm3_kernel<BM, BN, WM, WN, 1, NS, 1>;
+      static bool attr_set = false;
+      if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+      }
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), shm, s, *a);
+      return (int)hipGetLastError();
+    }
+  } else {
+    if (a->plain) return -1;
+  }
+  auto k = dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS, 0>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

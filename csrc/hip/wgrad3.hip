@@ -49,8 +49,10 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
   static_assert(A_BYTES % 4096 == 0 && B_BYTES % 4096 == 0, "every wave issues the same DMA count");
   static_assert(SA <= 1024 && SB <= 1024 && FM >= 1 && FN >= 1, "tile");
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  lds_char* const lds3 = (lds_char*)lds;  // 32-bit LDS addressing
+  const uint32_t lds_base = (uint32_t)(uintptr_t)lds3;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
 
   // ---- tile decode: XCD remap (each XCD gets a contiguous run of t), then tap fastest
@@ -96,29 +98,25 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
 
   int cur_k0 = kt0 * BK;  // first pixel of the next tile to issue
   auto issue = [&](int slot) {
-    char* sa = lds + slot * STAGE;
-    char* sb = sa + A_BYTES;
+    const uint32_t sa = lds_base + slot * STAGE;
+    const uint32_t sb = sa + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < PPW_A; ++i) {
+    for (int i = 0; i < PPW_A; ++i) {  // branch-free: invalid lanes get an out-of-range offset
       const int k = cur_k0 + a_row[i];
-      uint32_t off = OOB;
-      if (k < p.K && a_m[i] < p.Mc) {
-        const uint32_t b = fdiv((uint32_t)k, p.fd_hw);
-        const uint32_t rem = (uint32_t)k - b * (uint32_t)(p.Hd * p.Wd);
-        const uint32_t y = fdiv(rem, p.fd_w);
-        const uint32_t x = rem - y * (uint32_t)p.Wd;
-        const int iy = 2 * (int)y + ky - p.pl, ix = 2 * (int)x + kx - p.pl;
-        if ((unsigned)iy < (unsigned)p.Hg && (unsigned)ix < (unsigned)p.Wg)
-          off = (uint32_t)((((int)b * p.Hg + iy) * p.Wg + ix) * p.Mc + a_m[i]) * 2u;
-      }
-      dma16_asm(rg, sa + (wave + 4 * i) * 1024, off);
+      const uint32_t b = fdiv((uint32_t)k, p.fd_hw);
+      const uint32_t rem = (uint32_t)k - b * (uint32_t)(p.Hd * p.Wd);
+      const uint32_t y = fdiv(rem, p.fd_w);
+      const uint32_t x = rem - y * (uint32_t)p.Wd;
+      const int iy = 2 * (int)y + ky - p.pl, ix = 2 * (int)x + kx - p.pl;
+      const bool ok = k < p.K && a_m[i] < p.Mc && (unsigned)iy < (unsigned)p.Hg && (unsigned)ix < (unsigned)p.Wg;
+      dma16_asm_la(rg, sa + (wave + 4 * i) * 1024,
+                   oob_unless(ok, (uint32_t)((((int)b * p.Hg + iy) * p.Wg + ix) * p.Mc + a_m[i]) * 2u));
     }
 #pragma unroll
     for (int i = 0; i < PPW_B; ++i) {
       const int k = cur_k0 + b_row[i];
-      uint32_t off = OOB;
-      if (k < p.K && b_n[i] < p.Nc) off = (uint32_t)(k * p.Nc + b_n[i]) * 2u;
-      dma16_asm(rd, sb + (wave + 4 * i) * 1024, off);
+      dma16_asm_la(rd, sb + (wave + 4 * i) * 1024,
+                   oob_unless(k < p.K && b_n[i] < p.Nc, (uint32_t)(k * p.Nc + b_n[i]) * 2u));
     }
     cur_k0 += BK;
   };
@@ -144,8 +142,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
     // all waves' DMA of tile kt landed; all waves are done reading slot (kt-1) % NS
     asm volatile("s_barrier" ::: "memory");
     if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS);
-    const char* sa = lds + (kt % NS) * STAGE;
-    const char* sb = sa + A_BYTES;
+    const lds_char* sa = lds3 + (kt % NS) * STAGE;
+    const lds_char* sb = sa + A_BYTES;
     elem8 af[2][FM], bfr[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
