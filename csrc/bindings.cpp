@@ -478,6 +478,9 @@ class Program {
       throw std::runtime_error("wgrad3 operand exceeds the 3.875 GiB buffer-descriptor range");
     a.g_bytes = (uint32_t)(g_elems * es_); a.d_bytes = (uint32_t)(d_elems * es_);
     a.fd_hw = fastdiv_make(Hd * Wd); a.fd_w = fastdiv_make(Wd); a.Hd = Hd; a.Wd = Wd;
+    auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
+    a.lhw = lg2(Hd * Wd); a.lw = lg2(Wd);
+    if (a.lhw < 0 || a.lw < 0) a.lhw = a.lw = -1;  // pixel decode by shifts only for power-of-two images
     a.out = P<float>(dst); a.scale = scale;
     AccList acc;
     acc.r(G, g_elems * es_).r(Dm, d_elems * es_).w(dst, (size_t)25 * Mc * Nc * 4);

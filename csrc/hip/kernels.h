@@ -102,6 +102,7 @@ struct WGrad3Args {                 // wgrad3.hip: 25-tap gather GEMM, in-kernel
   float scale;
   float* ws;                           // [tiles][splits][BM*BN] fp32 slabs (splits > 1)
   unsigned* counters;                  // [tiles] arrival counters, zero between launches
+  int lhw, lw;                         // log2(Hd*Wd), log2(Wd) when both are powers of two, else -1
 };
 
 }  // namespace dcg

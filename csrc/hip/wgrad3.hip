@@ -34,7 +34,7 @@ __device__ __forceinline__ void w3_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int P2>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -103,10 +103,18 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
 #pragma unroll
     for (int i = 0; i < PPW_A; ++i) {  // branch-free: invalid lanes get an out-of-range offset
       const int k = cur_k0 + a_row[i];
-      const uint32_t b = fdiv((uint32_t)k, p.fd_hw);
-      const uint32_t rem = (uint32_t)k - b * (uint32_t)(p.Hd * p.Wd);
-      const uint32_t y = fdiv(rem, p.fd_w);
-      const uint32_t x = rem - y * (uint32_t)p.Wd;
+      uint32_t b, y, x;
+      if constexpr (P2) {  // power-of-two images: shifts and masks (every DCGAN resolution but 28)
+        b = (uint32_t)k >> p.lhw;
+        const uint32_t rem = (uint32_t)k & ((1u << p.lhw) - 1u);
+        y = rem >> p.lw;
+        x = rem & ((1u << p.lw) - 1u);
+      } else {
+        b = fdiv((uint32_t)k, p.fd_hw);
+        const uint32_t rem = (uint32_t)k - b * (uint32_t)(p.Hd * p.Wd);
+        y = fdiv(rem, p.fd_w);
+        x = rem - y * (uint32_t)p.Wd;
+      }
       const int iy = 2 * (int)y + ky - p.pl, ix = 2 * (int)x + kx - p.pl;
       const bool ok = k < p.K && a_m[i] < p.Mc && (unsigned)iy < (unsigned)p.Hg && (unsigned)ix < (unsigned)p.Wg;
       dma16_asm_la(rg, sa + (wave + 4 * i) * 1024,
@@ -258,10 +266,10 @@ extern "C" int DCG_API(dcg_wgrad3_tile)(int cfg, int* bm, int* bn, int* ns) {
   return -1;
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
-static int wlaunch3(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
+template <int BM, int BN, int WM, int WN, int NS, int P2>
+static int wlaunch3p(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
   constexpr size_t shm = (size_t)NS * (BM + BN) * 64 * 2;
-  auto k = dcg::wgrad3_kernel<BM, BN, WM, WN, NS>;
+  auto k = dcg::wgrad3_kernel<BM, BN, WM, WN, NS, P2>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
@@ -270,6 +278,11 @@ static int wlaunch3(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
   }
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), shm, s, *a);
   return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+static int wlaunch3(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
+  return a->lhw >= 0 ? wlaunch3p<BM, BN, WM, WN, NS, 1>(a, blocks, s) : wlaunch3p<BM, BN, WM, WN, NS, 0>(a, blocks, s);
 }
 
 extern "C" int DCG_API(dcg_wgrad3_launch)(const dcg::WGrad3Args* a, int cfg, hipStream_t s) {
