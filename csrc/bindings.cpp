@@ -32,6 +32,9 @@
 #include <vector>
 
 #include "hip/kernels.h"
+extern "C" {
+#include "hip/narrow2.inc"
+}
 
 // The fp16 and fp32 builds of the same kernels (csrc/build.py compiles every .hip three times):
 // identical C signatures (element pointers are void-compatible at the ABI level) with `_f16` /
@@ -40,11 +43,13 @@
 #define DCG_API(name) name##_f16
 extern "C" {
 #include "hip/launchers.inc"
+#include "hip/narrow2.inc"
 }
 #undef DCG_API
 #define DCG_API(name) name##_f32
 extern "C" {
 #include "hip/launchers.inc"
+#include "hip/narrow2.inc"
 }
 #undef DCG_API
 #define DCG_API(name) name
@@ -757,6 +762,53 @@ class Program {
     }, AccList().r(x, (size_t)B * H * W * Cin * es_).r(w, (size_t)25 * Cin * Cout * es_).r(bias, (size_t)Cout * 4)
            .w(y, (size_t)B * Ho * Wo * Cout * es_).v);
   }
+  // narrow2.hip: TF-SAME stride-2 5x5 conv, 1..4 input -> 64 output channels, persistent `grid`
+  // workgroups (<= tiles: nconv_tiles). bx != 0: fused BN-backward statistics of the layer below
+  // (x = bx, y = by, one BN group), one partial row [2][64] per workgroup into part.
+  int nconv(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int H, int W, int Cin,
+            int Ho, int Wo, int pad_y, int pad_x, int act, float leak, int grid, uintptr_t bx, uintptr_t by,
+            uintptr_t mean, uintptr_t rstd, int bact, float bleak, uintptr_t part, int stream) {
+    if (dt_ == 2) throw std::runtime_error("nconv: 16-bit builds only");
+    const int tiles = KF(dcg_nconv_tiles)(B, Ho, Wo);
+    if (grid < 1 || grid > tiles) throw std::runtime_error("nconv: grid must be in [1, tiles]");
+    const size_t out = (size_t)B * Ho * Wo * 64 * es_;
+    AccList acc;
+    acc.r(x, (size_t)B * H * W * Cin * es_).r(w, (size_t)25 * Cin * 64 * es_).r(bias, 64 * 4).w(y, out);
+    if (bx) acc.r(bx, out).r(by, out).r(mean, 64 * 4).r(rstd, 64 * 4).w(part, (size_t)grid * 128 * 4);
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_nconv)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B, H, W, Cin,
+                           Ho, Wo, pad_y, pad_x, act, leak, grid, P<const elem_t>(bx), P<const elem_t>(by),
+                           P<const float>(mean), P<const float>(rstd), bact, bleak, P<float>(part), s);
+    }, acc.v);
+  }
+  int nconv_tiles(int B, int Ho, int Wo) const { return KF(dcg_nconv_tiles)(B, Ho, Wo); }
+  bool nwgrad_ok(int H, int W, int Hd, int Wd) const {
+    int t, r, c;
+    return dt_ != 2 && KF(dcg_nwgrad_plan)(H, W, Hd, Wd, &t, &r, &c) == 0;
+  }
+  // narrow2.hip weight gradient of a 1..4-channel image layer: dst[25][Cin][64] (fp32, TF layout)
+  // = sum over output pixels of the stride-2 window of x times d; per-workgroup partials
+  // (workspace) summed in workgroup order by splitk_reduce -- deterministic.
+  int nwgrad(std::string name, uintptr_t x, int B, int H, int W, int Cin, uintptr_t d, int Hd, int Wd, int pad,
+             uintptr_t dst, int stream) {
+    int tyc, wr, wc;
+    if (dt_ == 2 || KF(dcg_nwgrad_plan)(H, W, Hd, Wd, &tyc, &wr, &wc))
+      throw std::runtime_error("nwgrad: unsupported shape / dtype");
+    const int chunks_img = (Hd + tyc - 1) / tyc;
+    const int total = B * chunks_img;
+    int cpw = total / 512;  // >= 512 workgroups where the batch allows it, <= 4 chunks each
+    cpw = cpw < 1 ? 1 : (cpw > 4 ? 4 : cpw);
+    const int wg = B * ((chunks_img + cpw - 1) / cpw);
+    const size_t n = (size_t)25 * Cin * 64;
+    float* part = reinterpret_cast<float*>(dev_alloc((size_t)wg * n * sizeof(float)));
+    add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_nwgrad)(P<const elem_t>(x), B, H, W, Cin, P<const elem_t>(d), Hd, Wd, pad, cpw, part, s);
+    }, AccList().r(x, (size_t)B * H * W * Cin * es_).r(d, (size_t)B * Hd * Wd * 64 * es_)
+           .w((uintptr_t)part, (size_t)wg * n * 4).v);
+    return add(name + ".reduce", stream, [=](hipStream_t s) {
+      return KF(dcg_splitk_reduce)(part, wg, n, P<float>(dst), 1.f, s);
+    }, AccList().r((uintptr_t)part, (size_t)wg * n * 4).w(dst, n * 4).v);
+  }
   // TF-SAME stride-2 5x5 conv_transpose with 1..4 output channels (direct VALU kernel)
   int narrow_deconv(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int Hi, int Wi,
                     int C, int Ho, int Wo, int N, int pad, int act, float leak, int stream) {
@@ -966,6 +1018,10 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("nonfinite_check", &Program::nonfinite_check)
       .def("narrow_deconv", &Program::narrow_deconv)
       .def("conv3_direct", &Program::conv3_direct)
+      .def("nconv", &Program::nconv)
+      .def("nconv_tiles", &Program::nconv_tiles)
+      .def("nwgrad_ok", &Program::nwgrad_ok)
+      .def("nwgrad", &Program::nwgrad)
       .def("pack", &Program::pack)
       .def("philox_uniform", &Program::philox_uniform)
       .def("im2col_s2", &Program::im2col_s2)

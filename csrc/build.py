@@ -12,6 +12,7 @@ package so they travel with the repository snapshot to the GPU box.
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -60,24 +61,44 @@ def _variants(path: str):
     return [VARIANTS[n] for n in names]
 
 
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps(path: str, seen=None):
+    """The file plus every quoted #include it pulls in, transitively (resolved next to the
+    including file, then under csrc/): an edit rebuilds only the objects that see it."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path) as f:
+        text = f.read()
+    for inc in _INCLUDE.findall(text):
+        for base in (os.path.dirname(path), CSRC):
+            cand = os.path.normpath(os.path.join(base, inc))
+            if os.path.exists(cand):
+                _deps(cand, seen)
+                break
+    return seen
+
+
 def build_hip(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
-    hdrs = [os.path.join(CSRC, "hip", h) for h in os.listdir(os.path.join(CSRC, "hip"))
-            if h.endswith((".h", ".inc"))]
     srcs = sorted(os.path.join(CSRC, "hip", f) for f in os.listdir(os.path.join(CSRC, "hip")) if f.endswith(".hip"))
     common = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC]
     jobs_list = []
     objs = []
     for s in srcs:  # every kernel file once per element type it declares (`// dcg-variants:`)
+        deps = sorted(_deps(s))
         for tag, defs in _variants(s):
             o = os.path.join(BUILD, os.path.basename(s) + tag + ".o")
             objs.append(o)
-            if _newer([s] + hdrs, o):
+            if _newer(deps, o):
                 jobs_list.append([HIPCC] + common + defs + ["-c", s, "-o", o])
     binding = os.path.join(CSRC, "bindings.cpp")
     bo = os.path.join(BUILD, "bindings.o")
     objs.append(bo)
-    if _newer([binding] + hdrs, bo):
+    if _newer(sorted(_deps(binding)), bo):
         inc = []
         for i in _py_includes():
             inc += ["-I", i]

@@ -456,6 +456,12 @@ class HipEngine:
                 return rpb
         return 1
 
+    def _g_out_direct(self) -> bool:
+        """G's 1..4-channel output layer backward on narrow2.hip (nconv data gradient + nwgrad)."""
+        L = self.gl[-1]
+        return (not self.f32 and L.cout <= 4 and L.cin == 64
+                and self.progA.nwgrad_ok(L.out_hw, L.out_hw, L.in_hw, L.in_hw))
+
     def _d0_direct(self) -> bool:
         """D layer 0 forward on the direct conv3 kernel (16-bit, Cin <= 4, Cout = 64) instead of
         im2col + GEMM."""
@@ -503,10 +509,10 @@ class HipEngine:
             w = Wd[L.name + "/w"]  # HWIO [5,5,ci,co] = [tap][K][N]
             pad = same_pads(L.in_hw)[0]
             rows = B2 * L.out_hw ** 2
-            if i == 0 and self._d0_direct():  # image tile in LDS, no column matrix (conv3.hip)
-                prog.conv3_direct("d0.conv3", _p(prev), _p(w), _p(Pd[L.name + "/biases"]), _p(self.d_a[L.name]), B2,
-                                  L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad, pad, LRELU,
-                                  cfg.lrelu_leak, 0)
+            if i == 0 and self._d0_direct():  # persistent direct MFMA conv, no column matrix (narrow2.hip)
+                prog.nconv("d0.nconv", _p(prev), _p(w), _p(Pd[L.name + "/biases"]), _p(self.d_a[L.name]), B2,
+                           L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, pad, pad, LRELU, cfg.lrelu_leak,
+                           H.nconv_grid(prog, B2, L.out_hw, L.out_hw), 0, 0, 0, 0, 0, 0.0, 0, 0)
             elif i == 0 and L.cin % 8 != 0:
                 prog.im2col_s2("d0.im2col", _p(prev), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                L.out_hw, pad, pad, self.kp_d0, 0)
@@ -572,9 +578,12 @@ class HipEngine:
             # weight gradient
             src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
             pad = same_pads(L.in_hw)[0]
-            if i == 0 and L.cin % 8 != 0:
-                if self._d0_direct():  # the forward ran without a column matrix: build it here, off the
-                    # critical path (D's chain is the shorter of the two concurrent backward chains)
+            if i == 0 and self._d0_direct() and prog.nwgrad_ok(L.in_hw, L.in_hw, L.out_hw, L.out_hw):
+                # image window staged per workgroup, no column matrix (narrow2.hip nwgrad)
+                prog.nwgrad(L.name + ".nwgrad", _p(self.d_in), B2, L.in_hw, L.in_hw, L.cin, _p(dx), L.out_hw,
+                            L.out_hw, pad, _p(gD[L.name + "/w"]), 0)
+            elif i == 0 and L.cin % 8 != 0:
+                if self._d0_direct():  # the forward ran without a column matrix: build it here
                     prog.im2col_s2("d0.im2col", _p(self.d_in), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin,
                                    L.out_hw, L.out_hw, pad, pad, self.kp_d0, 0)
                 self._wgrad(prog, L.name, 2, self.d0_col, 1, 1, self.kp_d0, dx, B2 * L.out_hw ** 2, 1, 1, L.cout, 0,
@@ -752,7 +761,20 @@ class HipEngine:
         bn_prev = self.gl[-2].bn if n > 1 else "g_bn0"
         padL = same_pads(Lg.out_hw)[0]
         wL = self.wbf_g[Lg.name + "/w"]  # [5,5,co,ci] read as [tap][K=co][N=ci]
-        if Lg.cout % 8 != 0:
+        if self._g_out_direct():
+            # narrow2.hip: the data gradient is the stride-2 conv of the image gradient with the
+            # [5,5,co,ci] = HWIO[5,5,3,64] weight (nconv, BN-backward statistics of the layer below
+            # fused), the weight gradient reads the image gradient's window directly (nwgrad)
+            grid = H.nconv_grid(prog, B, Lg.in_hw, Lg.in_hw)
+            part = self._stats_buf(bn_prev + ".bwd", grid, Lg.cin)
+            st = self.bn[bn_prev]
+            prog.nconv(Lg.name + ".dgrad", _p(self.img_g), _p(wL), 0, _p(da_prev), B, Lg.out_hw, Lg.out_hw, Lg.cout,
+                       Lg.in_hw, Lg.in_hw, padL, padL, NONE, 0.0, grid, _p(x_prev), _p(a_prev), _p(st["mean"]),
+                       _p(st["rstd"]), RELU, cfg.lrelu_leak, _p(part), 0)
+            fused_next = (part, grid, {})
+            prog.nwgrad(Lg.name + ".nwgrad", _p(self.img_g), B, Lg.out_hw, Lg.out_hw, Lg.cout, _p(a_prev), Lg.in_hw,
+                        Lg.in_hw, padL, _p(gG[Lg.name + "/w"]), 0)
+        elif Lg.cout % 8 != 0:
             prog.im2col_s2("g_out.im2col", _p(self.img_g), _p(self.g_last_col), B, Lg.out_hw, Lg.out_hw, Lg.cout,
                            Lg.in_hw, Lg.in_hw, padL, padL, self.kp_g, 0)
             self._wgrad(prog, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,

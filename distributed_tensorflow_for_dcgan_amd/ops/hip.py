@@ -449,6 +449,48 @@ def conv3_direct(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     return y
 
 
+NCONV_MAX_GRID = 512  # persistent workgroups of nconv (2 per CU: the kernel's occupancy)
+
+
+def nconv_grid(prog, B: int, Ho: int, Wo: int) -> int:
+    """Persistent workgroup count of an nconv launch (= its BN-backward partial rows)."""
+    return min(prog.nconv_tiles(B, Ho, Wo), NCONV_MAX_GRID)
+
+
+def nconv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
+          leak: float = 0.2, bnb: Optional[tuple] = None):
+    """TF-SAME stride-2 5x5 conv with Cin <= 4 and Cout = 64 on narrow2.hip's persistent MFMA
+    kernel. x [B,H,W,Cin], w HWIO [5,5,Cin,64]. bnb = (bx, by, mean[64], rstd[64], act): also
+    the BN-backward partial statistics (sum g, sum g*xhat), g = y_out * act'(by) -- returned as
+    [grid][2][64] next to the output."""
+    _check_bf16(x, w)
+    B, Hh, Ww, C = x.shape
+    Ho, Wo = -(-Hh // 2), -(-Ww // 2)
+    y = torch.empty(B, Ho, Wo, 64, device=x.device, dtype=x.dtype)
+    prog = ext().Program(x.dtype == torch.float16)
+    grid = nconv_grid(prog, B, Ho, Wo)
+    part = torch.empty(grid, 2, 64, device=x.device) if bnb is not None else None
+    bx, by, mean, rstd, bact = bnb if bnb is not None else (None, None, None, None, None)
+    prog.nconv("nconv", _p(x), _p(w), _p(bias), _p(y), B, Hh, Ww, C, Ho, Wo, same_pads(Hh)[0], same_pads(Ww)[0],
+               ACT[act], leak, grid, _p(bx), _p(by), _p(mean), _p(rstd), ACT[bact], leak, _p(part), 0)
+    run(prog)
+    return (y, part) if bnb is not None else y
+
+
+def nwgrad(x: torch.Tensor, d: torch.Tensor, pad: int) -> torch.Tensor:
+    """Weight gradient of a 1..4-channel stride-2 5x5 layer (narrow2.hip): out[25][Cin][64] =
+    sum over d's pixels of the stride-2 window of x (top/left padding `pad`) times d."""
+    _check_bf16(x, d)
+    B, Hh, Ww, C = x.shape
+    _, Hd, Wd, N = d.shape
+    assert N == 64
+    out = torch.empty(25, C, 64, device=x.device)
+    prog = ext().Program(x.dtype == torch.float16)
+    prog.nwgrad("nwgrad", _p(x), B, Hh, Ww, C, _p(d), Hd, Wd, pad, _p(out), 0)
+    run(prog)
+    return out
+
+
 def narrow_deconv(x: torch.Tensor, w: torch.Tensor, out_hw: Tuple[int, int], bias: Optional[torch.Tensor] = None,
                   act: Optional[str] = None, leak: float = 0.2) -> torch.Tensor:
     """TF-SAME stride-2 5x5 conv_transpose with N <= 4 output channels on the direct VALU

@@ -597,6 +597,75 @@ def test_conv3_direct(B, Hh, C, dtype):
     close(y, ref, 1e-2, "conv3 direct")
 
 
+@pytest.mark.parametrize("B,Hh,C,dtype", [(4, 64, 3, "bf16"), (2, 28, 1, "bf16"), (3, 33, 4, "bf16"),
+                                          (2, 64, 3, "fp16"), (1, 7, 3, "bf16"), (2, 128, 3, "bf16"),
+                                          (80, 64, 3, "bf16")])
+def test_nconv(B, Hh, C, dtype):
+    """narrow2.hip nconv (persistent, Cin <= 4 -> 64, + bias + lrelu) vs the fp32 TF-SAME oracle:
+    RGB / gray / 4-channel, odd sizes (partial tiles, pad 2 at 7 and 33), two column tiles
+    (128 -> 64 wide), more tiles than workgroups (80 images: the persistent loop), fp16 build."""
+    h = H()
+    edt = torch.float16 if dtype == "fp16" else torch.bfloat16
+    x = rnd(B, Hh, Hh, C, seed=70).to(edt)
+    w = rnd(5, 5, C, 64, scale=0.1, seed=71).to(edt)
+    bias = rnd(64, scale=0.1, seed=72)
+    y = h.nconv(x, w, bias=bias, act="lrelu")
+    ref = R.lrelu(R.conv2d_same(x.float(), w.float(), bias))
+    close(y, ref, 1e-2, "nconv")
+
+
+@pytest.mark.parametrize("B,Hh,act", [(4, 64, "relu"), (3, 33, "lrelu"), (70, 64, "relu")])
+def test_nconv_bn_backward_stats(B, Hh, act):
+    """nconv as G's RGB-layer data gradient (no bias / act) with the BN-backward statistics of
+    the layer below fused: the stored dL/da equals the plain conv; the per-workgroup partials
+    sum to (sum g, sum g*xhat), g = dL/da * act'(y), of the stored (rounded) values."""
+    h = H()
+    Ho = -(-Hh // 2)
+    dimg = bf(rnd(B, Hh, Hh, 3, seed=73))
+    w = bf(rnd(5, 5, 3, 64, scale=0.1, seed=74))
+    x = bf(rnd(B, Ho, Ho, 64, seed=75))
+    y = bf(rnd(B, Ho, Ho, 64, seed=76) - 0.3)
+    mean = rnd(64, scale=0.2, seed=77)
+    rstd = rnd(64, seed=78).abs() + 0.5
+    da, part = h.nconv(dimg, w, bnb=(x, y, mean, rstd, act))
+    ref = R.conv2d_same(dimg.float(), w.float())
+    close(da, ref, 1e-2, "nconv dgrad")
+    assert torch.equal(da, h.nconv(dimg, w))
+    slope = 0.2 if act == "lrelu" else 0.0
+    g = da.float() * torch.where(y.float() > 0, 1.0, slope)
+    xh = (x.float() - mean) * rstd
+    s = part.sum(0)
+    close(s[0], g.reshape(-1, 64).sum(0), 2e-3, "sum g")
+    close(s[1], (g * xh).reshape(-1, 64).sum(0), 2e-3, "sum g xhat")
+
+
+@pytest.mark.parametrize("B,Hh,C,dtype", [(4, 64, 3, "bf16"), (2, 28, 1, "bf16"), (3, 33, 4, "bf16"),
+                                          (2, 64, 3, "fp16"), (1, 7, 3, "bf16"), (2, 128, 3, "bf16"),
+                                          (40, 64, 3, "bf16")])
+def test_nwgrad(B, Hh, C, dtype):
+    """narrow2.hip nwgrad vs autograd: the conv role (D layer 0: x = image, d = dL/d(conv out))
+    and the deconv role (G's RGB layer: x = dL/d(deconv out), d = the layer input, TF layout
+    [5,5,co,ci]); gray / 4-channel, odd sizes, 64-wide outputs (4-row chunks), several chunks
+    per workgroup (40 images), fp16; a second launch gives the same bits."""
+    h = H()
+    edt = torch.float16 if dtype == "fp16" else torch.bfloat16
+    Ho = -(-Hh // 2)
+    pad = max((Ho - 1) * 2 + 5 - Hh, 0) // 2
+    x = rnd(B, Hh, Hh, C, seed=90).to(edt)
+    w = rnd(5, 5, C, 64, scale=0.05, seed=91).requires_grad_(True)
+    dy = rnd(B, Ho, Ho, 64, seed=92).to(edt)
+    (gw,) = torch.autograd.grad(R.conv2d_same(x.float(), w), w, dy.float())
+    out = h.nwgrad(x, dy, pad)
+    close(out.reshape(5, 5, C, 64), gw, 3e-3, "nwgrad conv")
+    assert torch.equal(out, h.nwgrad(x, dy, pad))
+    # deconv role: Y = deconv(X) [B,Hh,Hh,C] from X [B,Ho,Ho,64], W [5,5,C,64]
+    Xd = rnd(B, Ho, Ho, 64, seed=93).to(edt)
+    wd = rnd(5, 5, C, 64, scale=0.05, seed=94).requires_grad_(True)
+    dyd = rnd(B, Hh, Hh, C, seed=95).to(edt)
+    (gwd,) = torch.autograd.grad(R.conv2d_transpose_same(Xd.float(), wd, (Hh, Hh)), wd, dyd.float())
+    close(h.nwgrad(dyd, Xd, pad).reshape(5, 5, C, 64), gwd, 3e-3, "nwgrad deconv")
+
+
 @pytest.mark.parametrize("P,groups,C", [(2048, 2, 80), (700, 1, 512), (96, 2, 64)])
 def test_bn_finalize_split_paths(P, groups, C):
     """Many partial rows -> the sliced finalize with a last-arrival combine (counters reset, so a
