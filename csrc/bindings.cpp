@@ -782,6 +782,22 @@ class Program {
     }, acc.v);
   }
   int nconv_tiles(int B, int Ho, int Wo) const { return KF(dcg_nconv_tiles)(B, Ho, Wo); }
+  // G's RGB-layer image gradient with its activation backward fused (narrow.hip DACT variant):
+  // y = conv_transpose(x, w) * act'(ya), db[N] = column sums of y (per-workgroup partials + a
+  // sliced fixed-order sum) -- replaces narrow_deconv + act_bwd_dbias.
+  int narrow_deconv_dact(std::string name, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t ya, int B, int Hi, int Wi,
+                         int C, int Ho, int Wo, int N, int pad, int act, float leak, uintptr_t db, int stream) {
+    if (dt_ == 2) throw std::runtime_error("narrow_deconv_dact: 16-bit builds only");
+    const int tiles = KF(dcg_narrow_deconv_tiles)(B, Ho, Wo);
+    float* part = reinterpret_cast<float*>(dev_alloc((size_t)tiles * N * sizeof(float)));
+    const size_t out = (size_t)B * Ho * Wo * N * es_;
+    add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_narrow_deconv_dact)(P<const elem_t>(x), P<const elem_t>(w), P<elem_t>(y), P<const elem_t>(ya), B,
+                                        Hi, Wi, C, Ho, Wo, N, pad, act, leak, part, s);
+    }, AccList().r(x, (size_t)B * Hi * Wi * C * es_).r(w, (size_t)25 * N * C * es_).r(ya, out).w(y, out)
+           .w((uintptr_t)part, (size_t)tiles * N * 4).v);
+    return sum_partials(name + ".dbias", (uintptr_t)part, tiles, N, N, db, stream);
+  }
   bool nwgrad_ok(int H, int W, int Hd, int Wd) const {
     int t, r, c;
     return dt_ != 2 && KF(dcg_nwgrad_plan)(H, W, Hd, Wd, &t, &r, &c) == 0;
@@ -1020,6 +1036,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("conv3_direct", &Program::conv3_direct)
       .def("nconv", &Program::nconv)
       .def("nconv_tiles", &Program::nconv_tiles)
+      .def("narrow_deconv_dact", &Program::narrow_deconv_dact)
       .def("nwgrad_ok", &Program::nwgrad_ok)
       .def("nwgrad", &Program::nwgrad)
       .def("pack", &Program::pack)

@@ -923,7 +923,10 @@ extern "C" int DCG_API(dcg_adam2)(float* wA, elem_t* wbfA, const float* gA, floa
 
 extern "C" int DCG_API(dcg_splitk_reduce)(const float* src, int splits, size_t n, float* dst, float scale, hipStream_t s) {
   const size_t n4 = n / 4;
-  if (splits >= 64) {
+  if (splits >= 256) {  // many slabs of a small result (narrow2 nwgrad partials): 64 lanes per column
+    hipLaunchKernelGGL(dcg::splitk_reduce_kernel<64>, dim3((unsigned)((n4 + 3) / 4 + 1)), dim3(256), 0, s, src,
+                       splits, n, dst, scale);
+  } else if (splits >= 64) {
     hipLaunchKernelGGL(dcg::splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16 + 1)), dim3(256), 0, s, src,
                        splits, n, dst, scale);
   } else if (splits >= 8) {

@@ -118,13 +118,17 @@ __global__ __launch_bounds__(256) void narrow_deconv_kernel(const elem_t* __rest
 // channels x 16 outputs of the tap's weights (outputs >= N are zero lanes). N=3 pads to 16
 // (5.3x the useful MACs), but one MFMA replaces 64 lanes x 32 MACs of v_dot2 work at 4x the
 // per-SIMD rate of the VALU kernel above (measured: see BASELINE.md / profiles).
-template <int N, int C8, bool WG>  // WG: B fragments straight from global/L1 (no LDS weight copy)
+// DACT: the output is multiplied by act'(ya) (ya = the activation output at the same pixel: the
+// tanh backward of G's RGB layer fused into the image-gradient kernel) and every workgroup writes
+// its per-channel partial sum of the stored values (the bias gradient) to part[blockIdx][N].
+template <int N, int C8, bool WG, bool DACT = false>  // WG: B fragments straight from global/L1
 __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* __restrict__ x,
                                                                  const elem_t* __restrict__ w,
                                                                  const float* __restrict__ bias,
                                                                  elem_t* __restrict__ y, int Hi, int Wi, int Ho,
                                                                  int Wo, int pad, int act, float leak, int tiles_x,
-                                                                 int tiles_per_img) {
+                                                                 int tiles_per_img, const elem_t* __restrict__ ya,
+                                                                 float* __restrict__ part) {
   static_assert(C8 == 8, "the bank swizzle below assumes 8 chunks (64 channels) per pixel");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   elem8* xs = reinterpret_cast<elem8*>(smem);  // [HALO*HALO][C8], chunk c of pixel (row, col) at c ^ sw(col)
@@ -196,7 +200,26 @@ __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* _
   }
   __syncthreads();
   const int oy = ty0 + 2 * (lane >> 3) + py, ox = tx0 + 2 * (lane & 7) + px;
-  if (oy < Ho && ox < Wo) {
+  if constexpr (DACT) {
+    float ps[N];
+    const bool ok = oy < Ho && ox < Wo;
+    const size_t o = (((size_t)b * Ho + (ok ? oy : 0)) * Wo + (ok ? ox : 0)) * N;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const float v = ob[lane * N + n] + (bias ? bias[n] : 0.f);
+      const elem_t r = f2bf(v * act_grad_from_out((float)ya[o + n], act, leak));
+      if (ok) y[o + n] = r;
+      ps[n] = wave_sum(ok ? (float)r : 0.f);
+    }
+    __syncthreads();  // every wave has read its ob rows: reuse the LDS for the wave partials
+    float* wsum = reinterpret_cast<float*>(smem);
+    if (lane == 0) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) wsum[wave * N + n] = ps[n];
+    }
+    __syncthreads();
+    if (tid < N) part[(size_t)blockIdx.x * N + tid] = ((wsum[tid] + wsum[N + tid]) + wsum[2 * N + tid]) + wsum[3 * N + tid];
+  } else if (oy < Ho && ox < Wo) {
     elem_t* dst = y + (((size_t)b * Ho + oy) * Wo + ox) * N;
 #pragma unroll
     for (int n = 0; n < N; ++n) dst[n] = f2bf(apply_act(ob[lane * N + n] + (bias ? bias[n] : 0.f), act, leak));
@@ -228,7 +251,7 @@ extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, cons
       attr = true;                                                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL(k, grid, dim3(256), shm_m, s, x, w, bias, y, Hi, Wi, Ho, Wo, pad, act, leak, tiles_x,   \
-                       tiles_x * tiles_y);                                                                     \
+                       tiles_x * tiles_y, (const elem_t*)nullptr, (float*)nullptr);                            \
   }
     switch (N) {
       case 1: NW_MFMA(1) break;
@@ -259,4 +282,39 @@ extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, cons
   }
 #undef NW_LAUNCH
   return (int)hipGetLastError();
+}
+
+// image gradient of G's RGB layer with its activation backward fused (narrow_deconv_mfma_kernel
+// DACT): y = conv_transpose(x, w) * act'(ya); part[tiles][N] = per-workgroup column sums of y
+extern "C" int DCG_API(dcg_narrow_deconv_dact)(const elem_t* x, const elem_t* w, elem_t* y, const elem_t* ya, int B,
+                                               int Hi, int Wi, int C, int Ho, int Wo, int N, int pad, int act,
+                                               float leak, float* part, hipStream_t s) {
+  if (pad < 0 || pad > 2 || C != 64 || N < 1 || N > 4 || !ya || !part) return -2;
+  const int tiles_x = (Wo + dcg::NW_TILE - 1) / dcg::NW_TILE, tiles_y = (Ho + dcg::NW_TILE - 1) / dcg::NW_TILE;
+  const size_t shm = (size_t)dcg::NW_HALO * dcg::NW_HALO * C * sizeof(elem_t);
+  dim3 grid(B * tiles_x * tiles_y);
+#define NWD(NN)                                                                                                \
+  {                                                                                                            \
+    auto k = dcg::narrow_deconv_mfma_kernel<NN, 8, true, true>;                                                \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return (int)e;                                                                      \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm, s, x, w, (const float*)nullptr, y, Hi, Wi, Ho, Wo, pad, act, leak, \
+                       tiles_x, tiles_x * tiles_y, ya, part);                                                  \
+  }
+  switch (N) {
+    case 1: NWD(1) break;
+    case 2: NWD(2) break;
+    case 3: NWD(3) break;
+    default: NWD(4) break;
+  }
+#undef NWD
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_narrow_deconv_tiles)(int B, int Ho, int Wo) {
+  return B * ((Wo + dcg::NW_TILE - 1) / dcg::NW_TILE) * ((Ho + dcg::NW_TILE - 1) / dcg::NW_TILE);
 }

@@ -39,6 +39,9 @@ extern "C" int DCG_API(dcg_nconv_tiles)(int, int, int) { return -1; }
 extern "C" int DCG_API(dcg_nwgrad_plan)(int, int, int, int, int*, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_nwgrad)(const elem_t*, int, int, int, int, const elem_t*, int, int, int, int, float*,
                                    hipStream_t) { return -2; }
+extern "C" int DCG_API(dcg_narrow_deconv_dact)(const elem_t*, const elem_t*, elem_t*, const elem_t*, int, int, int, int,
+                                               int, int, int, int, int, float, float*, hipStream_t) { return -2; }
+extern "C" int DCG_API(dcg_narrow_deconv_tiles)(int, int, int) { return -1; }
 #else
 
 namespace dcg {

@@ -456,6 +456,12 @@ class HipEngine:
                 return rpb
         return 1
 
+    def _img_dact(self) -> bool:
+        """D layer 0's image gradient (g_loss chain) with G's tanh backward + bias gradient fused
+        (narrow.hip DACT): 16-bit, 64-channel D layer 0, <= 4 image channels."""
+        L = self.dl[0]
+        return not self.f32 and L.cin <= 4 and L.cout == 64 and self.gl[-1].cout == L.cin
+
     def _g_out_direct(self) -> bool:
         """G's 1..4-channel output layer backward on narrow2.hip (nconv data gradient + nwgrad)."""
         L = self.gl[-1]
@@ -744,7 +750,14 @@ class HipEngine:
                 self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, out, B, L.out_hw,
                             L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, **kw)
             else:
-                if not self.f32 and L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
+                if self._img_dact():
+                    # image gradient with G's tanh backward fused (dL/d(G pre-activation) straight out)
+                    # + the G output bias gradient from its per-workgroup column sums
+                    Lg = self.gl[-1]
+                    prog.narrow_deconv_dact("g." + L.name + ".dgrad_img+tanh_bwd", _p(dx), _p(nat), _p(self.img_g),
+                                            _p(self.fake), B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin,
+                                            pad, TANH, 0.0, _p(self.grad_g[Lg.name + "/biases"]), 0)
+                elif not self.f32 and L.cin <= 4 and L.cout % 8 == 0 and L.cout <= 256:  # 3-channel image gradient
                     prog.narrow_deconv("g." + L.name + ".dgrad_img", _p(dx), _p(nat), 0, _p(self.img_grad), B,
                                        L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, NONE, 0.0, 0)
                 else:
@@ -753,8 +766,9 @@ class HipEngine:
         # ---------------- G backward (reads no D state)
         n = len(self.gl)
         Lg = self.gl[-1]
-        self._act_bwd_dbias(prog, "g_out.tanh_bwd", self.img_grad, self.fake, self.img_g, B * Lg.out_hw ** 2,
-                            Lg.cout, TANH, gG[Lg.name + "/biases"], "g")
+        if not self._img_dact():  # (else fused into the image-gradient kernel above)
+            self._act_bwd_dbias(prog, "g_out.tanh_bwd", self.img_grad, self.fake, self.img_g, B * Lg.out_hw ** 2,
+                                Lg.cout, TANH, gG[Lg.name + "/biases"], "g")
         a_prev = self.g_a[self.gl[-2].name] if n > 1 else self.g_h0
         da_prev = self.g_da[self.gl[-2].name] if n > 1 else self.g_da0
         x_prev = self.g_x[self.gl[-2].name] if n > 1 else self.g_h0_pre

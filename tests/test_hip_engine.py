@@ -100,15 +100,21 @@ def test_engine_stagewise(size, c_dim, B, dtype):
             rep["g %s bn dx" % L.name] = rel(eng.gc_dx[L.name], gx)
         src = eng.d_in[B:] if i == 0 else eng.d_a[dl[i - 1].name][B:]
         gx, _ = conv_grads64(src, Pd[L.name + "/w"], eng.gc_dx[L.name], "conv", edt=edt)
-        if i == 0:
+        if i == 0 and eng._img_dact():  # G's tanh backward fused into the image-gradient kernel
+            fk = d64(eng.fake)
+            rep["g %s dgrad+tanh bwd" % L.name] = rel(eng.img_g, gx * (1 - fk * fk))
+        elif i == 0:
             rep["g %s dgrad" % L.name] = rel(eng.img_grad, gx)
         elif dl[i - 1].bn:
             rep["g %s dgrad" % L.name] = rel(eng.gc_da[dl[i - 1].name], gx)
         else:  # the act backward of a BN-less layer is fused into this GEMM: it stores dx
             rep["g %s dgrad+act" % L.name] = rel(eng.gc_dx[dl[i - 1].name], gx * _lrelu_d(eng.d_a[dl[i - 1].name][B:]))
     fake = d64(eng.fake)
-    img_g = d64(eng.img_grad) * (1 - fake * fake)
-    rep["G tanh bwd"] = rel(eng.img_g, img_g)
+    if eng._img_dact():
+        img_g = d64(eng.img_g)  # checked above against the oracle; the bias gradient sums it
+    else:
+        img_g = d64(eng.img_grad) * (1 - fake * fake)
+        rep["G tanh bwd"] = rel(eng.img_g, img_g)
     for j in range(len(gl) - 1, -1, -1):
         L = gl[j]
         src = eng.g_a[gl[j - 1].name] if j > 0 else eng.g_h0

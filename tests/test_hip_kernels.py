@@ -597,6 +597,27 @@ def test_conv3_direct(B, Hh, C, dtype):
     close(y, ref, 1e-2, "conv3 direct")
 
 
+@pytest.mark.parametrize("B,Hi,Ho,N", [(4, 32, 64, 3), (3, 14, 28, 1), (2, 9, 17, 4)])
+def test_narrow_deconv_dact(B, Hi, Ho, N):
+    """The image gradient with G's tanh backward fused: y = conv_transpose(x, w) * (1 - ya^2)
+    and the bias gradient sum(y) over every pixel (per-workgroup partials + sliced sum)."""
+    h = H()
+    x = bf(rnd(B, Hi, Hi, 64, seed=64))
+    w = bf(rnd(5, 5, N, 64, scale=0.05, seed=65))
+    ya = bf(torch.tanh(rnd(B, Ho, Ho, N, scale=2.0, seed=66)))
+    y = torch.empty(B, Ho, Ho, N, device=dev, dtype=torch.bfloat16)
+    db = torch.empty(N, device=dev)
+    prog = h.ext().Program()
+    pad = max((Hi - 1) * 2 + 5 - Ho, 0) // 2
+    prog.narrow_deconv_dact("nd", h._p(x), h._p(w), h._p(y), h._p(ya), B, Hi, Hi, 64, Ho, Ho, N, pad, 3, 0.0,
+                            h._p(db), 0)
+    h.run(prog)
+    torch.cuda.synchronize()
+    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho)) * (1 - ya.float() ** 2)
+    close(y, ref, 1e-2, "narrow deconv dact")
+    close(db, y.float().reshape(-1, N).sum(0), 1e-4, "dbias of the stored values")
+
+
 @pytest.mark.parametrize("B,Hh,C,dtype", [(4, 64, 3, "bf16"), (2, 28, 1, "bf16"), (3, 33, 4, "bf16"),
                                           (2, 64, 3, "fp16"), (1, 7, 3, "bf16"), (2, 128, 3, "bf16"),
                                           (80, 64, 3, "bf16")])
