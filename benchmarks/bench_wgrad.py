@@ -68,11 +68,14 @@ def main():
             p.wgrad(name, 0, G.data_ptr(), Hg, Wg, Mc, Dm.data_ptr(), Bn, Hd, Wd, Nc, pad, c0, sw, slabs.data_ptr(),
                     outs[(0, sw)].data_ptr(), 25 * Mc * Nc, 1.0, 0)
             progs[(0, sw)] = p
-        for c3 in (300, 301, 302, 303, 310, 311, 312, 313):
+        for c3 in (300, 301, 302, 303, 310, 311, 312, 313, 320, 322, 330, 332):
             bm, bn = H.WGRAD3_TILES[c3 % 10]
-            if bm > max(Mc, 64) or bn > max(Nc, 64):
+            if c3 >= 320:  # two taps per tile: BM = 2 Mc
+                if 2 * Mc != bm or bn > max(Nc, 64):
+                    continue
+            elif bm > max(Mc, 64) or bn > max(Nc, 64):
                 continue
-            for sp in (1, 2, 4, 8, 16):
+            for sp in (1, 2, 4, 8, 16, 24, 32):
                 if sp > 1 and kt // sp < 4:
                     continue
                 o = torch.empty(25, Mc, Nc, device=dev)

@@ -489,7 +489,9 @@ class Program {
     a.out = P<float>(dst); a.scale = scale;
     AccList acc;
     acc.r(G, g_elems * es_).r(Dm, d_elems * es_).w(dst, (size_t)25 * Mc * Nc * 4);
-    const size_t tiles = (size_t)((Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * 25;
+    const int tt = KF(dcg_wgrad3_taps_per_tile)(cfg);
+    if (tt == 2 && 2 * Mc != bm) throw std::runtime_error("wgrad3: two-tap tiles need BM = 2 Mc");
+    const size_t tiles = (size_t)(tt == 2 ? 1 : (Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * ((25 + tt - 1) / tt);
     if (splits > 1) {
       if ((size_t)splits * bm * bn * 4 >= OOB) throw std::runtime_error("wgrad3: split slabs too large");
       a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * (size_t)bm * bn * sizeof(float)));

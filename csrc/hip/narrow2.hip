@@ -42,6 +42,7 @@ extern "C" int DCG_API(dcg_nwgrad)(const elem_t*, int, int, int, int, const elem
 extern "C" int DCG_API(dcg_narrow_deconv_dact)(const elem_t*, const elem_t*, elem_t*, const elem_t*, int, int, int, int,
                                                int, int, int, int, int, float, float*, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_narrow_deconv_tiles)(int, int, int) { return -1; }
+extern "C" int DCG_API(dcg_wgrad3_taps_per_tile)(int) { return 1; }
 #else
 
 namespace dcg {

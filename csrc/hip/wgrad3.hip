@@ -34,7 +34,10 @@ __device__ __forceinline__ void w3_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int P2>
+// TT taps per tile (1 or 2): with TT = 2 the tile's BM rows are [tap 2 tg: Mc channels][tap 2 tg + 1:
+// Mc channels] (BM = 2 Mc): both taps share the B (Dm) tile -- half the DMA per MFMA of the 64-row
+// single-tap tile for the 64-channel layers (tap 25 of group 12 reads zeros and is not stored).
+template <int BM, int BN, int WM, int WN, int NS, int P2, int TT>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -57,22 +60,23 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
 
   // ---- tile decode: XCD remap (each XCD gets a contiguous run of t), then tap fastest
   const int S = p.splits;
-  const int ntm = (p.Mc + BM - 1) / BM, ntn = (p.Nc + BN - 1) / BN;
-  const int total = ntm * ntn * 25 * S;
+  constexpr int NTG = (25 + TT - 1) / TT;             // tap groups
+  const int ntm = TT == 1 ? (p.Mc + BM - 1) / BM : 1, ntn = (p.Nc + BN - 1) / BN;
+  const int total = ntm * ntn * NTG * S;
   int t = blockIdx.x;
   {
     const int q = total >> 3, rr = total & 7, xcd = t & 7;
     t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
   }
-  const int tap = t % 25;
-  int r_ = t / 25;
+  const int tap = t % NTG;  // TT = 2: the tap group
+  int r_ = t / NTG;
   const int nt = r_ % ntn;
   r_ /= ntn;
   const int mt = r_ % ntm;
   const int split = r_ / ntm;
   const int tile_id = (tap * ntm + mt) * ntn + nt;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+  constexpr int MCT = BM / TT;  // channels per tap in the tile (TT = 2: = Mc)
 
   const int KT = (p.K + BK - 1) / BK;
   const int kt0 = split * p.kt_per_split;
@@ -82,12 +86,18 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
   const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.Dm, p.d_bytes);
 
   // per-lane fixed parts of the DMA addresses: row within the tile and the swizzled chunk
-  int a_row[PPW_A], a_m[PPW_A], b_row[PPW_B], b_n[PPW_B];
+  int a_row[PPW_A], a_m[PPW_A], a_ky[PPW_A], a_kx[PPW_A], b_row[PPW_B], b_n[PPW_B];
+  bool a_tok[PPW_A];
 #pragma unroll
   for (int i = 0; i < PPW_A; ++i) {
     const int rr = (wave + 4 * i) * RPA + lane / CA;
     a_row[i] = rr;
-    a_m[i] = m0 + ((lane % CA) ^ (w3_swz<SA>(rr) >> 1)) * 8;
+    const int ml = ((lane % CA) ^ (w3_swz<SA>(rr) >> 1)) * 8;  // row of the tile this lane's chunk feeds
+    const int tp = TT == 1 ? tap : TT * tap + ml / MCT;          // its tap
+    a_m[i] = TT == 1 ? m0 + ml : ml % MCT;                       // its channel
+    a_tok[i] = tp < 25;
+    a_ky[i] = tp / 5;
+    a_kx[i] = tp - 5 * (tp / 5);
   }
 #pragma unroll
   for (int i = 0; i < PPW_B; ++i) {
@@ -115,8 +125,9 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
         y = fdiv(rem, p.fd_w);
         x = rem - y * (uint32_t)p.Wd;
       }
-      const int iy = 2 * (int)y + ky - p.pl, ix = 2 * (int)x + kx - p.pl;
-      const bool ok = k < p.K && a_m[i] < p.Mc && (unsigned)iy < (unsigned)p.Hg && (unsigned)ix < (unsigned)p.Wg;
+      const int iy = 2 * (int)y + a_ky[i] - p.pl, ix = 2 * (int)x + a_kx[i] - p.pl;
+      const bool ok = k < p.K && a_tok[i] && a_m[i] < p.Mc && (unsigned)iy < (unsigned)p.Hg &&
+                      (unsigned)ix < (unsigned)p.Wg;
       dma16_asm_la(rg, sa + (wave + 4 * i) * 1024,
                    oob_unless(ok, (uint32_t)((((int)b * p.Hg + iy) * p.Wg + ix) * p.Mc + a_m[i]) * 2u));
     }
@@ -237,7 +248,6 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
   }
 
   // ---- scaled store into the fp32 gradient (TF layout [tap][Mc][Nc])
-  float* out = p.out + (size_t)tap * p.Mc * p.Nc;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -245,31 +255,34 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
       const int n = n0 + wn * TN + j * 16 + li;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * TM + i * 16 + g4 * 4 + r;
-        if (m < p.Mc && n < p.Nc) out[(size_t)m * p.Nc + n] = acc[i][j][r] * p.scale;
+        const int ml = wm * TM + i * 16 + g4 * 4 + r;
+        const int tp = TT == 1 ? tap : TT * tap + ml / MCT;
+        const int m = TT == 1 ? m0 + ml : ml % MCT;
+        if (tp < 25 && m < p.Mc && n < p.Nc) p.out[((size_t)tp * p.Mc + m) * p.Nc + n] = acc[i][j][r] * p.scale;
       }
     }
 }
 
 }  // namespace dcg
 
-// cfg = 300 + 10 * (3 - NS) + id   (NS = 3 -> 300..303, NS = 2 -> 310..313)
+// cfg = 300 + 10 * (3 - NS) + id   (NS = 3 -> 300..303, NS = 2 -> 310..313); two taps per tile
+// (TT = 2, BM = 2 Mc): 320..323 with NS = 2, 330..333 with NS = 3
 #define DCG_WGRAD3_TILES(X) X(0, 128, 128, 2, 2) X(1, 64, 128, 2, 2) X(2, 128, 64, 2, 2) X(3, 64, 64, 2, 2)
 
 extern "C" int DCG_API(dcg_wgrad3_tile)(int cfg, int* bm, int* bn, int* ns) {
-  if (cfg < 300 || cfg >= 320 || cfg % 10 > 3) return -1;
+  if (cfg < 300 || cfg >= 340 || cfg % 10 > 3) return -1;
   const int id = cfg % 10;
-  *ns = cfg < 310 ? 3 : 2;
+  *ns = (cfg < 310 || cfg >= 330) ? 3 : 2;
 #define X(id_, BM_, BN_, WM_, WN_) if (id == id_) { *bm = BM_; *bn = BN_; return 0; }
   DCG_WGRAD3_TILES(X)
 #undef X
   return -1;
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int P2>
+template <int BM, int BN, int WM, int WN, int NS, int P2, int TT>
 static int wlaunch3p(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
   constexpr size_t shm = (size_t)NS * (BM + BN) * 64 * 2;
-  auto k = dcg::wgrad3_kernel<BM, BN, WM, WN, NS, P2>;
+  auto k = dcg::wgrad3_kernel<BM, BN, WM, WN, NS, P2, TT>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
@@ -280,19 +293,29 @@ static int wlaunch3p(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int TT>
 static int wlaunch3(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
-  return a->lhw >= 0 ? wlaunch3p<BM, BN, WM, WN, NS, 1>(a, blocks, s) : wlaunch3p<BM, BN, WM, WN, NS, 0>(a, blocks, s);
+  return a->lhw >= 0 ? wlaunch3p<BM, BN, WM, WN, NS, 1, TT>(a, blocks, s)
+                     : wlaunch3p<BM, BN, WM, WN, NS, 0, TT>(a, blocks, s);
 }
+
+extern "C" int DCG_API(dcg_wgrad3_taps_per_tile)(int cfg) { return cfg >= 320 ? 2 : 1; }
 
 extern "C" int DCG_API(dcg_wgrad3_launch)(const dcg::WGrad3Args* a, int cfg, hipStream_t s) {
   int bm, bn, ns;
   if (DCG_API(dcg_wgrad3_tile)(cfg, &bm, &bn, &ns)) return -1;
-  const unsigned blocks = (unsigned)(((a->Mc + bm - 1) / bm) * ((a->Nc + bn - 1) / bn) * 25 * a->splits);
+  const int tt = DCG_API(dcg_wgrad3_taps_per_tile)(cfg);
+  if (tt == 2 && 2 * a->Mc != bm) return -2;  // two-tap tiles hold exactly two taps of every channel
+  const unsigned mt = tt == 2 ? 1u : (unsigned)((a->Mc + bm - 1) / bm);
+  const unsigned blocks = mt * (unsigned)((a->Nc + bn - 1) / bn) * (unsigned)((25 + tt - 1) / tt) * a->splits;
   const int id = cfg % 10;
-#define X(id_, BM_, BN_, WM_, WN_)                                              \
-  if (id == id_) return ns == 3 ? wlaunch3<BM_, BN_, WM_, WN_, 3>(a, blocks, s) \
-                                : wlaunch3<BM_, BN_, WM_, WN_, 2>(a, blocks, s);
+#define X(id_, BM_, BN_, WM_, WN_)                                                               \
+  if (id == id_) {                                                                               \
+    if (tt == 2) return ns == 3 ? wlaunch3<BM_, BN_, WM_, WN_, 3, 2>(a, blocks, s)               \
+                                : wlaunch3<BM_, BN_, WM_, WN_, 2, 2>(a, blocks, s);              \
+    return ns == 3 ? wlaunch3<BM_, BN_, WM_, WN_, 3, 1>(a, blocks, s)                            \
+                   : wlaunch3<BM_, BN_, WM_, WN_, 2, 1>(a, blocks, s);                           \
+  }
   DCG_WGRAD3_TILES(X)
 #undef X
   return -1;

@@ -666,14 +666,14 @@ class HipEngine:
             prog.colsum_small(name, _p(x), rows, C, _p(sp), blocks, 0)
             prog.sum_partials(name + ".sum", _p(sp), blocks, C, C, _p(dst), 0)
 
-    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst):
+    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst, stream=0):
         K = Bn * Hd * Wd
         taps = 1 if mode == 2 else 25
         if mode == 0 and not self.f32:  # 25-tap layers: LDS-DMA pipelined kernel, split-K reduced in-kernel
             plan = H.wgrad3_cfg_for(Mc, Nc, Bn, Hd, Wd, Hg)
             if plan is not None:
                 prog.wgrad3(name + ".wgrad", _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, plan[0], plan[1],
-                            _p(dst), 1.0, 0)
+                            _p(dst), 1.0, stream)
                 return
         cfg, splits = H.pick_wgrad(Mc, Nc, K, taps, dtype=self.dt)
         if mode == 0 and not self.f32:
@@ -681,7 +681,7 @@ class HipEngine:
         slabs = self._t(splits, taps, Mc, Nc, dtype=torch.float32)
         self._keep.append(slabs)
         prog.wgrad(name + ".wgrad", mode, _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, cfg, splits, _p(slabs),
-                   _p(dst), dst.numel(), 1.0, 0)
+                   _p(dst), dst.numel(), 1.0, stream)
 
     def _bn_bwd(self, prog, name, x, dy, y, dx, rows, C, groups, act, P, grads, coef, write_param_grads,
                 row_offset_groups=None, fused=None):
@@ -840,6 +840,7 @@ class HipEngine:
                      self.coef["g_bn0"], write_param_grads=True, fused=fused_next)
         prog.linear_wgrad("g_h0_lin.wgrad", _p(self.z), _p(self.g_dx0), _p(gG["g_h0_lin/Matrix"]),
                           _p(gG["g_h0_lin/bias"]), B, cfg.z_dim, cfg.g_lin_out, 0)
+
 
     # ---- optimiser (+ 16-bit weight mirrors)
     def _build_update(self, prog, first: bool):
