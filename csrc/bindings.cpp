@@ -710,6 +710,29 @@ class Program {
                                s);
     }, acc.v);
   }
+  // the head with the top BN layer's apply + activation fused: x = that layer's pre-BN input,
+  // y = its activation (written here), scale / shift [groups][C] from its BN finalize
+  int gemv_head_bn(std::string name, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int R, int K, int stream,
+                   uintptr_t loss_out, uintptr_t dl_d, uintptr_t dl_g, uintptr_t prob, uintptr_t ls, uintptr_t scale,
+                   uintptr_t shift, int C, int rpg, int act, float leak, uintptr_t y) {
+    if (dt_ == 2) throw std::runtime_error("gemv_head_bn: 16-bit builds only");
+    unsigned* ctr = nullptr;
+    AccList acc;
+    const size_t groups = (size_t)((R + rpg - 1) / rpg);
+    acc.r(x, (size_t)R * K * es_).r(w, (size_t)K * 4).r(b, 4).w(out, (size_t)R * 4).r(scale, groups * C * 4)
+        .r(shift, groups * C * 4).w(y, (size_t)R * K * es_);
+    if (loss_out) {
+      ctr = reinterpret_cast<unsigned*>(dev_alloc(sizeof(unsigned), nullptr, true));
+      acc.w((uintptr_t)ctr, 4).w(loss_out, 16).w(dl_d, (size_t)R * 4).w(dl_g, (size_t)R * 2).w(prob, (size_t)R * 4)
+          .r(ls, 12);
+    }
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_gemv_head_bn)(P<const elem_t>(x), P<const float>(w), P<const float>(b), P<float>(out), R, K, ctr,
+                                  P<float>(loss_out), P<float>(dl_d), P<float>(dl_g), P<float>(prob),
+                                  P<const float>(ls), P<const float>(scale), P<const float>(shift), C, rpg, act, leak,
+                                  P<elem_t>(y), s);
+    }, acc.v);
+  }
   int head_dgrad(std::string name, uintptr_t dl, uintptr_t w, uintptr_t dx, int R, int K, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_head_dgrad)(P<const float>(dl), P<const float>(w), P<elem_t>(dx), R, K, s);
@@ -784,6 +807,20 @@ class Program {
     }, acc.v);
   }
   int nconv_tiles(int B, int Ho, int Wo) const { return KF(dcg_nconv_tiles)(B, Ho, Wo); }
+  // G's RGB layer forward with the BN apply + activation of the layer below fused into its halo
+  // staging: x = that layer's pre-BN output, a_out = its activation (written by the owning tiles)
+  int narrow_deconv_bnin(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int Hi,
+                         int Wi, int C, int Ho, int Wo, int N, int pad, int act, float leak, uintptr_t scale,
+                         uintptr_t shift, int bn_act, float bn_leak, uintptr_t a_out, int stream) {
+    if (dt_ == 2) throw std::runtime_error("narrow_deconv_bnin: 16-bit builds only");
+    const size_t in = (size_t)B * Hi * Wi * C * es_;
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_narrow_deconv_bnin)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B,
+                                        Hi, Wi, C, Ho, Wo, N, pad, act, leak, P<const float>(scale),
+                                        P<const float>(shift), bn_act, bn_leak, P<elem_t>(a_out), s);
+    }, AccList().r(x, in).r(w, (size_t)25 * N * C * es_).r(bias, (size_t)N * 4).r(scale, (size_t)C * 4)
+           .r(shift, (size_t)C * 4).w(a_out, in).w(y, (size_t)B * Ho * Wo * N * es_).v);
+  }
   // G's RGB-layer image gradient with its activation backward fused (narrow.hip DACT variant):
   // y = conv_transpose(x, w) * act'(ya), db[N] = column sums of y (per-workgroup partials + a
   // sliced fixed-order sum) -- replaces narrow_deconv + act_bwd_dbias.
@@ -1039,6 +1076,8 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("nconv", &Program::nconv)
       .def("nconv_tiles", &Program::nconv_tiles)
       .def("narrow_deconv_dact", &Program::narrow_deconv_dact)
+      .def("gemv_head_bn", &Program::gemv_head_bn)
+      .def("narrow_deconv_bnin", &Program::narrow_deconv_bnin)
       .def("nwgrad_ok", &Program::nwgrad_ok)
       .def("nwgrad", &Program::nwgrad)
       .def("pack", &Program::pack)

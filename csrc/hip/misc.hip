@@ -227,9 +227,18 @@ struct HeadLossArgs {  // fused gan loss (counter == nullptr: plain GEMV)
   const float* ls;
 };
 
+// BNA (optional): x is the top BN layer's PRE-BN input; the head applies that BN + activation on
+// the fly (y = act(x * scale[g][c] + shift[g][c]), c = k % C, g = row / rpg), writes y (the layer's
+// activation, which the backward reads) and dots the stored (rounded) y -- the layer's separate
+// BN-apply launch folded into the head.
+struct HeadBnArgs {
+  const float* scale; const float* shift; int C, rpg, act; float leak; elem_t* y;
+};
+
+template <bool BNA>
 __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ b, float* __restrict__ out, int R,
-                                                        int K, HeadLossArgs L) {
+                                                        int K, HeadLossArgs L, HeadBnArgs bn) {
   // one workgroup per row, each of the 4 waves a quarter of K with all its loads issued up
   // front (one wave per row walked K serially: latency-bound, 9 us for 256 x 8192)
   __shared__ float part[4];
@@ -237,6 +246,16 @@ __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict
   const int kq = K / 4;  // K % 32 == 0 (launcher): 16-byte chunks per quarter
   const elem_t* xr = x + (size_t)row * K + wave * kq;
   const float* wr = w + wave * kq;
+  const int grp = BNA ? row / bn.rpg : 0;
+  float bsc[BNA ? 8 : 1], bsh[BNA ? 8 : 1];  // BNA: channel (k % C) = lane * 8 % C for every chunk (512 % C == 0)
+  if constexpr (BNA) {
+    const int c = (lane * 8) % bn.C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = bn.scale[grp * bn.C + c + e];
+      bsh[e] = bn.shift[grp * bn.C + c + e];
+    }
+  }
   float s = 0.f;
   for (int k0 = lane * 8; k0 < kq; k0 += 4 * 512) {
     elem8 xv[4];
@@ -251,7 +270,12 @@ __global__ __launch_bounds__(256) void gemv_head_kernel(const elem_t* __restrict
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (k0 + u * 512 >= kq) break;
-      const elem8 xb = xv[u];
+      elem8 xb = xv[u];
+      if constexpr (BNA) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xb[e] = (elem_t)apply_act((float)xb[e] * bsc[e] + bsh[e], bn.act, bn.leak);
+        st8(bn.y + (size_t)row * K + wave * kq + k0 + u * 512, xb);
+      }
       s += (float)xb[0] * w0[u][0] + (float)xb[1] * w0[u][1] + (float)xb[2] * w0[u][2] + (float)xb[3] * w0[u][3] +
            (float)xb[4] * w1[u][0] + (float)xb[5] * w1[u][1] + (float)xb[6] * w1[u][2] + (float)xb[7] * w1[u][3];
     }
@@ -792,7 +816,20 @@ extern "C" int DCG_API(dcg_gemv_head)(const elem_t* x, const float* w, const flo
                                       const float* ls, hipStream_t s) {
   if (K % 32 || (counter && (R % 2 || !loss_out || !dl_d || !dl_g))) return -2;
   const dcg::HeadLossArgs L{counter, loss_out, dl_d, dl_g, prob, ls};
-  hipLaunchKernelGGL(gemv_head_kernel, dim3(R), dim3(256), 0, s, x, w, b, out, R, K, L);
+  hipLaunchKernelGGL(gemv_head_kernel<false>, dim3(R), dim3(256), 0, s, x, w, b, out, R, K, L, dcg::HeadBnArgs{});
+  return (int)hipGetLastError();
+}
+
+// the head with the top BN layer's apply + activation fused (x = pre-BN input, y = activation out)
+extern "C" int DCG_API(dcg_gemv_head_bn)(const elem_t* x, const float* w, const float* b, float* out, int R, int K,
+                                         unsigned* counter, float* loss_out, float* dl_d, float* dl_g, float* prob,
+                                         const float* ls, const float* scale, const float* shift, int C, int rpg,
+                                         int act, float leak, elem_t* y, hipStream_t s) {
+  if (K % 2048 || C % 8 || 512 % C || (counter && (R % 2 || !loss_out || !dl_d || !dl_g)) || !scale || !shift || !y)
+    return -2;  // (every 8-element chunk of a lane then holds channels lane * 8 % C ..: loaded once)
+  const dcg::HeadLossArgs L{counter, loss_out, dl_d, dl_g, prob, ls};
+  const dcg::HeadBnArgs bn{scale, shift, C, rpg, act, leak, y};
+  hipLaunchKernelGGL(gemv_head_kernel<true>, dim3(R), dim3(256), 0, s, x, w, b, out, R, K, L, bn);
   return (int)hipGetLastError();
 }
 

@@ -121,14 +121,22 @@ __global__ __launch_bounds__(256) void narrow_deconv_kernel(const elem_t* __rest
 // DACT: the output is multiplied by act'(ya) (ya = the activation output at the same pixel: the
 // tanh backward of G's RGB layer fused into the image-gradient kernel) and every workgroup writes
 // its per-channel partial sum of the stored values (the bias gradient) to part[blockIdx][N].
-template <int N, int C8, bool WG, bool DACT = false>  // WG: B fragments straight from global/L1
+// BNIN: x is the PRE-BN input of the layer below; the halo staging applies that BN + activation
+// (scale / shift [C], one group) and the workgroup writes the activation of the 8x8 input pixels
+// it owns (the ones under its 16x16 output tile) to a_out -- the layer's separate BN-apply launch
+// folded into this one (the backward reads a_out).
+struct NarrowBnIn {
+  const float* scale; const float* shift; int act; float leak; elem_t* a_out;
+};
+
+template <int N, int C8, bool WG, bool DACT = false, bool BNIN = false>  // WG: B fragments from global/L1
 __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* __restrict__ x,
                                                                  const elem_t* __restrict__ w,
                                                                  const float* __restrict__ bias,
                                                                  elem_t* __restrict__ y, int Hi, int Wi, int Ho,
                                                                  int Wo, int pad, int act, float leak, int tiles_x,
                                                                  int tiles_per_img, const elem_t* __restrict__ ya,
-                                                                 float* __restrict__ part) {
+                                                                 float* __restrict__ part, NarrowBnIn bnin) {
   static_assert(C8 == 8, "the bank swizzle below assumes 8 chunks (64 channels) per pixel");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   elem8* xs = reinterpret_cast<elem8*>(smem);  // [HALO*HALO][C8], chunk c of pixel (row, col) at c ^ sw(col)
@@ -143,13 +151,29 @@ __global__ __launch_bounds__(256) void narrow_deconv_mfma_kernel(const elem_t* _
   const int ty0 = (trem / tiles_x) * NW_TILE, tx0 = (trem % tiles_x) * NW_TILE;
   const int iy_lo = (ty0 + pad - 4) >> 1, ix_lo = (tx0 + pad - 4) >> 1;
   const elem8 zero8 = {};
+  float bsc[BNIN ? 8 : 1], bsh[BNIN ? 8 : 1];  // BNIN: this thread's chunk is always tid & 7
+  if constexpr (BNIN) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bsc[i] = bnin.scale[(tid & 7) * 8 + i];
+      bsh[i] = bnin.shift[(tid & 7) * 8 + i];
+    }
+  }
   for (int q = tid; q < NW_HALO * NW_HALO * C8; q += 256) {
     const int pix = q >> 3, c = q & 7;
     const int row = pix / NW_HALO, col = pix - row * NW_HALO;
     const int iy = iy_lo + row, ix = ix_lo + col;
     elem8 v = zero8;
-    if ((unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
-      v = *reinterpret_cast<const elem8*>(x + (((size_t)b * Hi + iy) * Wi + ix) * (C8 * 8) + c * 8);
+    if ((unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi) {
+      const size_t o = (((size_t)b * Hi + iy) * Wi + ix) * (C8 * 8) + c * 8;
+      v = *reinterpret_cast<const elem8*>(x + o);
+      if constexpr (BNIN) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (elem_t)apply_act((float)v[i] * bsc[i] + bsh[i], bnin.act, bnin.leak);
+        if ((iy >> 3) == (ty0 >> 4) && (ix >> 3) == (tx0 >> 4))  // this tile's own 8x8 input pixels
+          *reinterpret_cast<elem8*>(bnin.a_out + o) = v;
+      }
+    }
     xs[pix * C8 + (c ^ (((col >> 1) & 3) << 1))] = v;
   }
   if (!WG)
@@ -251,7 +275,7 @@ extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t* x, const elem_t* w, cons
       attr = true;                                                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL(k, grid, dim3(256), shm_m, s, x, w, bias, y, Hi, Wi, Ho, Wo, pad, act, leak, tiles_x,   \
-                       tiles_x * tiles_y, (const elem_t*)nullptr, (float*)nullptr);                            \
+                       tiles_x * tiles_y, (const elem_t*)nullptr, (float*)nullptr, dcg::NarrowBnIn{});         \
   }
     switch (N) {
       case 1: NW_MFMA(1) break;
@@ -303,7 +327,7 @@ extern "C" int DCG_API(dcg_narrow_deconv_dact)(const elem_t* x, const elem_t* w,
       attr = true;                                                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, s, x, w, (const float*)nullptr, y, Hi, Wi, Ho, Wo, pad, act, leak, \
-                       tiles_x, tiles_x * tiles_y, ya, part);                                                  \
+                       tiles_x, tiles_x * tiles_y, ya, part, dcg::NarrowBnIn{});                               \
   }
   switch (N) {
     case 1: NWD(1) break;
@@ -317,4 +341,39 @@ extern "C" int DCG_API(dcg_narrow_deconv_dact)(const elem_t* x, const elem_t* w,
 
 extern "C" int DCG_API(dcg_narrow_deconv_tiles)(int B, int Ho, int Wo) {
   return B * ((Wo + dcg::NW_TILE - 1) / dcg::NW_TILE) * ((Ho + dcg::NW_TILE - 1) / dcg::NW_TILE);
+}
+
+// G's RGB layer forward with the BN apply + activation of the layer below fused into the halo
+// staging (x = that layer's pre-BN output, a_out = its activation, written by the owning tiles)
+extern "C" int DCG_API(dcg_narrow_deconv_bnin)(const elem_t* x, const elem_t* w, const float* bias, elem_t* y, int B,
+                                               int Hi, int Wi, int C, int Ho, int Wo, int N, int pad, int act,
+                                               float leak, const float* scale, const float* shift, int bn_act,
+                                               float bn_leak, elem_t* a_out, hipStream_t s) {
+  // every input pixel must sit under exactly one 16x16 output tile: Ho = 2 Hi, Wo = 2 Wi
+  if (pad < 0 || pad > 2 || C != 64 || N < 1 || N > 4 || Ho != 2 * Hi || Wo != 2 * Wi || !scale || !shift || !a_out)
+    return -2;
+  const int tiles_x = (Wo + dcg::NW_TILE - 1) / dcg::NW_TILE, tiles_y = (Ho + dcg::NW_TILE - 1) / dcg::NW_TILE;
+  const size_t shm = (size_t)dcg::NW_HALO * dcg::NW_HALO * C * sizeof(elem_t);
+  dim3 grid(B * tiles_x * tiles_y);
+  const dcg::NarrowBnIn bn{scale, shift, bn_act, bn_leak, a_out};
+#define NWB(NN)                                                                                                \
+  {                                                                                                            \
+    auto k = dcg::narrow_deconv_mfma_kernel<NN, 8, true, false, true>;                                         \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return (int)e;                                                                      \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm, s, x, w, bias, y, Hi, Wi, Ho, Wo, pad, act, leak, tiles_x,     \
+                       tiles_x * tiles_y, (const elem_t*)nullptr, (float*)nullptr, bn);                        \
+  }
+  switch (N) {
+    case 1: NWB(1) break;
+    case 2: NWB(2) break;
+    case 3: NWB(3) break;
+    default: NWB(4) break;
+  }
+#undef NWB
+  return (int)hipGetLastError();
 }

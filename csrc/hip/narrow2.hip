@@ -43,6 +43,9 @@ extern "C" int DCG_API(dcg_narrow_deconv_dact)(const elem_t*, const elem_t*, ele
                                                int, int, int, int, int, float, float*, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_narrow_deconv_tiles)(int, int, int) { return -1; }
 extern "C" int DCG_API(dcg_wgrad3_taps_per_tile)(int) { return 1; }
+extern "C" int DCG_API(dcg_narrow_deconv_bnin)(const elem_t*, const elem_t*, const float*, elem_t*, int, int, int, int,
+                                               int, int, int, int, int, float, const float*, const float*, int, float,
+                                               elem_t*, hipStream_t) { return -2; }
 #else
 
 namespace dcg {

@@ -431,9 +431,9 @@ class HipEngine:
             self._igemm(prog, name, 1, x, w, y, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad,
                         bias=bias, act=act)
 
-    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema, fused=False):
+    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema, fused=False, apply=True):
         """BN finalize (+EMA) -- unless the statistics GEMM already ran it (fused) -- and
-        apply+act over `groups` row groups."""
+        apply+act over `groups` row groups (apply=False: the consumer applies it, e.g. the head)."""
         cfgm = self.cfg
         st = self.bn[name]
         bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
@@ -444,8 +444,9 @@ class HipEngine:
             prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
                              _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
                              _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
-        prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
-                          rows // groups, act, cfgm.lrelu_leak, 0)
+        if apply:
+            prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
+                              rows // groups, act, cfgm.lrelu_leak, 0)
 
     @staticmethod
     def _rows_per_block(rows_per_group: int, C: int) -> int:
@@ -455,6 +456,17 @@ class HipEngine:
             if rows_per_group % rpb == 0 and (rows_per_group // rpb >= 256 or rpb == 1):
                 return rpb
         return 1
+
+    def _gout_applies_bn(self) -> bool:
+        """G's RGB layer (narrow MFMA kernel) applies the BN + ReLU of the layer below itself."""
+        L = self.gl[-1]
+        return (not self.f32 and len(self.gl) > 1 and bool(self.gl[-2].bn) and L.cout <= 4 and L.cin == 64
+                and L.out_hw == 2 * L.in_hw)
+
+    def _head_applies_bn(self) -> bool:
+        """The D head GEMV applies the top BN layer's BN + LeakyReLU itself (16-bit builds)."""
+        L = self.dl[-1]
+        return not self.f32 and bool(L.bn) and L.cout % 8 == 0 and 512 % L.cout == 0 and self.cfg.d_lin_in % 2048 == 0
 
     def _img_dact(self) -> bool:
         """D layer 0's image gradient (g_loss chain) with G's tanh backward + bias gradient fused
@@ -504,9 +516,19 @@ class HipEngine:
                 self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
                             L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part,
                             fin=self._fin_fwd(prog, L.bn, rows, L.cout, 1, P, update_ema, hold))
+                out_applies = L is self.gl[-2] and self._gout_applies_bn()
                 self._bn_fwd(prog, L.bn, self.g_x[L.name], self.g_a[L.name], rows, L.cout, 1, RELU, part, P,
-                             update_ema, fused=bool(hold))
+                             update_ema, fused=bool(hold), apply=not out_applies)
                 a_prev = self.g_a[L.name]
+            elif self._gout_applies_bn():
+                # RGB layer: the lower layer's BN apply + ReLU in its halo staging (writes that
+                # activation), + bias, tanh into the fake half of D's input
+                Lp = self.gl[-2]
+                st = self.bn[Lp.bn]
+                prog.narrow_deconv_bnin(L.name + "+bn_apply", _p(self.g_x[Lp.name]), _p(nat), _p(Pg[L.name + "/biases"]),
+                                        _p(self.fake), B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad,
+                                        TANH, cfg.lrelu_leak, _p(st["scale"]), _p(st["shift"]), RELU, cfg.lrelu_leak,
+                                        _p(self.g_a[Lp.name]), 0)
             else:  # last: + bias, tanh, written into the fake half of D's input
                 self._deconv_out(prog, L.name, a_prev, nat, self.fake, B, L, pad, Pg[L.name + "/biases"], TANH)
         # D forward on [real | fake]
@@ -547,14 +569,25 @@ class HipEngine:
                     part = self._stats_buf(L.bn, P, L.cout)
                     prog.colstats(L.bn + ".stats", 0, _p(self.d_x[L.name]), 0, 0, 0, 0, 0, 0.0, rows, L.cout, rpb,
                                   rpg, _p(part), 0)
+                head_bn = i == len(self.dl) - 1 and self._head_applies_bn()
                 self._bn_fwd(prog, L.bn, self.d_x[L.name], self.d_a[L.name], rows, L.cout, 2, LRELU, part, P // 2,
-                             update_ema, fused=bool(hold))
+                             update_ema, fused=bool(hold), apply=not head_bn)
             prev = self.d_a[L.name]
         lin = cfg.d_lin_name
-        # head GEMV + the fused 3-loss BCE in its last-arriving block
-        prog.gemv_head("d_head+loss", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits),
-                       B2, cfg.d_lin_in, 0, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob),
-                       _p(self.loss_scale))
+        last = self.dl[-1]
+        if last.bn and self._head_applies_bn():
+            # head GEMV with the top BN layer's apply + LeakyReLU fused (writes its activation) + the
+            # fused 3-loss BCE in its last-arriving block
+            st = self.bn[last.bn]
+            prog.gemv_head_bn("d_head+bn_apply+loss", _p(self.d_x[last.name]), _p(Pd[lin + "/Matrix"]),
+                              _p(Pd[lin + "/bias"]), _p(self.logits), B2, cfg.d_lin_in, 0, _p(self.losses),
+                              _p(self.dl_d), _p(self.dl_g), _p(self.prob), _p(self.loss_scale), _p(st["scale"]),
+                              _p(st["shift"]), last.cout, B, LRELU, cfg.lrelu_leak, _p(self.d_a[last.name]))
+        else:
+            # head GEMV + the fused 3-loss BCE in its last-arriving block
+            prog.gemv_head("d_head+loss", _p(prev), _p(Pd[lin + "/Matrix"]), _p(Pd[lin + "/bias"]), _p(self.logits),
+                           B2, cfg.d_lin_in, 0, _p(self.losses), _p(self.dl_d), _p(self.dl_g), _p(self.prob),
+                           _p(self.loss_scale))
 
     # ---- D backward for d_loss (2B rows, both groups) -> all D gradients
     def _build_d_backward_dloss(self, prog):

@@ -830,3 +830,57 @@ def test_head_gemv_fused_loss_matches_separate():
         torch.cuda.synchronize()
         for a, b in zip(bufs[0], bufs[1]):
             assert torch.equal(a, b)
+
+
+def test_head_gemv_bn_apply_fused():
+    """gemv_head_bn (the top BN layer's apply + LeakyReLU inside the head GEMV, two row groups)
+    == bn_apply_act + gemv_head: the written activation bitwise, logits / losses / seeds too."""
+    h = H()
+    B, K, C = 64, 8192, 512
+    x = bf(rnd(2 * B, K, scale=2.0, seed=113))
+    w = rnd(K, scale=0.02, seed=114)
+    hb = rnd(1, seed=115)
+    scale = (1 + 0.2 * rnd(2, C, seed=116)).contiguous()
+    shift = (0.2 * rnd(2, C, seed=117)).contiguous()
+    ya = torch.empty_like(x)
+    yb = torch.empty_like(x)
+    bufs = [[torch.full((n,), float("nan"), device=dev) for n in (2 * B, 4, 2 * B, B, 2 * B)] for _ in range(2)]
+    pr = _prog()
+    lg, lo, dd, dg, pb = bufs[0]
+    pr.bn_apply_act("apply", _p(x), _p(ya), _p(scale), _p(shift), 2 * B * (K // C), C, B * (K // C), 2, 0.2, 0)
+    pr.gemv_head("hl", _p(ya), _p(w), _p(hb), _p(lg), 2 * B, K, 0, _p(lo), _p(dd), _p(dg), _p(pb), 0)
+    lg2, lo2, dd2, dg2, pb2 = bufs[1]
+    pr.gemv_head_bn("hbn", _p(x), _p(w), _p(hb), _p(lg2), 2 * B, K, 0, _p(lo2), _p(dd2), _p(dg2), _p(pb2), 0,
+                    _p(scale), _p(shift), C, B, 2, 0.2, _p(yb))
+    for _ in range(2):
+        h.run(pr)
+        torch.cuda.synchronize()
+        assert torch.equal(ya, yb)  # the activation the backward reads: bitwise
+        for a, b in zip(bufs[0], bufs[1]):  # same operands; FMA contraction may differ in the last bit
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,Hi,N", [(4, 32, 3), (3, 16, 1)])
+def test_narrow_deconv_bn_input_fused(B, Hi, N):
+    """narrow_deconv_bnin (the lower layer's BN apply + ReLU in the halo staging) == bn_apply_act
+    + narrow_deconv: the written activation and the RGB output bitwise."""
+    h = H()
+    Ho = 2 * Hi
+    pad = max((Hi - 1) * 2 + 5 - Ho, 0) // 2
+    x = bf(rnd(B, Hi, Hi, 64, scale=2.0, seed=120))
+    w = bf(rnd(5, 5, N, 64, scale=0.05, seed=121))
+    bias = rnd(N, scale=0.1, seed=122)
+    scale = (1 + 0.2 * rnd(64, seed=123)).contiguous()
+    shift = (0.2 * rnd(64, seed=124)).contiguous()
+    a1, a2 = torch.empty_like(x), torch.empty_like(x)
+    y1 = torch.empty(B, Ho, Ho, N, device=dev, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y1)
+    pr = _prog()
+    pr.bn_apply_act("apply", _p(x), _p(a1), _p(scale), _p(shift), B * Hi * Hi, 64, B * Hi * Hi, 1, 0.2, 0)
+    pr.narrow_deconv("nd", _p(a1), _p(w), _p(bias), _p(y1), B, Hi, Hi, 64, Ho, Ho, N, pad, 3, 0.2, 0)
+    pr.narrow_deconv_bnin("ndb", _p(x), _p(w), _p(bias), _p(y2), B, Hi, Hi, 64, Ho, Ho, N, pad, 3, 0.2, _p(scale),
+                          _p(shift), 1, 0.2, _p(a2), 0)
+    h.run(pr)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2)
+    assert torch.equal(y1, y2)
