@@ -57,6 +57,10 @@ def main():
         x = (torch.rand(B, 64, 64, 3, device=dev) * 2 - 1).to(torch.bfloat16)
         d = (torch.rand(B, 32, 32, 64, device=dev) * 2 - 1).to(torch.bfloat16)
         out = torch.empty(25, 3, 64, device=dev)
+        for cpw in (1, 2, 4, 8):
+            p_c = ext.Program()
+            p_c.nwgrad("nw", H._p(x), B, 64, 64, 3, H._p(d), 32, 32, 1, H._p(out), 0, cpw)
+            res.setdefault(name, {})["nwgrad+reduce_cpw%d_us" % cpw] = timeit(p_c, a.reps)
         p_new = ext.Program()
         p_new.nwgrad("nw", H._p(x), B, 64, 64, 3, H._p(d), 32, 32, 1, H._p(out), 0)
         col = torch.empty(B * 32 * 32, 80, device=dev, dtype=torch.bfloat16)
@@ -66,7 +70,7 @@ def main():
         p_old.im2col_s2("i2c", H._p(x), H._p(col), B, 64, 64, 3, 32, 32, 1, 1, 80, 0)
         p_old.wgrad("wg", 2, H._p(col), 1, 1, 80, H._p(d), B * 1024, 1, 1, 64, 0, cfg, splits, H._p(slabs),
                     H._p(out), 75 * 64, 1.0, 0)
-        res[name] = {"im2col+wgrad+reduce_us": timeit(p_old, a.reps), "nwgrad+reduce_us": timeit(p_new, a.reps)}
+        res[name].update({"im2col+wgrad+reduce_us": timeit(p_old, a.reps), "nwgrad+reduce_us": timeit(p_new, a.reps)})
     for k, v in res.items():
         print(json.dumps({"shape": k, **{kk: round(vv, 2) for kk, vv in v.items()}}))
 

@@ -845,14 +845,16 @@ class Program {
   // = sum over output pixels of the stride-2 window of x times d; per-workgroup partials
   // (workspace) summed in workgroup order by splitk_reduce -- deterministic.
   int nwgrad(std::string name, uintptr_t x, int B, int H, int W, int Cin, uintptr_t d, int Hd, int Wd, int pad,
-             uintptr_t dst, int stream) {
+             uintptr_t dst, int stream, int chunks_per_wg) {
     int tyc, wr, wc;
     if (dt_ == 2 || KF(dcg_nwgrad_plan)(H, W, Hd, Wd, &tyc, &wr, &wc))
       throw std::runtime_error("nwgrad: unsupported shape / dtype");
     const int chunks_img = (Hd + tyc - 1) / tyc;
     const int total = B * chunks_img;
-    int cpw = total / 512;  // >= 512 workgroups where the batch allows it, <= 4 chunks each
-    cpw = cpw < 1 ? 1 : (cpw > 4 ? 4 : cpw);
+    // auto: chunks per workgroup (<= 8) so that about NWG_TARGET workgroups run -- fewer
+    // workgroups = fewer partial slabs for the reduce, more = more latency hiding
+    int cpw = chunks_per_wg > 0 ? chunks_per_wg : total / 256;
+    cpw = cpw < 1 ? 1 : (cpw > 8 ? 8 : cpw);
     const int wg = B * ((chunks_img + cpw - 1) / cpw);
     const size_t n = (size_t)25 * Cin * 64;
     float* part = reinterpret_cast<float*>(dev_alloc((size_t)wg * n * sizeof(float)));
@@ -1079,7 +1081,9 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("gemv_head_bn", &Program::gemv_head_bn)
       .def("narrow_deconv_bnin", &Program::narrow_deconv_bnin)
       .def("nwgrad_ok", &Program::nwgrad_ok)
-      .def("nwgrad", &Program::nwgrad)
+      .def("nwgrad", &Program::nwgrad, py::arg("name"), py::arg("x"), py::arg("B"), py::arg("H"), py::arg("W"),
+           py::arg("Cin"), py::arg("d"), py::arg("Hd"), py::arg("Wd"), py::arg("pad"), py::arg("dst"), py::arg("stream"),
+           py::arg("chunks_per_wg") = 0)
       .def("pack", &Program::pack)
       .def("philox_uniform", &Program::philox_uniform)
       .def("im2col_s2", &Program::im2col_s2)
