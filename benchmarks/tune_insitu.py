@@ -1,0 +1,158 @@
+"""In-situ tile tuning: pick each GEMM's (tile, LDS stages, split-K) by the WHOLE training step's
+time instead of the kernel's isolated time (``bench_kernels.py`` / ``bench_wgrad.py``).
+
+In the step, the D chain and the G chain run concurrently and every kernel shares the GPU with
+another one, so the isolated optimum is not always the step optimum (a tile with fewer workgroups
+can co-run better). Coordinate descent over the tuned-table entries the step uses: for each entry,
+try its neighbours (half / double split-K, one more / one fewer LDS stage, a few sibling tiles),
+rebuild the engine, time ``--steps`` graph-replayed steps, keep a change only if it beats the
+incumbent by more than ``--min_gain``. One process, every candidate on the same GPU.
+
+``python -m benchmarks.tune_insitu [--steps 150] [--passes 1] [--write]`` -- ``--write`` stores the
+result in ops/igemm_tuned.json (the table the engine reads).
+"""
+import argparse
+import gc
+import json
+import os
+import time
+
+import torch
+
+from distributed_tensorflow_for_dcgan_amd.ops import hip as H
+from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+
+
+def step_ms(cfg, B, steps, warmup):
+    dev = torch.device("cuda", 0)
+    eng = HipEngine(cfg, B, dev, seed=0)
+    real = torch.rand(B, cfg.output_size, cfg.output_size, cfg.c_dim, device=dev) * 2 - 1
+    eng.set_synthetic_batch(real)
+    for _ in range(warmup):
+        eng.train_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.train_step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    del eng
+    gc.collect()
+    torch.cuda.empty_cache()
+    return ms
+
+
+def used_keys(cfg, B):
+    """Tuned-table keys the engine consults while building the step."""
+    seen = []
+    orig_i, orig_w = H.igemm_cfg_for, H.wgrad3_cfg_for
+
+    def log_i(mode, Bn, Hin, Win, Kc, Hout, Wout, N, *a, **k):
+        key = "%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N)
+        if key not in seen:
+            seen.append(key)
+        return orig_i(mode, Bn, Hin, Win, Kc, Hout, Wout, N, *a, **k)
+
+    def log_w(Mc, Nc, Bn, Hd, Wd, Hg):
+        key = H.wgrad3_key(Mc, Nc, Bn, Hd, Wd, Hg)
+        if key not in seen:
+            seen.append(key)
+        return orig_w(Mc, Nc, Bn, Hd, Wd, Hg)
+
+    H.igemm_cfg_for, H.wgrad3_cfg_for = log_i, log_w
+    import distributed_tensorflow_for_dcgan_amd.engine.hip_engine as E
+    E.H.igemm_cfg_for, E.H.wgrad3_cfg_for = log_i, log_w
+    try:
+        eng = HipEngine(cfg, B, torch.device("cuda", 0), seed=0, graph=False)
+        del eng
+    finally:
+        H.igemm_cfg_for, H.wgrad3_cfg_for = orig_i, orig_w
+        E.H.igemm_cfg_for, E.H.wgrad3_cfg_for = orig_i, orig_w
+    gc.collect()
+    torch.cuda.empty_cache()
+    return [k for k in seen if k in H.tuned_table()]
+
+
+def neighbours(key, cur, tiles=False):
+    cfg, sp = cur
+    out = []
+    for s2 in (sp // 2, sp * 2, sp + 1, sp - 1):
+        if 1 <= s2 <= 32 and s2 != sp:
+            out.append((cfg, s2))
+    if key.startswith("w3,"):
+        sib = {310: (311, 313), 311: (310, 313), 313: (311, 312), 312: (313, 311), 300: (310,), 301: (311,)}
+        out += [(c, sp) for c in sib.get(cfg, ())]
+    elif cfg >= 200:
+        ns = (cfg - 200) // 10
+        tile = cfg % 10
+        for ns2 in (0, 1):  # NS = 3 (20x) and NS = 2 (21x)
+            if ns2 != ns:
+                out.append((200 + 10 * ns2 + tile, sp))
+        for t2 in ((0, 1, 3, 4, 6) if tiles else ()):
+            if t2 != tile:
+                out.append((200 + 10 * ns + t2, sp))
+    seen, res = set(), []
+    for c in out:
+        if c not in seen and c != cur:
+            seen.add(c)
+            res.append(c)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=150)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--passes", type=int, default=1)
+    ap.add_argument("--min_gain", type=float, default=0.003, help="relative step-time gain to accept a change")
+    ap.add_argument("--only", default="", help="comma-separated key prefixes")
+    ap.add_argument("--tiles", action="store_true", help="also try sibling tiles (slower)")
+    ap.add_argument("--write", action="store_true")
+    ap.add_argument("--out", default="", help="also write the resulting table (JSON) here")
+    a = ap.parse_args()
+    cfg = DCGANConfig()
+    table = H.tuned_table()
+    keys = used_keys(cfg, a.batch)
+    if a.only:
+        keys = [k for k in keys if any(k.startswith(p) for p in a.only.split(","))]
+    print("keys in the step: %d" % len(keys), flush=True)
+    best = step_ms(cfg, a.batch, a.steps, a.warmup)
+    print("incumbent %.4f ms" % best, flush=True)
+    log = []
+    for ps in range(a.passes):
+        for key in keys:
+            cur = table[key]
+            for cand in neighbours(key, cur, a.tiles):
+                table[key] = cand
+                try:
+                    ms = step_ms(cfg, a.batch, a.steps, a.warmup)
+                except Exception as e:  # illegal combination for this layer: skip
+                    print("  %s %d:%d failed: %s" % (key, cand[0], cand[1], str(e)[:80]), flush=True)
+                    table[key] = cur
+                    continue
+                gain = (best - ms) / best
+                print("  %-28s %d:%d -> %d:%d  %.4f ms (%+.2f%%)" % (key, cur[0], cur[1], cand[0], cand[1], ms,
+                                                                     100 * gain), flush=True)
+                log.append({"key": key, "from": "%d:%d" % cur, "to": "%d:%d" % cand, "ms": round(ms, 4)})
+                if gain > a.min_gain:
+                    cur, best = cand, ms
+                    print("  * keep %s = %d:%d (%.4f ms)" % (key, cand[0], cand[1], ms), flush=True)
+                else:
+                    table[key] = cur
+            table[key] = cur
+        # re-measure the incumbent (noise guard for the next pass)
+        best = step_ms(cfg, a.batch, a.steps, a.warmup)
+        print("pass %d done: %.4f ms" % (ps + 1, best), flush=True)
+    out = {k: "%d:%d" % v for k, v in sorted(table.items())}
+    if a.out:
+        json.dump({"table": out, "final_ms": best, "trials": log}, open(a.out, "w"), indent=1)
+    if a.write:
+        path = os.path.join(os.path.dirname(H.__file__), "igemm_tuned.json")
+        json.dump(out, open(path, "w"), indent=1, sort_keys=True)
+        print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()
