@@ -81,15 +81,18 @@ def neighbours(key, cur, tiles=False):
         if 1 <= s2 <= 32 and s2 != sp:
             out.append((cfg, s2))
     if key.startswith("w3,"):
-        sib = {310: (311, 313), 311: (310, 313), 313: (311, 312), 312: (313, 311), 300: (310,), 301: (311,)}
-        out += [(c, sp) for c in sib.get(cfg, ())]
+        Mc = int(key.split(",")[1])
+        fam = [300, 301, 302, 303, 310, 311, 312, 313] + ([320, 322, 330, 332] if Mc == 64 else [])
+        if not tiles:
+            fam = {310: (311, 313), 311: (310, 313), 313: (311, 312), 312: (313, 311)}.get(cfg, ())
+        out += [(c, sp) for c in fam]
     elif cfg >= 200:
         ns = (cfg - 200) // 10
         tile = cfg % 10
-        for ns2 in (0, 1):  # NS = 3 (20x) and NS = 2 (21x)
+        for ns2 in (0, 1, 2):  # NS = 3 (20x), 2 (21x), 4 (22x)
             if ns2 != ns:
                 out.append((200 + 10 * ns2 + tile, sp))
-        for t2 in ((0, 1, 3, 4, 6) if tiles else ()):
+        for t2 in (range(9) if tiles else ()):
             if t2 != tile:
                 out.append((200 + 10 * ns + t2, sp))
     seen, res = set(), []
