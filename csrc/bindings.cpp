@@ -652,6 +652,33 @@ class Program {
                               P<const float>(rstd), C, rpg, act, leak, P<float>(part), s);
     }, acc.v);
   }
+  // the head backward with RS row splits: BN partial rows [(g RS + y) S + sp] (ppg = RS S);
+  // dW partials in a workspace summed by the last split of each column block (in-kernel)
+  int head_bwd_rs(std::string name, uintptr_t x, uintptr_t dl, uintptr_t w, uintptr_t dx, uintptr_t dW, uintptr_t db,
+                  int R, int K, int stream, uintptr_t bx, uintptr_t by, uintptr_t mean, uintptr_t rstd, int C, int rpg,
+                  int act, float leak, uintptr_t part, int RS) {
+    const size_t t = (size_t)R * K * es_;
+    AccList acc;
+    acc.r(x, t).r(dl, (size_t)R * 4).r(w, (size_t)K * 4).w(dx, t).w(dW, (size_t)K * 4).w(db, 4);
+    if (bx) {
+      const size_t groups = (size_t)((R + rpg - 1) / rpg);
+      acc.r(bx, t).r(by, t).r(mean, groups * C * 4).r(rstd, groups * C * 4)
+          .w(part, groups * RS * (K / C) * 2 * C * 4);
+    }
+    float* ws = nullptr;
+    unsigned* ctr = nullptr;
+    if (dW && RS > 1) {
+      ws = reinterpret_cast<float*>(dev_alloc((size_t)RS * K * sizeof(float)));
+      ctr = reinterpret_cast<unsigned*>(dev_alloc((size_t)((K + 63) / 64) * sizeof(unsigned), nullptr, true));
+      acc.w((uintptr_t)ws, (size_t)RS * K * 4).w((uintptr_t)ctr, (size_t)((K + 63) / 64) * 4);
+    }
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_head_bwd_rs)(P<const elem_t>(x), P<const float>(dl), P<const float>(w), P<elem_t>(dx),
+                                 P<float>(dW), P<float>(db), R, K, P<const elem_t>(bx), P<const elem_t>(by),
+                                 P<const float>(mean), P<const float>(rstd), C, rpg, act, leak, P<float>(part), RS, ws,
+                                 ctr, s);
+    }, acc.v);
+  }
 
   int sum_partials(std::string name, uintptr_t part, int Pn, int stride, int C, uintptr_t dst, int stream) {
     AccList acc;
@@ -1093,6 +1120,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("nconv_tiles", &Program::nconv_tiles)
       .def("narrow_deconv_dact", &Program::narrow_deconv_dact)
       .def("gemv_head_bn", &Program::gemv_head_bn)
+      .def("head_bwd_rs", &Program::head_bwd_rs)
       .def("narrow_deconv_bnin", &Program::narrow_deconv_bnin)
       .def("nwgrad_ok", &Program::nwgrad_ok)
       .def("nwgrad", &Program::nwgrad, py::arg("name"), py::arg("x"), py::arg("B"), py::arg("H"), py::arg("W"),

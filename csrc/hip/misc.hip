@@ -365,12 +365,18 @@ __global__ void sum_vec_kernel(const float* __restrict__ v, int n, float* __rest
 //   g = dx * act'(y), xhat = (x - mean[g][c]) * rstd[g][c] -- of the STORED (rounded) dx.
 // block = 64 columns (8 chunks of 8, inside one spatial position) x 32 row lanes; row lanes
 // reduce through LDS in a fixed order (deterministic). Block 0's second wave sums dl for db.
+// Row splits (gridDim.y = RS > 1): workgroup (x, y) takes rows [y R/RS, (y+1) R/RS) of column block
+// x -- RS times the workgroups for the same bytes. The BN-statistics partial rows become
+// [(g RS + y) S + sp] (zeros for a group the split does not touch); dW partials go to dw_ws[y][K]
+// (write-through) and the last of the RS arrivals per column block (counter dw_ctr[x], re-armed)
+// sums them in split order -- deterministic.
 __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict__ xa, const float* __restrict__ dl,
                                                        const float* __restrict__ w, elem_t* __restrict__ dx,
                                                        float* __restrict__ dW, float* __restrict__ db, int R, int K,
                                                        const elem_t* __restrict__ bx, const elem_t* __restrict__ by,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                       int C, int rpg, int act, float leak, float* __restrict__ part) {
+                                                       int C, int rpg, int act, float leak, float* __restrict__ part,
+                                                       float* __restrict__ dw_ws, unsigned* __restrict__ dw_ctr) {
   __shared__ float red[32][65];
   __shared__ float bred[2][2][32][65];  // [group][stat][lane][col]
   const int tid = threadIdx.x, c = tid & 7, rl = tid >> 3;
@@ -392,13 +398,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
     }
   }
   const float slope = act == ACT_LRELU ? leak : 0.f;
+  const int RS = gridDim.y, rsp = blockIdx.y;
+  const int r_lo = rsp * (R / RS), r_hi = RS > 1 ? r_lo + R / RS : R;
   if (kok) {
-    for (int rb = rl; rb < R; rb += 4 * 32) {  // 4 rows per iteration, loads first
+    for (int rb = r_lo + rl; rb < r_hi; rb += 4 * 32) {  // 4 rows per iteration, loads first
       elem8 xv[4], yv[4], xb[4];
       float gv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int r = rb + 32 * u < R ? rb + 32 * u : rb;
+        const int r = rb + 32 * u < r_hi ? rb + 32 * u : rb;
         const size_t o = (size_t)r * K + k;
         xv[u] = xa ? ld8(xa + o) : (elem8)(elem_t)0.f;
         if (stats) {
@@ -410,7 +418,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = rb + 32 * u;
-        if (r >= R) break;
+        if (r >= r_hi) break;
         const int grp = r >= rpg ? 1 : 0;
         const elem8 xe = xv[u];
         elem8 ob;
@@ -447,10 +455,25 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
       }
   }
   __syncthreads();
-  if (dW && tid < 64 && blockIdx.x * 64 + tid < K) {
+  if (dW && RS == 1 && tid < 64 && blockIdx.x * 64 + tid < K) {
     float a = 0.f;
     for (int l = 0; l < 32; ++l) a += red[l][tid];
     dW[blockIdx.x * 64 + tid] = a;
+  }
+  if (dW && RS > 1) {  // split partial, then the last arrival of the column block sums the splits in order
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(dw_ws, (uint32_t)((size_t)RS * K * 4));
+    const int col = blockIdx.x * 64 + tid;
+    if (tid < 64 && col < K) {
+      float a = 0.f;
+      for (int l = 0; l < 32; ++l) a += red[l][tid];
+      st_sc1_f32(rw, (uint32_t)((size_t)rsp * K + col) * 4u, a);
+    }
+    __shared__ int last_s;
+    if (last_arrival(dw_ctr + blockIdx.x, (unsigned)RS, &last_s) && tid < 64 && col < K) {
+      float a = 0.f;
+      for (int q = 0; q < RS; ++q) a += ld_sc1_f32(rw, (uint32_t)((size_t)q * K + col) * 4u);
+      dW[col] = a;
+    }
   }
   if (stats) {
     for (int h = 16; h > 0; h >>= 1) {  // fixed-order tree over the 32 row lanes
@@ -465,10 +488,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
     const int k0 = blockIdx.x * 64, sp = k0 / C, c0 = k0 % C;
     for (int q = tid; q < groups * 2 * 64; q += 256) {
       const int col = q & 63, st = (q >> 6) & 1, g = q >> 7;
-      part[((size_t)(g * S + sp) * 2 + st) * C + c0 + col] = bred[g][st][0][col];
+      part[((size_t)((g * RS + rsp) * S + sp) * 2 + st) * C + c0 + col] = bred[g][st][0][col];
     }
   }
-  if (db && blockIdx.x == 0 && tid >= 64 && tid < 128) {
+  if (db && blockIdx.x == 0 && blockIdx.y == 0 && tid >= 64 && tid < 128) {
     const int lane = tid - 64;
     float a = 0.f;
     for (int r = lane; r < R; r += 64) a += dl[r];
@@ -936,7 +959,23 @@ extern "C" int DCG_API(dcg_head_bwd)(const elem_t* x, const float* dl, const flo
   if (bx && (C <= 0 || C % 64 || K % C || rpg <= 0 || (R + rpg - 1) / rpg > 2 || !by || !mean || !rstd || !part))
     return -2;
   hipLaunchKernelGGL(head_bwd_kernel, dim3((K + 63) / 64), dim3(256), 0, s, x, dl, w, dx, dW, db, R, K, bx, by, mean,
-                     rstd, C, rpg > 0 ? rpg : R, act, leak, part);
+                     rstd, C, rpg > 0 ? rpg : R, act, leak, part, (float*)nullptr, (unsigned*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// the head backward with RS row splits (R % RS == 0; with statistics, R / RS must divide rpg):
+// dw_ws [RS][K] and dw_ctr [ceil(K / 64)] (zero-initialised) when dW != nullptr and RS > 1
+extern "C" int DCG_API(dcg_head_bwd_rs)(const elem_t* x, const float* dl, const float* w, elem_t* dx, float* dW,
+                                        float* db, int R, int K, const elem_t* bx, const elem_t* by,
+                                        const float* mean, const float* rstd, int C, int rpg, int act, float leak,
+                                        float* part, int RS, float* dw_ws, unsigned* dw_ctr, hipStream_t s) {
+  if (K % 8 || RS < 1 || R % RS) return -2;
+  if (bx && (C <= 0 || C % 64 || K % C || rpg <= 0 || (R + rpg - 1) / rpg > 2 || !by || !mean || !rstd || !part ||
+             (RS > 1 && rpg % (R / RS))))
+    return -2;
+  if (dW && RS > 1 && (!dw_ws || !dw_ctr)) return -2;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((K + 63) / 64, RS), dim3(256), 0, s, x, dl, w, dx, dW, db, R, K, bx, by,
+                     mean, rstd, C, rpg > 0 ? rpg : R, act, leak, part, dw_ws, dw_ctr);
   return (int)hipGetLastError();
 }
 

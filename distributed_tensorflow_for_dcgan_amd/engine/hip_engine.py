@@ -679,13 +679,17 @@ class HipEngine:
             prog.head_bwd(name, _p(xa), _p(dl), _p(Pd[lin + "/Matrix"]), _p(dx), _p(dW), _p(db), R, K, 0)
             return None
         S = K // C
-        part = self._stats_buf(name + ".bnstats", groups * S, C)
+        # row splits: RS x the workgroups of one-per-64-columns (the head's R rows are few)
+        RS = 2  # (A/B 1 / 2 / 4 splits: 2 best, profiles/r2/ab_head_nconv_nwgrad_r2.txt)
+        while RS > 1 and (R % RS or (R // groups) % (R // RS)):
+            RS //= 2
+        part = self._stats_buf(name + ".bnstats", groups * RS * S, C)
         st = self.bn[last.bn]
         r0 = 0 if group_offset == 0 else self.B
-        prog.head_bwd(name, _p(xa), _p(dl), _p(Pd[lin + "/Matrix"]), _p(dx), _p(dW), _p(db), R, K, 0,
-                      _p(self.d_x[last.name][r0:]), _p(self.d_a[last.name][r0:]), _p(st["mean"][group_offset:]),
-                      _p(st["rstd"][group_offset:]), C, R // groups, LRELU, cfg.lrelu_leak, _p(part))
-        return part, S
+        prog.head_bwd_rs(name, _p(xa), _p(dl), _p(Pd[lin + "/Matrix"]), _p(dx), _p(dW), _p(db), R, K, 0,
+                         _p(self.d_x[last.name][r0:]), _p(self.d_a[last.name][r0:]), _p(st["mean"][group_offset:]),
+                         _p(st["rstd"][group_offset:]), C, R // groups, LRELU, cfg.lrelu_leak, _p(part), RS)
+        return part, RS * S
 
     def _colsum(self, prog, name, x, rows, C, dst, chain):
         if C % 8 == 0:
@@ -812,6 +816,7 @@ class HipEngine:
             # narrow2.hip: the data gradient is the stride-2 conv of the image gradient with the
             # [5,5,co,ci] = HWIO[5,5,3,64] weight (nconv, BN-backward statistics of the layer below
             # fused), the weight gradient reads the image gradient's window directly (nwgrad)
+            # persistent grid (one workgroup per tile measured the same beside the D chain)
             grid = H.nconv_grid(prog, B, Lg.in_hw, Lg.in_hw)
             part = self._stats_buf(bn_prev + ".bwd", grid, Lg.cin)
             st = self.bn[bn_prev]

@@ -452,9 +452,11 @@ def conv3_direct(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
 NCONV_MAX_GRID = 512  # persistent workgroups of nconv (2 per CU: the kernel's occupancy)
 
 
-def nconv_grid(prog, B: int, Ho: int, Wo: int) -> int:
-    """Persistent workgroup count of an nconv launch (= its BN-backward partial rows)."""
-    return min(prog.nconv_tiles(B, Ho, Wo), NCONV_MAX_GRID)
+def nconv_grid(prog, B: int, Ho: int, Wo: int, cap: int = NCONV_MAX_GRID) -> int:
+    """Workgroup count of an nconv launch (= its BN-backward partial rows): persistent (cap
+    workgroups looping over the tiles) or, with cap <= 0, one workgroup per tile."""
+    tiles = prog.nconv_tiles(B, Ho, Wo)
+    return tiles if cap <= 0 else min(tiles, cap)
 
 
 def nconv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,

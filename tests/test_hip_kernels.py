@@ -884,3 +884,45 @@ def test_narrow_deconv_bn_input_fused(B, Hi, N):
     torch.cuda.synchronize()
     assert torch.equal(a1, a2)
     assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize("R,groups,RS", [(256, 2, 4), (128, 1, 4), (256, 2, 2)])
+def test_head_bwd_row_splits(R, groups, RS):
+    """Head backward with RS row splits: dx bitwise, dW (split partials summed in order by the
+    last split of each column block, counters re-armed across launches), per-group BN partial
+    rows [(g RS + y) S + sp] summing to the reference statistics."""
+    h = H()
+    K, C = 8192, 512
+    S = K // C
+    xa = bf(rnd(R, K, seed=130))
+    dl = rnd(R, seed=131)
+    w = rnd(K, scale=0.02, seed=132)
+    bx = bf(rnd(R, K, seed=133))
+    by = bf(rnd(R, K, seed=134))
+    mean = rnd(groups, C, scale=0.1, seed=135)
+    rstd = rnd(groups, C, seed=136).abs() + 0.5
+    dx = torch.empty_like(xa)
+    dW = torch.empty(K, device=dev)
+    db = torch.empty(1, device=dev)
+    part = torch.full((groups * RS * S, 2, C), float("nan"), device=dev)
+    pr = _prog()
+    pr.head_bwd_rs("hbs", _p(xa), _p(dl), _p(w), _p(dx), _p(dW), _p(db), R, K, 0, _p(bx), _p(by), _p(mean), _p(rstd),
+                   C, R // groups, 2, 0.2, _p(part), RS)
+    for rep in range(2):
+        h.run(pr)
+        torch.cuda.synchronize()
+        if rep == 0:
+            first = dW.clone()
+    assert torch.equal(first, dW)
+    assert torch.equal(dx, (dl[:, None] * w[None, :]).to(torch.bfloat16))
+    close(dW, xa.float().t() @ dl, 1e-4, "dW")
+    close(db, dl.sum().reshape(1), 1e-5, "db")
+    g = dx.float() * torch.where(by.float() > 0, 1.0, 0.2)
+    rpg = R // groups
+    ppg = RS * S
+    for gi in range(groups):
+        gg = g[gi * rpg:(gi + 1) * rpg].reshape(rpg, S, C)
+        xh = (bx.float()[gi * rpg:(gi + 1) * rpg].reshape(rpg, S, C) - mean[gi]) * rstd[gi]
+        pg = part[gi * ppg:(gi + 1) * ppg].reshape(RS, S, 2, C).sum(0)
+        close(pg[:, 0], gg.sum(0), 1e-4, "sum g")
+        close(pg[:, 1], (gg * xh).sum(0), 1e-4, "sum g xhat")
