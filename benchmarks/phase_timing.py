@@ -49,9 +49,10 @@ def main():
     if a.fake_comm_us:
         g_us, top_us, rest_us = (float(x) for x in a.fake_comm_us.split(","))
         cpu = _cycles_per_us()
-        # collective call points of DDP on a comm stream (the programs were built for W=1, so the
-        # Adam 1/W scale stays 1 -- only the stream order of the DDP step is emulated)
+        # collective call points of DDP on a comm stream; the update program is rebuilt for W=2
+        # (Adam scales the un-reduced gradients by 1/2: only timing and stream order are emulated)
         eng.world = 2
+        eng._build_updates()  # the update program a real W=2 build runs (split Adam(G) / Adam(D))
         eng.comm_stream = torch.cuda.Stream(device=dev)
         eng._ar_g, eng._ar_dtop, eng._ar_drest = (FakeReducer(u, cpu) for u in (g_us, top_us, rest_us))
     eng.set_synthetic_batch(torch.rand(a.batch_size, 64, 64, 3, device=dev) * 2 - 1)

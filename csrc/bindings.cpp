@@ -319,7 +319,13 @@ class Program {
       const size_t lds = hh ? h_shm : (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
       const size_t nt = v3 ? (size_t)KF(dcg_igemm3_threads)(cfg) : 256;
-      if ((size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + 64 * nt > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
+      // igemm3 (waves along M per tile id, igemm3.hip DCG_IGEMM3_TILES): the row-lane scratch may
+      // alias the C tile; v1 / igemmh keep them apart
+      static const int kWM3[10] = {2, 4, 1, 2, 2, 2, 4, 2, 8, 2};
+      const size_t wm = v3 && !hh ? (size_t)kWM3[cfg % 10] : 4;
+      const size_t ct = (size_t)bm * (bn + 8) * 2, r2 = 64 * nt;
+      const size_t need = (bm + 2 * wm * bn) * 4 + (v3 && !hh ? std::max(ct, r2) : ct + r2);
+      if (need > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
       const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
       if (bnb_store_g) {  // activation backward only (no BN): x, mean, rstd and groups unused

@@ -128,8 +128,9 @@ __device__ __forceinline__ void lane_tree(float* red2) {
 // the BN backward needs, without a separate pass over three tensors. Each thread owns one fixed
 // 8-channel chunk; row lanes are reduced through LDS scratch (red2, 16 KiB) in a fixed order.
 // Requires elem_t output with N % 8 == 0 (the caller checks) and a tile inside one BN group.
-// NT threads per workgroup; red2 holds 64 * NT bytes.
-template <int BM, int BN, int NT = 256>
+// NT threads per workgroup; red2 holds 64 * NT bytes. ALIAS: red2 overlaps ctile (a barrier
+// separates the last ctile read from the first red2 write).
+template <int BM, int BN, int NT = 256, bool ALIAS = false>
 __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* rowoff, const elem_t* ctile,
                                               float* red2, int n0, int m0, float* dst) {
   constexpr int CPAD = BN + 8, CPR = BN / 8, RL = NT / CPR;
@@ -159,6 +160,7 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
       }
       *reinterpret_cast<u32x4*>(C + o) = __builtin_bit_cast(u32x4, gv);
     }
+    if constexpr (ALIAS) __syncthreads();
 #pragma unroll
     for (int i = 0; i < 8; ++i) red2[(rl * BN + 8 * c + i) * 2 + 0] = s[i];
     __syncthreads();
@@ -196,6 +198,7 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
       s2[i] += gv * ((float)xv[i] - mu[i]) * rs[i];
     }
   }
+  if constexpr (ALIAS) __syncthreads();
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     red2[(rl * BN + 8 * c + i) * 2 + 0] = s[i];

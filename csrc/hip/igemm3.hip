@@ -373,11 +373,16 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   frag_epilogue_dispatch<FM, FN, TM, TN, BN>(acc, p, rowoff, red, ctile, wm, wn, fr, fq, n0, do_stats, vec, m0);
   if (stamp && tid == 0) stamp[5] = __builtin_amdgcn_s_memtime();
   if (p.bnb_x) {  // BN-backward statistics fused into the store pass (epilogue.h)
-    constexpr bool kFits = (BM + 2 * WM * BN) * 4 + BM * CPAD * 2 + 64 * NT <= NS * STAGE;
-    if constexpr (kFits) {
+    // row-lane scratch (64 * NT bytes) after the C tile, or -- when that does not fit (8-wave
+    // tiles at NS = 2) -- over the C tile, written after a barrier once the store pass read it
+    constexpr int kEpi = (BM + 2 * WM * BN) * 4, kCt = BM * CPAD * 2, kRed2 = 64 * NT;
+    constexpr bool kSep = kEpi + kCt + kRed2 <= NS * STAGE;
+    constexpr bool kAlias = !kSep && kEpi + (kCt > kRed2 ? kCt : kRed2) <= NS * STAGE;
+    if constexpr (kSep || kAlias) {
       __syncthreads();
-      float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + BM * CPAD * 2);
-      vec_store_bnb<BM, BN, NT>(p, rowoff, ctile, red2, n0, m0, p.stats + (size_t)(mt * p.nphases + phase) * 2 * N);
+      float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + (kSep ? kCt : 0));
+      vec_store_bnb<BM, BN, NT, kAlias>(p, rowoff, ctile, red2, n0, m0,
+                                        p.stats + (size_t)(mt * p.nphases + phase) * 2 * N);
       if (p.fin) tile_bn_finalize<BN, NT>(*p.fin, mt * p.nphases + phase, nt, n0, reinterpret_cast<int*>(lds));
     } else {
       __builtin_trap();  // the host only requests fused statistics on tiles with the LDS for them

@@ -72,6 +72,7 @@ IGEMM_CFGS = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (32, 64
 IGEMM3_TILES = {0: (128, 128), 1: (256, 64), 2: (64, 256), 3: (128, 64), 4: (64, 128), 5: (64, 64),
                 6: (256, 128), 7: (128, 256), 8: (512, 64)}  # 6..8: 8-wave (512-thread) workgroups
 IGEMM3_WAVES = {6: 8, 7: 8, 8: 8}
+IGEMM3_WM = {0: 2, 1: 4, 2: 1, 3: 2, 4: 2, 5: 2, 6: 4, 7: 2, 8: 8}  # waves along M (igemm3.hip tiles)
 IGEMM3_STAGES = (3, 2, 4, 5)  # LDS stages of igemm3 cfg 200+10k+id
 
 
@@ -169,9 +170,13 @@ def bnb_fits(cfg: int) -> bool:
     if cfg >= 400:  # igemmh sizes its LDS per launch (the host rejects a launch that cannot fit)
         return True
     bm, bn = tile_of(cfg)
-    ns = IGEMM3_STAGES[(cfg - 200) // 10] if cfg >= 200 else 2
-    nt = 64 * IGEMM3_WAVES.get(cfg % 10, 4) if cfg >= 200 else 256
-    return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 64 * nt <= ns * (bm + bn) * 128
+    if cfg < 200:
+        return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= 2 * (bm + bn) * 128
+    ns = IGEMM3_STAGES[(cfg - 200) // 10]
+    nt = 64 * IGEMM3_WAVES.get(cfg % 10, 4)
+    wm = IGEMM3_WM[cfg % 10]
+    # igemm3: the row-lane scratch may alias the C tile (the store pass has read it by then)
+    return (bm + 2 * wm * bn) * 4 + max(bm * (bn + 8) * 2, 64 * nt) <= ns * (bm + bn) * 128
 
 
 WGRAD_CFGS = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64), 4: (32, 64), 5: (64, 32), 6: (32, 32)}

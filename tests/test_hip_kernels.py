@@ -183,7 +183,7 @@ def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
             close(out, gx, 2e-3, "G dgrad cfg%d s%d" % (cfg, splits))
 
 
-@pytest.mark.parametrize("cfg", [200, 211, 213, 206, 218, 403, 414])
+@pytest.mark.parametrize("cfg", [200, 211, 213, 206, 216, 217, 218, 403, 414])
 def test_igemm_fused_bn_backward_stats(cfg):
     """Data-gradient GEMM with the BN-backward statistics fused into its store pass (epilogue.h
     vec_store_bnb): stored dL/da == the plain GEMM's, partials sum to (sum g, sum g * xhat) with
@@ -926,3 +926,4 @@ def test_head_bwd_row_splits(R, groups, RS):
         pg = part[gi * ppg:(gi + 1) * ppg].reshape(RS, S, 2, C).sum(0)
         close(pg[:, 0], gg.sum(0), 1e-4, "sum g")
         close(pg[:, 1], (gg * xh).sum(0), 1e-4, "sum g xhat")
+
