@@ -10,6 +10,9 @@ graph launches:
                  D calls) -> fused 3-loss BCE
   progA[a_fwd:]  the g_loss chain back through D(fake) (pre-update D weights) and G's
                  backward (G grads final)                          -- the "G chain"
+  progW          G's weight gradients, each tied to the progA position that produces its operand;
+                 under "fused" they run on the D chain's stream after that chain, beside G's
+                 data-gradient chain
   progB          D's backward of d_loss, both halves (D grads final) -- the "D chain";
                  runs on its own stream concurrently with the G chain (disjoint buffers,
                  both only READ D's forward state and weights)
@@ -41,7 +44,7 @@ from __future__ import annotations
 import math
 import os
 from collections import OrderedDict
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -259,9 +262,11 @@ class HipEngine:
         self._keep: List[torch.Tensor] = []
         self.progA = self._prog()
         self.progB = self._prog()
+        self.progW = self._prog()  # G's weight gradients (see _build_gloss_and_g_backward)
+        self._g_w: List[Tuple[int, int]] = []
         self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
         self._a_fwd = self.progA.size()  # forward done: D's d_loss backward may start from here
-        self._build_gloss_and_g_backward(self.progA)
+        self._build_gloss_and_g_backward(self.progA, self.progW)
         self._build_d_backward_dloss(self.progB)  # sets self._b_split (top layer done)
         self._build_updates()
         # D-gradient slice final after the D chain's first segment: the top conv layer (+ its BN)
@@ -655,6 +660,11 @@ class HipEngine:
                 self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
                             L.in_hw, L.in_hw, L.cin, pad, **kw)
 
+    def _w_mark(self, prog, progw, begin: int) -> None:
+        """progW[begin:] (one layer's weight gradient) needs progA up to its current end."""
+        if progw.size() > begin:
+            self._g_w.append((prog.size(), progw.size()))
+
     def _act_bwd_dbias(self, prog, name, dy, y, dx, rows, C, act, db, chain):
         """dx = dy * act'(y) and the bias gradient db = column sums of dx: one fused launch
         when the channel count has a kernel variant, else act_bwd + a column-sum pass."""
@@ -750,7 +760,11 @@ class HipEngine:
                           self.cfg.lrelu_leak, 0)
 
     # ---- g_loss back through D(fake) (fake rows only, no D grads) and G backward
-    def _build_gloss_and_g_backward(self, prog):
+    def _build_gloss_and_g_backward(self, prog, progw):
+        """progA: g_loss back through D(fake), then G's data-gradient chain; progw: G's weight
+        gradients, each recorded with the progA position it needs (self._g_w). Under the fused
+        schedule they run on the D chain's stream once that chain is done, beside the G
+        data-gradient chain (which then has nothing else on its critical path)."""
         cfg, B = self.cfg, self.B
         Pd, Pg, gG = self.model.d, self.model.g, self.grad_g
         last = self.dl[-1]
@@ -820,17 +834,21 @@ class HipEngine:
             grid = H.nconv_grid(prog, B, Lg.in_hw, Lg.in_hw)
             part = self._stats_buf(bn_prev + ".bwd", grid, Lg.cin)
             st = self.bn[bn_prev]
+            w0 = progw.size()
+            progw.nwgrad(Lg.name + ".nwgrad", _p(self.img_g), B, Lg.out_hw, Lg.out_hw, Lg.cout, _p(a_prev), Lg.in_hw,
+                         Lg.in_hw, padL, _p(gG[Lg.name + "/w"]), 0)
+            self._w_mark(prog, progw, w0)
             prog.nconv(Lg.name + ".dgrad", _p(self.img_g), _p(wL), 0, _p(da_prev), B, Lg.out_hw, Lg.out_hw, Lg.cout,
                        Lg.in_hw, Lg.in_hw, padL, padL, NONE, 0.0, grid, _p(x_prev), _p(a_prev), _p(st["mean"]),
                        _p(st["rstd"]), RELU, cfg.lrelu_leak, _p(part), 0)
             fused_next = (part, grid, {})
-            prog.nwgrad(Lg.name + ".nwgrad", _p(self.img_g), B, Lg.out_hw, Lg.out_hw, Lg.cout, _p(a_prev), Lg.in_hw,
-                        Lg.in_hw, padL, _p(gG[Lg.name + "/w"]), 0)
         elif Lg.cout % 8 != 0:
             prog.im2col_s2("g_out.im2col", _p(self.img_g), _p(self.g_last_col), B, Lg.out_hw, Lg.out_hw, Lg.cout,
                            Lg.in_hw, Lg.in_hw, padL, padL, self.kp_g, 0)
-            self._wgrad(prog, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
+            w0 = progw.size()
+            self._wgrad(progw, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
                         0, gG[Lg.name + "/w"])
+            self._w_mark(prog, progw, w0)
             r = self._dgrad_bnb(prog, 2, B, 1, 1, self.kp_g, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev,
                                 a_prev, 1, RELU, fin=(Pg, gG, self.coef[bn_prev]))
             fused_next = None
@@ -840,8 +858,10 @@ class HipEngine:
             self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, wL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
                         Lg.in_hw, Lg.cin, 0, bkn=True, kb_valid=25 * Lg.cout, **kw)
         else:
-            self._wgrad(prog, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
+            w0 = progw.size()
+            self._wgrad(progw, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
                         Lg.cin, padL, gG[Lg.name + "/w"])
+            self._w_mark(prog, progw, w0)
             r = self._dgrad_bnb(prog, 0, B, Lg.out_hw, Lg.out_hw, Lg.cout, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev,
                                 x_prev, a_prev, 1, RELU, fin=(Pg, gG, self.coef[bn_prev]))
             fused_next = None
@@ -861,8 +881,10 @@ class HipEngine:
             xsrc = self.g_x[self.gl[j - 1].name] if j > 0 else self.g_h0_pre
             bsrc = self.gl[j - 1].bn if j > 0 else "g_bn0"
             pad = same_pads(L.out_hw)[0]
-            self._wgrad(prog, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
+            w0 = progw.size()
+            self._wgrad(progw, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
                         gG[L.name + "/w"])
+            self._w_mark(prog, progw, w0)
             r = self._dgrad_bnb(prog, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc,
                                 src, 1, RELU, fin=(Pg, gG, self.coef[bsrc]))
             fused_next = None
@@ -925,6 +947,7 @@ class HipEngine:
 
     # ------------------------------------------------------------------ execution
     MAIN, ALT = 0, 1
+    G_WGRAD_ON_D_STREAM = True
 
     def _schedule(self) -> str:
         req = self._sched_req
@@ -935,16 +958,16 @@ class HipEngine:
     def _segments(self):
         """The step as a list of (name, [(program, begin, end)], stream) segments."""
         sch = self._schedule()
-        A, B, C = self.progA, self.progB, self.progC
+        A, B, C, W = self.progA, self.progB, self.progC, self.progW
         M = self.MAIN
         if sch == "fused":
-            return [("step", [(A, 0, -1), (B, 0, -1), (C, 0, -1)], M)]
+            return [("step", [(A, 0, -1), (B, 0, -1), (W, 0, -1), (C, 0, -1)], M)]
         if sch == "serial":
-            return [("fwd+G_bwd", [(A, 0, -1)], M), ("D_bwd_top", [(B, 0, self._b_split)], M),
+            return [("fwd+G_bwd", [(A, 0, -1), (W, 0, -1)], M), ("D_bwd_top", [(B, 0, self._b_split)], M),
                     ("D_bwd_rest", [(B, self._b_split, -1)], M), ("adam_G", [(C, 0, self._c_split)], M),
                     ("adam_D", [(C, self._c_split, -1)], M)]
         return [("fwd", [(A, 0, self._a_fwd)], M), ("D_bwd_top", [(B, 0, self._b_split)], self.ALT),
-                ("G_chain", [(A, self._a_fwd, -1)], M), ("D_bwd_rest", [(B, self._b_split, -1)], self.ALT),
+                ("G_chain", [(A, self._a_fwd, -1), (W, 0, -1)], M), ("D_bwd_rest", [(B, self._b_split, -1)], self.ALT),
                 ("adam_G", [(C, 0, self._c_split)], M), ("adam_D", [(C, self._c_split, -1)], M)]
 
     def enable_timing(self) -> None:
@@ -986,7 +1009,25 @@ class HipEngine:
         ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
         ex.wait(ex.alt[0], cs)
         ex.run(self.progB, ex.alt)
-        ex.run(self.progA, [cs, ex.side], self._a_fwd, -1)
+        # the G chain: data gradients on cs; each G weight gradient on the D chain's stream after
+        # that chain, once cs has produced its operand (a mark after that progA position)
+        if not self.G_WGRAD_ON_D_STREAM:  # A/B: every G gradient on cs
+            ex.run(self.progA, [cs, ex.side], self._a_fwd, -1)
+            ex.run(self.progW, [cs, ex.side])
+            ex.wait(cs, ex.alt[0])
+            ex.run(self.progC, [cs, ex.side])
+            return
+        pos, marks = self._a_fwd, []
+        for a_end, _ in self._g_w:
+            ex.run(self.progA, [cs, ex.side], pos, a_end)
+            marks.append(ex.mark(cs))
+            pos = a_end
+        ex.run(self.progA, [cs, ex.side], pos, -1)
+        w = 0
+        for m, (_, w_end) in zip(marks, self._g_w):
+            ex.wait_mark(ex.alt[0], m)
+            ex.run(self.progW, ex.alt, w, w_end)
+            w = w_end
         ex.wait(cs, ex.alt[0])
         ex.run(self.progC, [cs, ex.side])
 
@@ -1279,13 +1320,13 @@ class HipEngine:
 
     def op_names(self) -> List[str]:
         out = []
-        for p in (self.progA, self.progB, self.progC):
+        for p in (self.progA, self.progB, self.progW, self.progC):
             out += [p.name(i) for i in range(p.size())]
         return out
 
     def kernel_count(self) -> int:
         """Kernel launches per training step (events excluded)."""
         n = 0
-        for p in (self.progA, self.progB, self.progC):
+        for p in (self.progA, self.progB, self.progW, self.progC):
             n += sum(1 for i in range(p.size()) if p.op_info(i)[2] == self.ext.OP_LAUNCH)
         return n

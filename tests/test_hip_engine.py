@@ -85,7 +85,8 @@ def test_engine_stagewise(size, c_dim, B, dtype):
     real = (torch.rand(B, size, size, c_dim, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     eng.set_batch(real)
     st = [torch.cuda.current_stream(), torch.cuda.Stream()]  # main + side stream slots
-    H.run(eng.progA, st)          # forward, g_loss chain through D(fake), G backward (G grads final)
+    H.run(eng.progA, st)          # forward, g_loss chain through D(fake), G data gradients
+    H.run(eng.progW, st)          # G weight gradients (G grads final)
     torch.cuda.synchronize()
     Pd, Pg, gD, gG = eng.model.d, eng.model.g, eng.grad_d, eng.grad_g
     rep = {}

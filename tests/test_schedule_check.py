@@ -72,7 +72,7 @@ def test_checker_finds_a_missing_join():
 def test_op_accesses_are_recorded():
     eng = _dry()
     names = set()
-    for p in (eng.progA, eng.progB, eng.progC):
+    for p in (eng.progA, eng.progB, eng.progW, eng.progC):
         for i in range(p.size()):
             name, slot, kind, ev, acc = p.op_info(i)
             names.add(name)
@@ -80,6 +80,6 @@ def test_op_accesses_are_recorded():
                 assert acc, "op %s records no accesses" % name
                 assert all(n > 0 for _, n, _ in acc)
     assert ("adam_gd" in names or {"adam_g", "adam_d"} <= names) and any(n.startswith("d_head") and n.endswith("+loss") for n in names)
-    launches = sum(p.op_info(i)[2] == eng.ext.OP_LAUNCH for p in (eng.progA, eng.progB, eng.progC)
+    launches = sum(p.op_info(i)[2] == eng.ext.OP_LAUNCH for p in (eng.progA, eng.progB, eng.progW, eng.progC)
                    for i in range(p.size()))
     assert eng.kernel_count() == launches
