@@ -99,21 +99,20 @@ __device__ __forceinline__ float philox_uniform_at(size_t idx, uint64_t seed, ui
 // gen_step != nullptr: z is not read but generated here -- z ~ U(-1,1) by Philox keyed by
 // (gen_seed, *gen_step), bit-identical to philox_uniform_kernel -- and written to z by the
 // column-0 blocks (the backward and the summaries read it): one launch less per step.
-template <int RB, int KU>  // KU % 4 == 0
+template <int RB>
 __global__ __launch_bounds__(256) void linear_fwd_kernel(float* __restrict__ z, const float* __restrict__ W,
                                                          const float* __restrict__ bias, elem_t* __restrict__ out,
                                                          int B, int K, int N, float* __restrict__ stats, int C,
                                                          const unsigned long long* __restrict__ gen_step,
                                                          uint64_t gen_seed) {
-  extern __shared__ __attribute__((aligned(16))) float zs[];  // [RB][Kp], Kp = K rounded up to KU (zero pad)
+  extern __shared__ __attribute__((aligned(16))) float zs[];  // [RB][K]
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * RB;
-  const int Kp = (K + KU - 1) / KU * KU;
   const uint64_t st = gen_step ? gen_step[0] : 0ull;
-  for (int i = threadIdx.x; i < RB * Kp; i += 256) {
-    const int r = i / Kp, k = i - r * Kp;
+  for (int i = threadIdx.x; i < RB * K; i += 256) {
+    const int r = i / K, k = i - r * K;
     float v = 0.f;
-    if (r0 + r < B && k < K) {
+    if (r0 + r < B) {
       const size_t idx = (size_t)(r0 + r) * K + k;
       if (gen_step) {
         v = philox_uniform_at(idx, gen_seed, st, 0, -1.f, 1.f);
@@ -129,21 +128,29 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(float* __restrict__ z, 
   float acc[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) acc[r] = 0.f;
-  // KU weight loads in flight per thread (the loop is load-latency bound: 20 per batch took 5
-  // dependent round trips for K = 100); z from LDS as float4 (broadcast); the pad rows of zs are
-  // zero, so the clamped weight loads past K contribute nothing
-  for (int k = 0; k < Kp; k += KU) {
-    float w[KU];
+  // z is read from LDS as float4 (4 k per ds_read_b128, broadcast): with scalar reads the loop
+  // was LDS-instruction bound (8 rows x 100 k reads per thread)
+  constexpr int KU = 20;
+  int k = 0;
+  if ((K & 3) == 0) {
+    for (; k + KU <= K; k += KU) {
+      float w[KU];
 #pragma unroll
-    for (int u = 0; u < KU; ++u) w[u] = W[(size_t)min(k + u, K - 1) * N + n];
+      for (int u = 0; u < KU; ++u) w[u] = W[(size_t)(k + u) * N + n];
 #pragma unroll
-    for (int r = 0; r < RB; ++r)
+      for (int r = 0; r < RB; ++r)
 #pragma unroll
-      for (int u4 = 0; u4 < KU / 4; ++u4) {
-        const f32x4 zv = *reinterpret_cast<const f32x4*>(zs + r * Kp + k + 4 * u4);
+        for (int u4 = 0; u4 < KU / 4; ++u4) {
+          const f32x4 zv = *reinterpret_cast<const f32x4*>(zs + r * K + k + 4 * u4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[r] += zv[e] * w[4 * u4 + e];
-      }
+          for (int e = 0; e < 4; ++e) acc[r] += zv[e] * w[4 * u4 + e];
+        }
+    }
+  }
+  for (; k < K; ++k) {
+    const float w = W[(size_t)k * N + n];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[r] += zs[r * K + k] * w;
   }
   const float b = bias ? bias[n] : 0.f;
   float s = 0.f, s2 = 0.f;
@@ -183,12 +190,12 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
 #pragma unroll
   for (int k = 0; k < KC; ++k) acc[k] = 0.f;
   int b = 0;
-  for (; b + 32 <= B; b += 32) {  // 32 dh loads in flight (load-latency bound), z rows as float4 LDS reads
-    float g[32];
+  for (; b + 8 <= B; b += 8) {  // 8 dh loads in flight, z rows as float4 LDS reads
+    float g[8];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) g[u] = (float)dh[(size_t)(b + u) * N + n];
+    for (int u = 0; u < 8; ++u) g[u] = (float)dh[(size_t)(b + u) * N + n];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
+    for (int u = 0; u < 8; ++u) {
       sb += g[u];
 #pragma unroll
       for (int k4 = 0; k4 < KC / 4; ++k4) {
@@ -811,13 +818,10 @@ extern "C" int DCG_API(dcg_linear_fwd)(float* z, const float* W, const float* b,
                               float* stats, int C, const unsigned long long* gen_step, uint64_t gen_seed,
                               hipStream_t s) {
   if (stats && (C <= 0 || N % C)) return -2;
-  constexpr int RB = 8;   // (N/256) x (B/8) = 512 blocks for the 64x64 model at B=128
-  constexpr int KU = 52;  // z_dim 100 -> two batches of weight loads
-  const int Kp = (K + KU - 1) / KU * KU;
-  if ((size_t)RB * Kp * sizeof(float) > 65536) return -3;
+  constexpr int RB = 8;  // (N/256) x (B/8) = 512 blocks for the 64x64 model at B=128
   dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
-  hipLaunchKernelGGL((linear_fwd_kernel<RB, KU>), grid, dim3(256), RB * Kp * sizeof(float), s, z, W, b, out, B, K,
-                     N, stats, C, gen_step, gen_seed);
+  hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N,
+                     stats, C, gen_step, gen_seed);
   return (int)hipGetLastError();
 }
 

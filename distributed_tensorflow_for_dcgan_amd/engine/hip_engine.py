@@ -619,46 +619,58 @@ class HipEngine:
             else:  # live bias (no BN after it): db = sum over rows of dx, fused with the act backward
                 self._act_bwd_dbias(prog, L.name + ".act_bwd", da, a, dx, rows, L.cout, LRELU, gD[L.name + "/biases"],
                                     "d")
-            # weight gradient
-            src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
-            pad = same_pads(L.in_hw)[0]
-            if i == 0 and self._d0_direct() and prog.nwgrad_ok(L.in_hw, L.in_hw, L.out_hw, L.out_hw):
-                # image window staged per workgroup, no column matrix (narrow2.hip nwgrad)
-                prog.nwgrad(L.name + ".nwgrad", _p(self.d_in), B2, L.in_hw, L.in_hw, L.cin, _p(dx), L.out_hw,
-                            L.out_hw, pad, _p(gD[L.name + "/w"]), 0)
-            elif i == 0 and L.cin % 8 != 0:
-                if self._d0_direct():  # the forward ran without a column matrix: build it here
-                    prog.im2col_s2("d0.im2col", _p(self.d_in), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin,
-                                   L.out_hw, L.out_hw, pad, pad, self.kp_d0, 0)
-                self._wgrad(prog, L.name, 2, self.d0_col, 1, 1, self.kp_d0, dx, B2 * L.out_hw ** 2, 1, 1, L.cout, 0,
-                            gD[L.name + "/w"])
-            else:
-                self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
-                            gD[L.name + "/w"])
-            if i == len(self.dl) - 1:
-                # head + top layer gradients final: DDP splits the segment here so their
-                # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
-                self._b_split = prog.size()
-            # data gradient into the previous activation (not needed below layer 0)
-            fused_next = None
-            if i > 0:
-                nat = self.wbf_d[L.name + "/w"]
-                P_ = self.dl[i - 1]
-                kw = {}
-                out = self.d_da[P_.name]
-                if P_.bn:
-                    r = self._dgrad_bnb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
-                                        P_.bn, self.d_x[P_.name], self.d_a[P_.name], 2, LRELU,
-                                        fin=(Pd, gD, self.coef[P_.bn]))
-                    if r is not None:
-                        kw, fused_next = r[0], (r[1], r[2], r[3])
+
+            def emit_wgrad(i=i, L=L, dx=dx):
+                src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
+                pad = same_pads(L.in_hw)[0]
+                if i == 0 and self._d0_direct() and prog.nwgrad_ok(L.in_hw, L.in_hw, L.out_hw, L.out_hw):
+                    # image window staged per workgroup, no column matrix (narrow2.hip nwgrad)
+                    prog.nwgrad(L.name + ".nwgrad", _p(self.d_in), B2, L.in_hw, L.in_hw, L.cin, _p(dx), L.out_hw,
+                                L.out_hw, pad, _p(gD[L.name + "/w"]), 0)
+                elif i == 0 and L.cin % 8 != 0:
+                    if self._d0_direct():  # the forward ran without a column matrix: build it here
+                        prog.im2col_s2("d0.im2col", _p(self.d_in), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin,
+                                       L.out_hw, L.out_hw, pad, pad, self.kp_d0, 0)
+                    self._wgrad(prog, L.name, 2, self.d0_col, 1, 1, self.kp_d0, dx, B2 * L.out_hw ** 2, 1, 1, L.cout, 0,
+                                gD[L.name + "/w"])
                 else:
-                    r = self._dgrad_actb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
-                                         P_.name, self.d_a[P_.name], LRELU, db=gD[P_.name + "/biases"])
-                    if r is not None:
-                        kw, fused_next, out = r[0], (r[1], r[2], r[3]), self.d_dx[P_.name]
-                self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
-                            L.in_hw, L.in_hw, L.cin, pad, **kw)
+                    self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
+                                gD[L.name + "/w"])
+                if i == len(self.dl) - 1:
+                    # head + top layer gradients final: DDP splits the segment here so their
+                    # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
+                    self._b_split = prog.size()
+
+            def emit_dgrad(i=i, L=L, dx=dx):
+                fused = None
+                pad = same_pads(L.in_hw)[0]
+                if i > 0:
+                    nat = self.wbf_d[L.name + "/w"]
+                    P_ = self.dl[i - 1]
+                    kw = {}
+                    out = self.d_da[P_.name]
+                    if P_.bn:
+                        r = self._dgrad_bnb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                                            P_.bn, self.d_x[P_.name], self.d_a[P_.name], 2, LRELU,
+                                            fin=(Pd, gD, self.coef[P_.bn]))
+                        if r is not None:
+                            kw, fused = r[0], (r[1], r[2], r[3])
+                    else:
+                        r = self._dgrad_actb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
+                                             P_.name, self.d_a[P_.name], LRELU, db=gD[P_.name + "/biases"])
+                        if r is not None:
+                            kw, fused, out = r[0], (r[1], r[2], r[3]), self.d_dx[P_.name]
+                    self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
+                                L.in_hw, L.in_hw, L.cin, pad, **kw)
+                return fused
+
+            # (below the top layer, the data gradient first: it leads the chain, the weight gradient is a leaf)
+            if self.D_DGRAD_FIRST and i < len(self.dl) - 1:
+                fused_next = emit_dgrad()
+                emit_wgrad()
+            else:
+                emit_wgrad()
+                fused_next = emit_dgrad()
 
     def _w_mark(self, prog, progw, begin: int) -> None:
         """progW[begin:] (one layer's weight gradient) needs progA up to its current end."""
@@ -948,6 +960,7 @@ class HipEngine:
     # ------------------------------------------------------------------ execution
     MAIN, ALT = 0, 1
     G_WGRAD_ON_D_STREAM = True
+    D_DGRAD_FIRST = False  # A/B switch (profiles/r2/ab_d_dgrad_first_r2.txt)
 
     def _schedule(self) -> str:
         req = self._sched_req
