@@ -283,16 +283,37 @@ class HipEngine:
     def _build_updates(self):
         """progC for the current schedule. The one-launch Adam over BOTH models is only used
         where nothing else can be touching D's gradients or weights any more ("fused": after
-        the join of the two backward chains); every other schedule runs Adam(G) (segment
-        "adam_G", first _c_split ops) and Adam(D) + the step counter (segment "adam_D") apart."""
+        the join of the two backward chains). "serial" runs Adam(G) first (progC[:_c_split],
+        overlapping D's all-reduces), then Adam(D) + the step counter; "concurrent" -- whose D
+        chain ends first -- runs Adam(D) first (overlapping G's all-reduce), then Adam(G) + the
+        step counter. fp16: one overflow check gates both, everything in the second part."""
         self.progC = self._prog()
-        if self._schedule() == "fused" and self.dt == 0:
+        sch = self._schedule()
+        if sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
             self._c_split = self.progC.size()
+        elif sch == "concurrent" and not self.f16:
+            self._build_update_d_first(self.progC)
         else:
             self._build_update(self.progC, first=True)
             self._c_split = self.progC.size()
             self._build_update(self.progC, first=False)
+
+    def _build_update_d_first(self, prog):
+        """Adam(D) (progC[:_c_split]), then Adam(G) + beta powers / global step: the step counter
+        update must follow both Adams (each reads its model's beta powers)."""
+        gs = 1.0 / self.world
+        od, og = self.opt_d, self.opt_g
+        ls = _p(self.loss_scale)
+        mg = 0 if self.f32 else _p(self.wbf_g.flat)
+        md = 0 if self.f32 else _p(self.wbf_d.flat)
+        prog.adam_bf("adam_d", _p(self.model.d.flat), md, _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
+                     _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0, ls)
+        self._c_split = prog.size()
+        prog.adam_bf("adam_g", _p(self.model.g.flat), mg, _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
+                     _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0, ls)
+        prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
+                      _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
 
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
@@ -981,7 +1002,7 @@ class HipEngine:
                     ("adam_D", [(C, self._c_split, -1)], M)]
         return [("fwd", [(A, 0, self._a_fwd)], M), ("D_bwd_top", [(B, 0, self._b_split)], self.ALT),
                 ("G_chain", [(A, self._a_fwd, -1), (W, 0, -1)], M), ("D_bwd_rest", [(B, self._b_split, -1)], self.ALT),
-                ("adam_G", [(C, 0, self._c_split)], M), ("adam_D", [(C, self._c_split, -1)], M)]
+                ("adam_D", [(C, 0, self._c_split)], M), ("adam_G", [(C, self._c_split, -1)], M)]
 
     def enable_timing(self) -> None:
         """Per-phase GPU timers: the step runs as segments with events between
@@ -1088,16 +1109,20 @@ class HipEngine:
             self._ar_launch(ex, "dtop", alt)
             self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward -> grad_g final
             self._tick(3, cs)
-            self._ar_launch(ex, "g", cs)
             self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
-            self._ar_join(ex, cs)              # cs waits for the dtop + G collectives
-            self._seg(ex, 4, cs)               # Adam G -> G mirror (overlaps the last D all-reduce)
-            self._tick(5, cs)
+            # the D chain ends first: D's last bucket goes on the wire before G's, and Adam(D)
+            # runs while G's all-reduce is in flight
             self._ar_launch(ex, "drest", alt)
-            self._ar_join(ex, cs)
+            d_done = ex.mark(ex.comm) if self.world > 1 else None
+            self._ar_launch(ex, "g", cs)
+            if d_done is not None:
+                ex.wait_mark(cs, d_done)       # dtop + drest collectives
             ex.wait(cs, alt)                   # (W = 1, timed: the D chain itself)
-            self._seg(ex, 5, cs)               # Adam D, step counter, D mirror
+            self._seg(ex, 4, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
+            self._tick(5, cs)
+            self._ar_join(ex, cs)              # G's collective
+            self._seg(ex, 5, cs)               # Adam G, step counter, G mirror
             self._tick(6, cs)
             return
         self._tick(0, cs)

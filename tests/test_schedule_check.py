@@ -39,14 +39,27 @@ def _dry(world=1, timing=False):
 
 def test_checker_finds_the_round1_adam_race():
     """Round 1: at W=1 with --timing the concurrent schedule kept the fused two-model Adam in
-    its "adam_G" segment, which runs before the main stream joins the D chain."""
+    its first update segment, which ran before the main stream joined the D chain."""
     eng = _dry(timing=True)
     assert eng._schedule() == "concurrent"
     hz, _ = SC.check_engine(eng)
     assert hz == []
     eng.progC = eng._prog()
     eng._build_update_fused(eng.progC)   # the round-1 program
-    eng._c_split = eng.progC.size()      # ... all of it in "adam_G"
+    eng._c_split = eng.progC.size()      # ... all of it in the first update segment
+
+    def round1_order(ex):                # ... issued before the cs <- D-chain join
+        cs, alt = ex.main(), ex.alt[0]
+        eng._seg(ex, 0, cs)
+        ex.wait(alt, cs)
+        eng._seg(ex, 1, alt)
+        eng._seg(ex, 2, cs)
+        eng._seg(ex, 3, alt)
+        eng._seg(ex, 4, cs)
+        ex.wait(cs, alt)
+        eng._seg(ex, 5, cs)
+
+    eng._run_step = round1_order
     hz, _ = SC.check_engine(eng)
     assert hz, "the checker missed the Adam(D) / D-backward race"
     txt = "\n".join(map(str, hz))
