@@ -9,7 +9,8 @@ def main():
     flag, value = sys.argv[1], int(sys.argv[2])
     if not hasattr(HipEngine, flag):
         raise SystemExit("HipEngine has no switch %s" % flag)
-    setattr(HipEngine, flag, type(getattr(HipEngine, flag))(value))
+    cur = getattr(HipEngine, flag)
+    setattr(HipEngine, flag, bool(value) if cur is None or isinstance(cur, bool) else type(cur)(value))
     sys.argv = ["bench.py"] + sys.argv[3:]
     import bench
     bench.main()

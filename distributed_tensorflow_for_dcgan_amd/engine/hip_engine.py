@@ -980,7 +980,16 @@ class HipEngine:
 
     # ------------------------------------------------------------------ execution
     MAIN, ALT = 0, 1
-    G_WGRAD_ON_D_STREAM = True
+    # G's weight gradients behind the D chain (fused schedule): None = by image size. Measured
+    # (profiles/r2/ab_g_wgrad_after_d_chain_r2.txt): 64x64 1.105 vs 1.13 ms, 28x28 even, 128x128
+    # 5.84 vs 5.70 ms, 256x256 106.2 vs 104.6 ms -- at the larger sizes the D chain (2B rows of
+    # the bigger images) is the longer one already
+    G_WGRAD_ON_D_STREAM: Optional[bool] = None
+
+    def _g_wgrad_on_d_stream(self) -> bool:
+        if self.G_WGRAD_ON_D_STREAM is not None:
+            return bool(self.G_WGRAD_ON_D_STREAM)
+        return self.cfg.output_size <= 64
     D_DGRAD_FIRST = False  # A/B switch (profiles/r2/ab_d_dgrad_first_r2.txt)
 
     def _schedule(self) -> str:
@@ -1045,7 +1054,7 @@ class HipEngine:
         ex.run(self.progB, ex.alt)
         # the G chain: data gradients on cs; each G weight gradient on the D chain's stream after
         # that chain, once cs has produced its operand (a mark after that progA position)
-        if not self.G_WGRAD_ON_D_STREAM:  # A/B: every G gradient on cs
+        if not self._g_wgrad_on_d_stream():  # every G gradient on cs
             ex.run(self.progA, [cs, ex.side], self._a_fwd, -1)
             ex.run(self.progW, [cs, ex.side])
             ex.wait(cs, ex.alt[0])
