@@ -609,13 +609,19 @@ class Program {
                                  P<float>(coef), s);
     }, acc.v);
   }
+  // fscale / fshift (optional): the forward BN coefficients -- act' from x instead of reading y
   int bn_bwd_apply(std::string name, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t coef, uintptr_t dx, int R,
-                   int C, int rows_per_group, int act, float leak, int stream) {
+                   int C, int rows_per_group, int act, float leak, int stream, uintptr_t fscale, uintptr_t fshift) {
     const size_t t = (size_t)R * C * es_, gc = (size_t)((R + rows_per_group - 1) / rows_per_group) * C * 4;
+    AccList acc;
+    acc.r(dy, t).r(x, t).r(coef, 3 * gc).w(dx, t);
+    if (fscale) acc.r(fscale, gc).r(fshift, gc);
+    else acc.r(y, t);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_bwd_apply)(P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x), P<const float>(coef),
-                              P<elem_t>(dx), R, C, rows_per_group, act, leak, s);
-    }, AccList().r(dy, t).r(y, t).r(x, t).r(coef, 3 * gc).w(dx, t).v);
+                              P<elem_t>(dx), R, C, rows_per_group, act, leak, P<const float>(fscale),
+                              P<const float>(fshift), s);
+    }, acc.v);
   }
   int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
     return add(name, stream, [=](hipStream_t s) {
@@ -1091,7 +1097,9 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("stream"), py::arg("debias_ptr") = 0)
       .def("bn_apply_act", &Program::bn_apply_act)
       .def("bn_bwd_finalize", &Program::bn_bwd_finalize)
-      .def("bn_bwd_apply", &Program::bn_bwd_apply)
+      .def("bn_bwd_apply", &Program::bn_bwd_apply, py::arg("name"), py::arg("dy"), py::arg("y"), py::arg("x"),
+           py::arg("coef"), py::arg("dx"), py::arg("R"), py::arg("C"), py::arg("rows_per_group"), py::arg("act"),
+           py::arg("leak"), py::arg("stream"), py::arg("fscale") = 0, py::arg("fshift") = 0)
       .def("act_bwd", &Program::act_bwd)
       .def("sum_partials", &Program::sum_partials)
       .def("act_bwd_dbias", &Program::act_bwd_dbias)

@@ -789,8 +789,14 @@ class HipEngine:
         if not done:
             prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg),
                                  _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
+        # act' from the sign of the forward's pre-activation x * scale + shift (no read of y)
+        fsc, fsh = st["scale"], st["shift"]
+        if row_offset_groups is not None:
+            fsc = fsc[row_offset_groups:row_offset_groups + 1]
+            fsh = fsh[row_offset_groups:row_offset_groups + 1]
+        recompute = act in (RELU, LRELU) and self.BWD_ACT_FROM_X
         prog.bn_bwd_apply(name + ".bwd_apply", _p(dy), _p(y), _p(x), _p(coef), _p(dx), rows, C, rpg, act,
-                          self.cfg.lrelu_leak, 0)
+                          self.cfg.lrelu_leak, 0, _p(fsc) if recompute else 0, _p(fsh) if recompute else 0)
 
     # ---- g_loss back through D(fake) (fake rows only, no D grads) and G backward
     def _build_gloss_and_g_backward(self, prog, progw):
@@ -985,6 +991,7 @@ class HipEngine:
     # 5.84 vs 5.70 ms, 256x256 106.2 vs 104.6 ms -- at the larger sizes the D chain (2B rows of
     # the bigger images) is the longer one already
     G_WGRAD_ON_D_STREAM: Optional[bool] = None
+    BWD_ACT_FROM_X = False  # act' from x and the forward coefficients: measured slower, ab_bwd_act_from_x_r2.txt
 
     def _g_wgrad_on_d_stream(self) -> bool:
         if self.G_WGRAD_ON_D_STREAM is not None:

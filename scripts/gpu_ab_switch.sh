@@ -2,7 +2,7 @@
 # A/B of one HipEngine switch (see the echo lines): 1 vs 0, alternating
 mkdir -p gpurun_out
 FLAG=${1:?usage: gpu_ab_switch.sh HipEngine_switch}
-timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread -k "engine or ddp or trainer or linear" \
+timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread -k "${2:-engine or ddp or trainer or linear}" \
   > gpurun_out/gpu_quick.log 2>&1 || { tail -20 gpurun_out/gpu_quick.log; exit 1; }
 tail -1 gpurun_out/gpu_quick.log
 for i in 1 2; do

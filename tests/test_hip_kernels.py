@@ -443,6 +443,13 @@ def test_bn_forward_backward_groups():
     close(dgam, gg, 2e-2, "dgamma")
     close(dbet, gb, 2e-2, "dbeta")
     close(dx, gx, 3e-2, "dx")
+    # act' from the sign of x * scale + shift (no read of y): the same dx, bit for bit
+    dx2 = torch.empty_like(x)
+    pr = _prog()
+    pr.bn_bwd_apply("bapp2", _p(dy), 0, _p(x), _p(coef), _p(dx2), R_, C, R_ // groups, 2, 0.2, 0, _p(scale), _p(shift))
+    h.run(pr)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx)
 
 
 def test_adam_matches_tf_formula():
