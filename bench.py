@@ -35,6 +35,8 @@ def parse():
     p.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip engine)")
     p.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--force_ddp", action="store_true",
+                   help="run the data-parallel step (process group + RCCL collectives) even at N=1")
     return p.parse_args()
 
 
@@ -59,6 +61,8 @@ def main():
               else torch.device("cpu"))
     if device.type == "cuda":
         torch.cuda.set_device(device)
+    if args.force_ddp:
+        os.environ["DCGAN_FORCE_DDP"] = "1"
     pg = D.init_distributed(world, rank, device)
     cfg = DCGANConfig(output_size=args.output_size, c_dim=args.c_dim)
     eng = build_engine(cfg, args.batch_size, device, engine=args.engine, dtype=args.dtype, seed=args.seed,

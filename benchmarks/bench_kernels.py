@@ -51,6 +51,7 @@ def shapes(cfg: DCGANConfig, B: int):
 
 
 V1 = False  # --v1: also time the first-generation igemm.hip tiles
+IG4 = True  # --no-ig4: leave out igemm4.hip
 
 
 def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
@@ -75,6 +76,12 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
             if H.IGEMMH_TILES[c % 10][1] > N:
                 continue
             out.append((c, 1))
+    if mode in (0, 1) and IG4:  # igemm4: halo window + loader waves (geometry checked per shape)
+        pad = same_pads(Hout)[0] if mode == 1 else same_pads(2 * Hout)[0]
+        for c in range(500, 520):
+            if c % 10 in H.IGEMM4_TILES and H.IGEMM4_TILES[c % 10][1] <= N and \
+                    H.igemm4_lds(c, mode, Bn, Kc, Hout, Wout, N, pad, pad) is not None:
+                out.append((c, 1))
     for c in range(200, 240):
         if c % 10 not in H.IGEMM3_TILES or H.igemm3_lds(c) > 160 * 1024:
             continue
@@ -108,12 +115,14 @@ def main():
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--only", default="")
     ap.add_argument("--v1", action="store_true", help="also time igemm.hip (v1) tiles")
+    ap.add_argument("--no-ig4", action="store_true", help="leave out igemm4.hip tiles")
     ap.add_argument("--out", default="", help="also write this run's table (JSON) here")
     ap.add_argument("--top", type=int, default=6, help="candidates listed per shape")
     ap.add_argument("--cfgs", default="", help="comma-separated cfg prefix filter, e.g. 4,21")
     a = ap.parse_args()
-    global V1
+    global V1, IG4
     V1 = a.v1
+    IG4 = not a.no_ig4
     cfg = DCGANConfig(output_size=a.size)
     ext = H.ext()
     dev = torch.device("cuda", 0)
@@ -141,7 +150,7 @@ def main():
             p = ext.Program()
             p.igemm_ex(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad,
                        pad, c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn if c >= 200 else 0,
-                       kb if 200 <= c < 400 else -1, sp)
+                       kb if 200 <= c < 400 else -1, sp)  # noqa
             progs[(c, sp)] = p
         times = {c: [] for c in cands}
         s = torch.cuda.current_stream()

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "hip/kernels.h"
+#include "hip/ig4.h"
 extern "C" {
 #include "hip/narrow2.inc"
 }
@@ -178,6 +179,13 @@ class Program {
                uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
                int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0, int fin = -1) {
+    if (cfg >= 500) {
+      if (out_f32 || splits != 1 || fin >= 0 || (kb_valid >= 0 && kb_valid != Kc))
+        throw std::runtime_error("igemm4: elem_t output, no split-K, no fused finalize");
+      return igemm4_ex(name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad_y, pad_x, cfg, ldc, cofs, bias,
+                       act, leak, stats, stream, bkn, bnb_x, bnb_y, bnb_mean, bnb_rstd, bnb_rpg, bnb_act, bnb_leak,
+                       bnb_store_g);
+    }
     int bm = 0, bn = 0, ns = 0;
     const bool hh = cfg >= 400;          // igemmh.hip (halo window in LDS)
     const bool v3 = cfg >= 200 && !hh;
@@ -370,6 +378,161 @@ class Program {
     const unsigned blocks = (unsigned)(tiles * splits);
     return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); },
                acc.v);
+  }
+
+  // ------------------------------------------------------------------ igemm4 (halo window, loader waves)
+  // Geometry of csrc/hip/igemm4.hip: a tile is NI whole images or TR whole rows of one image of
+  // the (phase) output grid; every tap of every phase reads its activation fragments from the
+  // tile's input window at a constant pixel offset (tap table), stride-2 windows stored
+  // column-split by parity. Returns the LDS bytes of the launch through *shm_out when non-null
+  // (igemm4_plan, for the tile policy) without recording anything.
+  static bool igemm4_geometry(IG4Args& g, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x,
+                              int bm, int bn, int nsb, int wmc, std::string* why) {
+    auto fail = [&](const char* m) { if (why) *why = m; return false; };
+    if (mode != 0 && mode != 1) return fail("igemm4: conv (mode 0) or deconv (mode 1) only");
+    if (Kc % 64) return fail("igemm4: Kc must be a multiple of 64");
+    if (N % bn) return fail("igemm4: N must be a multiple of the tile width");
+    int Hq, Wq;
+    std::vector<int> ntap, toff, wtap, oyo, oxo;  // per phase
+    std::vector<std::vector<int>> ry, rx, wt;    // per phase per tap: input row / col relative to the grid pixel
+    if (mode == 0) {
+      Hq = Hout; Wq = Wout;
+      ry.assign(1, {}); rx.assign(1, {}); wt.assign(1, {});
+      for (int t = 0; t < 25; ++t) { ry[0].push_back(t / 5 - pad_y); rx[0].push_back(t % 5 - pad_x); wt[0].push_back(t); }
+      oyo = {0}; oxo = {0};
+    } else {
+      if (Hout % 2 || Wout % 2) return fail("igemm4: deconv needs an even output size");
+      Hq = Hout / 2; Wq = Wout / 2;
+      for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+          const int kys = (py + pad_y) & 1, kxs = (px + pad_x) & 1;
+          const int iy0 = (py + pad_y - kys) / 2, ix0 = (px + pad_x - kxs) / 2;
+          std::vector<int> a, b, c;
+          for (int ty = 0; kys + 2 * ty < 5; ++ty)
+            for (int tx = 0; kxs + 2 * tx < 5; ++tx) {
+              a.push_back(iy0 - ty); b.push_back(ix0 - tx); c.push_back((kys + 2 * ty) * 5 + kxs + 2 * tx);
+            }
+          ry.push_back(a); rx.push_back(b); wt.push_back(c);
+          oyo.push_back(py); oxo.push_back(px);
+        }
+    }
+    const int S = mode == 0 ? 2 : 1;
+    const int HW = Hq * Wq;
+    int TR, NI;
+    if (bm <= HW) {
+      if (HW % bm || bm % Wq) return fail("igemm4: tile rows must be whole grid rows dividing the image");
+      TR = bm / Wq; NI = 1;
+    } else {
+      if (bm % HW) return fail("igemm4: tile rows must be whole images");
+      TR = Hq; NI = bm / HW;
+    }
+    if (((size_t)Bn * HW) % bm) return fail("igemm4: the tile rows must divide the batch rows");
+    int miny = 1 << 20, maxy = -(1 << 20), minx = 1 << 20, maxx = -(1 << 20);
+    for (size_t p = 0; p < ry.size(); ++p)
+      for (size_t t = 0; t < ry[p].size(); ++t) {
+        miny = std::min(miny, ry[p][t]); maxy = std::max(maxy, ry[p][t]);
+        minx = std::min(minx, rx[p][t]); maxx = std::max(maxx, rx[p][t]);
+      }
+    g.S = S; g.Hq = Hq; g.Wq = Wq; g.TR = TR; g.NI = NI;
+    g.WY = S * (TR - 1) + maxy - miny + 1;
+    g.WX = S * (Wq - 1) + maxx - minx + 1;
+    if (S == 2) { g.HX = (g.WX + 1) / 2; g.WXP = 2 * g.HX; } else { g.HX = 0; g.WXP = g.WX; }
+    g.win_oy = miny; g.win_ox = minx;
+    g.nphases = (int)ry.size();
+    for (int p = 0; p < 4; ++p) { g.ntaps[p] = 0; g.oy_off[p] = 0; g.ox_off[p] = 0; }
+    for (int p = 0; p < g.nphases; ++p) {
+      g.ntaps[p] = (int)ry[p].size();
+      if (g.ntaps[p] < nsb) return fail("igemm4: a phase has fewer taps than ring stages");
+      g.oy_off[p] = oyo[p]; g.ox_off[p] = oxo[p];
+      for (int t = 0; t < g.ntaps[p]; ++t) {
+        const int wy = ry[p][t] - miny, wx = rx[p][t] - minx;
+        const int X = S == 2 ? (wx & 1) * g.HX + (wx >> 1) : wx;
+        g.tap[p][t] = (wy * g.WXP + X) | (wt[p][t] << 16);
+      }
+    }
+    g.wpix = NI * g.WY * g.WXP;
+    g.npw = (g.wpix + 7) / 8;
+    g.win_bytes = g.npw * 1024;
+    g.nch = Kc / 64;
+    g.shared_win = g.nch == 1;
+    g.ring_bytes = nsb * bn * 128;
+    const int scratch = wmc * bn * 8 + 64;
+    g.nwb = (g.nch > 1 && g.ring_bytes + 2 * g.win_bytes + scratch <= 160 * 1024) ? 2 : 1;
+    if (g.ring_bytes + g.nwb * g.win_bytes + scratch > 160 * 1024) return fail("igemm4: window + ring exceed 160 KiB of LDS");
+    int steps = 0, w = 0;
+    for (int p = 0; p < g.nphases; ++p)
+      for (int c = 0; c < g.nch; ++c, ++w) steps += g.ntaps[p] + ((w > 0 && !g.shared_win && g.nwb == 1) ? nsb - 1 : 0);
+    g.steps = steps;
+    g.fd_hw = fastdiv_make(HW); g.fd_tw = fastdiv_make(TR * Wq); g.fd_wq = fastdiv_make(Wq);
+    g.fd_wimg = fastdiv_make(g.WY * g.WXP); g.fd_wxp = fastdiv_make(g.WXP);
+    g.mtiles = (int)(((size_t)Bn * HW) / bm);
+    g.ntiles = N / bn;
+    return true;
+  }
+
+  // LDS bytes of an igemm4 launch, or -1 (with the reason) when the shape does not fit the tile
+  py::tuple igemm4_plan(int cfg, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x) {
+    int bm, bn, nsb, wmc, wnc;
+    if (dt_ == 2 || KF(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wmc, &wnc)) return py::make_tuple(-1, std::string("bad cfg"));
+    IG4Args g{};
+    std::string why;
+    if (!igemm4_geometry(g, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, &why))
+      return py::make_tuple(-1, why);
+    return py::make_tuple(g.ring_bytes + g.nwb * g.win_bytes + wmc * bn * 8 + 64, std::string("nwb=") + std::to_string(g.nwb));
+  }
+
+  int igemm4_ex(const std::string& name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win,
+                int Kc, int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int ldc, int cofs, uintptr_t bias,
+                int act, float leak, uintptr_t stats, int stream, int bkn, uintptr_t bnb_x, uintptr_t bnb_y,
+                uintptr_t bnb_mean, uintptr_t bnb_rstd, int bnb_rpg, int bnb_act, float bnb_leak, int bnb_store_g) {
+    int bm, bn, nsb, wmc, wnc;
+    if (dt_ == 2 || KF(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wmc, &wnc))
+      throw std::runtime_error("bad igemm4 cfg " + std::to_string(cfg) + " for this element type");
+    IG4Args a{};
+    std::string why;
+    if (!igemm4_geometry(a, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, &why))
+      throw std::runtime_error(why);
+    if ((mode == 0 && (Hout != (Hin + 1) / 2 || Wout != (Win + 1) / 2)) || (mode == 1 && (Hout != 2 * Hin || Wout != 2 * Win)))
+      throw std::runtime_error("igemm4: stride-2 SAME shapes only");
+    if (ldc % 4 || cofs % 4 || ldc < cofs + N) throw std::runtime_error("igemm4: 8-byte output rows");
+    a.A = P<const elem_t>(A); a.Bn = Bn; a.H = Hin; a.W = Win; a.Kc = Kc;
+    a.Bw = P<const elem_t>(Bw); a.N = N;
+    a.C = P<elem_t>(C); a.outH = Hout; a.outW = Wout; a.ldc = ldc; a.cofs = cofs; a.ostride = mode == 1 ? 2 : 1;
+    a.bias = P<const float>(bias); a.act = act; a.leak = leak; a.stats = P<float>(stats);
+    const size_t a_elems = (size_t)Bn * Hin * Win * Kc, b_elems = (size_t)25 * N * Kc;
+    if (a_elems * es_ >= OOB || b_elems * es_ >= OOB) throw std::runtime_error("igemm4 operand exceeds the buffer range");
+    a.a_bytes = (uint32_t)(a_elems * es_); a.b_bytes = (uint32_t)(b_elems * es_);
+    const size_t c_rows = (size_t)Bn * Hout * Wout;
+    AccList acc;
+    acc.r(A, a_elems * es_).r(Bw, b_elems * es_).r(bias, (size_t)N * 4)
+        .w(C, (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_)
+        .w(stats, (size_t)a.mtiles * a.nphases * 2 * N * 4);
+    if (bnb_x || bnb_store_g) {
+      const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
+      if (!stats || !bnb_y) throw std::runtime_error("igemm4 fused backward: needs stats and y");
+      if (bnb_store_g) {
+        a.bnb_x = P<const elem_t>(bnb_y); a.bnb_y = P<const elem_t>(bnb_y);
+        a.bnb_rpg = 1 << 30; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak; a.bnb_store_g = 1;
+        acc.r(bnb_y, xy_bytes);
+      } else {
+        if (bnb_rpg <= 0 || !bnb_mean || !bnb_rstd) throw std::runtime_error("igemm4 bnb: needs rows-per-group, mean, rstd");
+        if (bnb_rpg % bm || ((size_t)Bn * a.Hq * a.Wq) % bnb_rpg)
+          throw std::runtime_error("igemm4 bnb: tile rows must divide the group");
+        a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
+        a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
+        a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
+        const size_t groups = (size_t)Bn * a.Hq * a.Wq / bnb_rpg;
+        acc.r(bnb_x, xy_bytes).r(bnb_y, xy_bytes).r(bnb_mean, groups * N * 4).r(bnb_rstd, groups * N * 4);
+      }
+    }
+    if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
+    last_mtiles_ = a.mtiles;
+    last_nphases_ = a.nphases;
+    const size_t shm = (size_t)a.ring_bytes + (size_t)a.nwb * a.win_bytes + (size_t)wmc * bn * 8 + 64;
+    const unsigned blocks = (unsigned)(a.mtiles * a.ntiles);
+    return add(name, stream, [this, a, cfg, bkn, blocks, shm](hipStream_t s) {
+      return KF(dcg_igemm4_launch)(&a, cfg, bkn, blocks, shm, s);
+    }, acc.v);
   }
 
   // ------------------------------------------------------------------ fused BN finalize (finalize.h)
@@ -1086,6 +1249,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("bn_fin_fwd", &Program::bn_fin_fwd)
       .def("bn_fin_bwd", &Program::bn_fin_bwd)
       .def("bn_fin_sum", &Program::bn_fin_sum)
+      .def("igemm4_plan", &Program::igemm4_plan)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)

@@ -118,6 +118,8 @@ __device__ __forceinline__ void buf_load16_lds(__amdgpu_buffer_rsrc_t r, void* l
 
 // 32-bit LDS address space (ds_* addressing: no generic-pointer null checks)
 typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) int lds_i32;
 
 // The same 16-byte LDS-DMA as inline asm. hipcc cannot tell which LDS bytes a DMA writes, so
 // after the builtin form it waits vmcnt(0) before the next ds_read of ANY LDS address -- which

@@ -1,0 +1,580 @@
+// dcg-variants: bf16 f16
+// Implicit-GEMM convolution, version 4: input window in LDS ("halo"), loader waves, and a
+// transposed accumulator layout with a register-direct epilogue.
+//
+// Why (profiles/r3/dma_bw_r3.txt, profiles/r2/igemm3_ablations_r2.txt): igemm3's K loop is bound by
+// LDS-DMA issue. A buffer_load ... lds of 1 KiB costs its wave ~60-110 issue cycles, and a CU
+// moves at most ~75 GB/s from L2 into LDS with 4 issuing waves (~115 GB/s with 16). igemm3
+// gathers every operand byte once per tap: a 128x128 tile moves 32 KiB per 64-deep k-step for
+// 2 MFLOP, i.e. 64 FLOP per byte, below the ~75 FLOP/B the MFMA rate needs.
+//
+// Here:
+//  * A (activations): a workgroup's output tile is NI images x TR grid rows x Wq columns, so the
+//    input pixels all its taps read form a small window (halo). The window of one 64-channel
+//    chunk is staged ONCE (full 128-byte lines) and all 25 taps (conv) / 9+6+6+4 taps (the four
+//    sub-pixel phases of a deconv, run one after the other) read their fragments out of it at a
+//    constant pixel offset. Stride-2 convs store the window column-split by parity
+//    (space-to-depth), so 16 lanes reading 16 consecutive output columns read 16 consecutive
+//    LDS pixels; a 16-byte chunk XOR (bits 1..3 of the pixel) makes those reads conflict-free.
+//  * B (weights): one 64-deep k-step of BN columns per ring stage (NSB stages), as igemm3.
+//  * Loader waves: 4 extra waves (one per SIMD) issue every LDS-DMA; the compute waves only
+//    ds_read fragments and run MFMAs. One s_barrier per k-step; the loaders keep stage s+1
+//    landed at barrier s, so compute waves prefetch the next step's first fragments before it.
+//    The next chunk's window streams into the second window buffer in slices behind the B stages
+//    (nwb = 2), or -- when two windows do not fit -- after NSB-1 empty steps (nwb = 1).
+//  * Transposed MFMA: acc = mfma(weights, activations), so a lane holds 4 consecutive output
+//    channels of one pixel: bias / activation / BN statistics / BN-backward statistics and an
+//    8-byte packed store straight from registers. Per-channel sums are reduced over the 16
+//    pixel lanes with shuffles, and across the compute waves of a column in LDS by the last of
+//    them to arrive (LDS counter; in wave order: deterministic) -- no barrier, so the loader
+//    waves keep streaming while a deconv phase's epilogue runs.
+// Statistics rows: one per (m tile, phase), as igemm3 (engine-compatible).
+#include "ig4.h"
+
+namespace dcg {
+namespace ig4 {
+
+constexpr int NL = 4;  // loader waves
+
+template <int N_>
+__device__ __forceinline__ void wvm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (rounded down above 15: waiting longer is safe)
+__device__ __forceinline__ void wvm_dyn(int n) {
+  if (n >= 16) {
+    if (n >= 48) wvm<48>();
+    else if (n >= 32) wvm<32>();
+    else if (n >= 24) wvm<24>();
+    else wvm<16>();
+    return;
+  }
+  switch (n) {
+    case 15: wvm<15>(); break;
+    case 14: wvm<14>(); break;
+    case 13: wvm<13>(); break;
+    case 12: wvm<12>(); break;
+    case 11: wvm<11>(); break;
+    case 10: wvm<10>(); break;
+    case 9: wvm<9>(); break;
+    case 8: wvm<8>(); break;
+    case 7: wvm<7>(); break;
+    case 6: wvm<6>(); break;
+    case 5: wvm<5>(); break;
+    case 4: wvm<4>(); break;
+    case 3: wvm<3>(); break;
+    case 2: wvm<2>(); break;
+    case 1: wvm<1>(); break;
+    default: wvm<0>(); break;
+  }
+}
+
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// 16-byte chunk XOR of a 128-byte LDS row r (window pixel or B row): rows r, r+1 share a 256-byte
+// bank row, so XOR bits 1..3 of r -> 16 consecutive rows x one chunk = 16 distinct bank slots
+__device__ __forceinline__ int sw8(int r) { return (r >> 1) & 7; }
+
+template <int S>
+__device__ __forceinline__ int kn_swz(int r) {  // as igemm3.hip (k-major B rows of S bytes)
+  if constexpr (S >= 256) return 4 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else if constexpr (S == 128) return 4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+  else return 4 * ((r >> 3) & 1);
+}
+
+// The schedule constants in SGPRs: read once from the kernel arguments (indexing the kernarg arrays
+// with a runtime value inside the K loop would be an s_load per step, and its s_waitcnt lgkmcnt(0)
+// also waits for every outstanding ds_read -- it serialised fragment reads and MFMAs).
+struct Sched {
+  int nt0, nt1, nt2, nt3, nch, nph, shared, nwb;
+  __device__ __forceinline__ int ntaps(int p) const { return p == 0 ? nt0 : p == 1 ? nt1 : p == 2 ? nt2 : nt3; }
+};
+
+__device__ __forceinline__ Sched sched_of(const IG4Args& a) {
+  Sched q;
+  q.nt0 = a.ntaps[0]; q.nt1 = a.ntaps[1]; q.nt2 = a.ntaps[2]; q.nt3 = a.ntaps[3];
+  q.nch = a.nch; q.nph = a.nphases; q.shared = a.shared_win; q.nwb = a.nwb;
+  return q;
+}
+
+// Step cursor (wave-uniform): phase p, channel chunk c, tap t (t < 0: empty step ahead of a
+// reloaded window when only one window buffer fits), window load ordinal wl, steps taken in the
+// current window sw, steps in it wlen.
+struct Cur {
+  int p, c, t, wl, sw, wlen;
+};
+
+template <int NSB>
+__device__ __forceinline__ void cur_init(Cur& k, const Sched& q) {
+  k.p = 0; k.c = 0; k.t = 0; k.wl = 0; k.sw = 0; k.wlen = q.nt0;
+}
+
+template <int NSB>
+__device__ __forceinline__ void cur_next(Cur& k, const Sched& q) {
+  ++k.t;
+  ++k.sw;
+  if (k.t < q.ntaps(k.p)) return;
+  if (++k.c == q.nch) { k.c = 0; ++k.p; }
+  if (k.p >= q.nph) { k.p = q.nph - 1; k.t = 1 << 20; return; }  // past the end (never consumed)
+  const bool load = !q.shared;
+  if (load) ++k.wl;
+  const int pre = (load && q.nwb == 1) ? NSB - 1 : 0;
+  k.t = -pre;
+  k.sw = 0;
+  k.wlen = pre + q.ntaps(k.p);
+}
+
+// tap table entry (phase p, tap t) from a lane-distributed copy: lane i of v0 / v1 holds entry i /
+// 64 + i of the flat [4][25] table (v_readlane: no memory access in the K loop)
+__device__ __forceinline__ int tap_of(int v0, int v1, int p, int t) {
+  const int i = p * 25 + t;
+  return i < 64 ? __builtin_amdgcn_readlane(v0, i) : __builtin_amdgcn_readlane(v1, i - 64);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float v, float leak) {
+  if constexpr (ACT == ACT_RELU) return fmaxf(v, 0.f);
+  else if constexpr (ACT == ACT_LRELU) return fmaxf(v, leak * v);
+  else if constexpr (ACT == ACT_TANH) return tanhf(v);
+  else return v;
+}
+
+__device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+  const elem4 v = {f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ f32x4 unpack4(uint2 u) {
+  const elem4 v = __builtin_bit_cast(elem4, u);
+  return (f32x4){(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+__device__ __forceinline__ float red16(float v) {  // sum over the 16 lanes of a row (lane & 15)
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+}  // namespace ig4
+
+// EPI: 0 plain (+bias, statistics of the stored value, activation), 1 BN-backward statistics of
+// the layer whose dL/da this GEMM produces, 2 activation backward only (store g, sums of g)
+template <int FM, int FN, int TM, int TN, int WMC, int BN, int ACT, int EPI>
+__device__ __forceinline__ void ig4_epilogue(f32x4 (&acc)[FN][FM], const IG4Args& a, int p, int mt, int m0, int n0,
+                                             int b0, int y0, int wm, int wn, int fr, int fq, lds_f32* part,
+                                             lds_i32* ctr) {
+  const int lane = threadIdx.x & 63;
+  int off[FM];
+#pragma unroll
+  for (int im = 0; im < FM; ++im) {
+    const int ml = wm * TM + im * 16 + fr;
+    const int bl = (int)fdiv((uint32_t)ml, a.fd_tw);
+    const int rem = ml - bl * a.TR * a.Wq;
+    const int ty = (int)fdiv((uint32_t)rem, a.fd_wq);
+    const int x = rem - ty * a.Wq;
+    off[im] = (((b0 + bl) * a.outH + (y0 + ty) * a.ostride + a.oy_off[p]) * a.outW + x * a.ostride + a.ox_off[p]) *
+                  a.ldc + a.cofs;
+  }
+  const bool do_stats = a.stats != nullptr;
+  const float slope = a.bnb_act == ACT_LRELU ? a.bnb_leak : 0.f;
+  const int g = EPI == 1 ? m0 / a.bnb_rpg : 0;
+#pragma unroll
+  for (int jn = 0; jn < FN; ++jn) {
+    const int n = n0 + wn * TN + jn * 16 + fq * 4;
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (EPI == 0 && a.bias) bv = *reinterpret_cast<const f32x4*>(a.bias + n);
+    f32x4 mu = bv, rs = bv;
+    if constexpr (EPI == 1) {
+      mu = *reinterpret_cast<const f32x4*>(a.bnb_mean + g * a.N + n);
+      rs = *reinterpret_cast<const f32x4*>(a.bnb_rstd + g * a.N + n);
+    }
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int im = 0; im < FM; ++im) {
+      const f32x4 v = acc[jn][im] + bv;
+      f32x4 vs;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vs[r] = (float)f2bf(v[r]);  // statistics of exactly the stored tensor
+      elem_t* dst = a.C + off[im] + n;
+      if constexpr (EPI == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s[r] += vs[r]; s2[r] += vs[r] * vs[r]; }
+        *reinterpret_cast<uint2*>(dst) = ig4::pack4(ig4::act_f<ACT>(v[0], a.leak), ig4::act_f<ACT>(v[1], a.leak),
+                                                    ig4::act_f<ACT>(v[2], a.leak), ig4::act_f<ACT>(v[3], a.leak));
+      } else if constexpr (EPI == 1) {
+        const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
+        const f32x4 xv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_x + off[im] + n));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gv = vs[r] * (yv[r] > 0.f ? 1.f : slope);
+          s[r] += gv;
+          s2[r] += gv * (xv[r] - mu[r]) * rs[r];
+        }
+        *reinterpret_cast<uint2*>(dst) = ig4::pack4(vs[0], vs[1], vs[2], vs[3]);
+      } else {
+        const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
+        f32x4 gv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = a.bnb_act == ACT_TANH ? 1.f - yv[r] * yv[r] : (yv[r] > 0.f ? 1.f : slope);
+          gv[r] = (float)f2bf(vs[r] * d);
+          s[r] += gv[r];
+        }
+        *reinterpret_cast<uint2*>(dst) = ig4::pack4(gv[0], gv[1], gv[2], gv[3]);
+      }
+    }
+    if (do_stats) {
+      // sums over the wave's TM rows: in registers over im, then over the 16 pixel lanes; lanes
+      // 0, 16, 32, 48 put 4 channels each into this wave's partial row part[wm][BN][2]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[r] = ig4::red16(s[r]);
+        s2[r] = EPI == 2 ? 0.f : ig4::red16(s2[r]);
+      }
+      if (fr == 0) {
+        lds_f32* q = part + (wm * BN + wn * TN + jn * 16 + fq * 4) * 2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { q[2 * r] = s[r]; q[2 * r + 1] = s2[r]; }
+      }
+    }
+  }
+  if (!do_stats) return;
+  // the last compute wave of column wn to arrive sums the partial rows in wave order
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(ctr + wn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = __shfl(old, 0, 64);
+  if (old != WMC - 1) return;
+  if (lane == 0) __hip_atomic_store(ctr + wn, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  float* dst = a.stats + (size_t)(mt * a.nphases + p) * 2 * a.N;
+  for (int c = lane; c < TN; c += 64) {
+    const int nl = wn * TN + c;
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WMC; ++w) {
+      t0 += part[(w * BN + nl) * 2];
+      t1 += part[(w * BN + nl) * 2 + 1];
+    }
+    dst[n0 + nl] = t0;
+    dst[a.N + n0 + nl] = t1;
+  }
+}
+
+template <int BM, int BN, int WMC, int WNC, int NSB, int BKN>
+__global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4Args a) {
+  using namespace ig4;
+  constexpr int NC = WMC * WNC;
+  constexpr int TM = BM / WMC, TN = BN / WNC;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int BSTAGE = BN * 128;  // 64 k-rows x BN columns x 2 bytes
+  constexpr int NPB = BSTAGE / 1024;
+  constexpr int PBL = NPB / NL;     // B pieces per loader wave per stage
+  constexpr int SB = BN * 2;        // k-major (BKN) B row bytes
+  static_assert(NPB % NL == 0 && PBL >= 1, "B stage pieces split evenly over the loader waves");
+  static_assert(FM >= 1 && FN >= 1 && TM % 16 == 0 && TN % 16 == 0, "wave tile");
+  static_assert(!BKN || (SB <= 1024 && 1024 % SB == 0), "k-major B rows");
+  static_assert(NSB == 3 || NSB == 4, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  lds_char* const l3 = (lds_char*)lds;
+  const uint32_t lbase = (uint32_t)(uintptr_t)l3;
+  const uint32_t win0 = (uint32_t)a.ring_bytes;  // window buffers after the ring
+  lds_f32* part = reinterpret_cast<lds_f32*>(l3 + a.ring_bytes + a.nwb * a.win_bytes);
+  lds_i32* ctr = reinterpret_cast<lds_i32*>(part + WMC * BN * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // ---- tile: n fastest (tiles of one window on one XCD), XCD-aware bijective remap
+  int t = blockIdx.x;
+  {
+    const int total = a.mtiles * a.ntiles;
+    const int q = total >> 3, rr = total & 7, xcd = t & 7;
+    t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+  }
+  const int nt = t % a.ntiles, mt = t / a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int b0 = (int)fdiv((uint32_t)m0, a.fd_hw);
+  const int y0 = (int)fdiv((uint32_t)(m0 - b0 * a.Hq * a.Wq), a.fd_wq);
+  const int S_ = a.steps;
+  const Sched q = sched_of(a);
+  const int* tflat = &a.tap[0][0];
+  int vt0 = tflat[lane], vt1 = lane < 36 ? tflat[64 + lane] : 0;
+  asm volatile("" : "+v"(vt0), "+v"(vt1));  // loaded (and waited for) here, not re-loaded in the K loop
+
+  if (tid < 64 && lane < WNC) ctr[lane] = 0;
+
+  if (wave >= NC) {
+    // =============================================================== loader waves
+    const int lid = wave - NC;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a.a_bytes);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.Bw, a.b_bytes);
+    const int Kc = a.Kc, N = a.N;
+    // window pieces [q0, q1) of chunk `ch` into window buffer `buf`: this loader takes q = lid mod NL
+    auto issue_win = [&](int q0, int q1, int buf, int ch) -> int {
+      int n = 0;
+      const uint32_t dst0 = lbase + win0 + (uint32_t)buf * a.win_bytes;
+      for (int q = q0 + lid; q < q1; q += NL, ++n) {
+        const int L = q * 64 + lane;
+        const int P = L >> 3;
+        const int j = (L & 7) ^ sw8(P);
+        uint32_t off = OOB;
+        if (P < a.wpix) {
+          const int bl = (int)fdiv((uint32_t)P, a.fd_wimg);
+          const int rem = P - bl * a.WY * a.WXP;
+          const int wy = (int)fdiv((uint32_t)rem, a.fd_wxp);
+          const int X = rem - wy * a.WXP;
+          const int wx = a.S == 2 ? (X < a.HX ? 2 * X : 2 * (X - a.HX) + 1) : X;
+          const int iy = y0 * a.S + a.win_oy + wy, ix = a.win_ox + wx;
+          const int b = b0 + bl;
+          if (wx < a.WX && b < a.Bn && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+            off = (uint32_t)((((b * a.H + iy) * a.W + ix) * Kc + ch * 64 + j * 8) * 2);
+        }
+        dma16_asm_la(ra, dst0 + q * 1024, off);
+      }
+      return n;
+    };
+    // B pieces of step k (one 64-deep k slice of weight tap wt) into ring slot `slot`
+    auto issue_b = [&](const Cur& k, int slot) {
+      const int wt = tap_of(vt0, vt1, k.p, k.t) >> 16;
+      const int k0 = k.c * 64;
+      const uint32_t dst0 = lbase + (uint32_t)slot * BSTAGE;
+#pragma unroll
+      for (int i = 0; i < PBL; ++i) {
+        const int q = lid * PBL + i;
+        uint32_t off;
+        if constexpr (BKN) {
+          const int rr = q * (1024 / SB) + lane / (SB / 16);
+          const int n = n0 + ((lane % (SB / 16)) ^ (kn_swz<SB>(rr) >> 1)) * 8;
+          off = (uint32_t)(((wt * Kc + k0 + rr) * N + n) * 2);
+        } else {
+          const int r = q * 8 + (lane >> 3);
+          const int j = (lane & 7) ^ sw8(r);
+          off = (uint32_t)(((wt * N + n0 + r) * Kc + k0 + j * 8) * 2);
+        }
+        dma16_asm_la(rb, dst0 + q * 1024, off);
+      }
+    };
+    // everything stage x (= step of cursor k) carries for this loader; returns its DMA count
+    auto issue_stage = [&](const Cur& k, int slot) -> int {
+      int n = 0;
+      if (a.ablate & 2) return 0;  // timing study: no DMA at all
+      if (k.t >= 0) { issue_b(k, slot); n += PBL; }
+      if (!a.shared_win) {
+        if (a.nwb == 2) {
+          // the NEXT window streams in slices over this window's steps NSB-1 .. wlen-1
+          const bool last_win = (k.c + 1 == q.nch) && (k.p + 1 == q.nph);
+          if (!last_win && k.sw >= NSB - 1) {
+            const int ns = k.wlen - (NSB - 1), i = k.sw - (NSB - 1);
+            const int ch = k.c + 1 == q.nch ? 0 : k.c + 1;
+            n += issue_win(i * a.npw / ns, (i + 1) * a.npw / ns, (k.wl + 1) & 1, ch);
+          }
+        } else if (k.wl > 0 && k.t == 0) {
+          n += issue_win(0, a.npw, 0, k.c);  // behind NSB-1 empty steps: the old window is dead
+        }
+      }
+      return n;
+    };
+
+    Cur ki;
+    cur_init<NSB>(ki, q);
+    int cnt[NSB];
+    if (!(a.ablate & 2)) issue_win(0, a.npw, 0, 0);
+#pragma unroll
+    for (int x = 0; x < NSB - 1; ++x) {
+      cnt[x] = 0;
+      if (x < S_) { cnt[x] = issue_stage(ki, x % NSB); cur_next<NSB>(ki, q); }
+    }
+    // stages 0 and 1 (and window 0) landed at barrier 0
+    if constexpr (NSB == 4) wvm_dyn(cnt[2]);
+    else wvm<0>();
+    barrier();
+    for (int s = 0; s + 1 < S_; ++s) {
+      const int x = s + NSB - 1;
+      int cx = 0;
+      if (x < S_) { cx = issue_stage(ki, x % NSB); cur_next<NSB>(ki, q); }
+      // stage s+2 landed at barrier s+1 (stage s+3 = x may stay in flight when NSB = 4)
+      if constexpr (NSB == 4) wvm_dyn(cx);
+      else wvm<0>();
+      barrier();
+    }
+    wvm<0>();
+    return;
+  }
+
+  // ================================================================= compute waves
+  const int wm = wave / WNC, wn = wave % WNC;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  // window pixel of each activation-fragment row of this lane at tap offset 0
+  int pbase[FM];
+#pragma unroll
+  for (int im = 0; im < FM; ++im) {
+    const int ml = wm * TM + im * 16 + fr;
+    const int bl = (int)fdiv((uint32_t)ml, a.fd_tw);
+    const int rem = ml - bl * a.TR * a.Wq;
+    const int ty = (int)fdiv((uint32_t)rem, a.fd_wq);
+    const int x = rem - ty * a.Wq;
+    pbase[im] = (bl * a.WY + a.S * ty) * a.WXP + x;
+  }
+  // BKN = 0: weight-fragment row byte offsets in a stage (chunk fq of row r, XOR-swizzled)
+  int wrow[FN];
+#pragma unroll
+  for (int jn = 0; jn < FN; ++jn) {
+    const int r = wn * TN + jn * 16 + fr;
+    wrow[jn] = r * 128 + ((fq ^ sw8(r)) << 4);
+  }
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int jn = 0; jn < FN; ++jn)
+#pragma unroll
+    for (int im = 0; im < FM; ++im) acc[jn][im] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragments of k-half h (32 of the 64 k rows) of the step at cursor k
+  auto read_frags = [&](int h, const Cur& k, int slot, elem8 (&af)[FM], elem8 (&wf)[FN]) {
+    const lds_char* wb = l3 + win0 + (uint32_t)(a.nwb == 2 ? k.wl & 1 : 0) * a.win_bytes;
+    const int toff = tap_of(vt0, vt1, k.p, k.t) & 0xffff;
+#pragma unroll
+    for (int im = 0; im < FM; ++im) {
+      const int P = pbase[im] + toff;
+      const uint32_t o = (uint32_t)(P * 128 + ((fq ^ sw8(P)) << 4)) ^ (uint32_t)(h * 64);
+      af[im] = *LDS_PTR(const elem8, wb + o);
+    }
+    const lds_char* sb = l3 + slot * BSTAGE;
+    if constexpr (BKN) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = h * 32 + 8 * g4 + 4 * hh + q4;
+#pragma unroll
+        for (int jn = 0; jn < FN; ++jn) {
+          const int c8 = (wn * TN + jn * 16) / 4 + p4;
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, sb + r * SB + ((c8 ^ kn_swz<SB>(r)) * 8)));
+          const elem4 vb = __builtin_bit_cast(elem4, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wf[jn][4 * hh + e] = vb[e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int jn = 0; jn < FN; ++jn) wf[jn] = *LDS_PTR(const elem8, sb + (wrow[jn] ^ (h * 64)));
+    }
+  };
+  auto mfmas = [&](const elem8 (&af)[FM], const elem8 (&wf)[FN]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jn = 0; jn < FN; ++jn)
+#pragma unroll
+      for (int im = 0; im < FM; ++im) acc[jn][im] = DCG_MFMA_16x16x32(wf[jn], af[im], acc[jn][im], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto epilogue = [&](int p) {
+#define DCG_IG4_EPI(ACT_, EPI_) \
+  ig4_epilogue<FM, FN, TM, TN, WMC, BN, ACT_, EPI_>(acc, a, p, mt, m0, n0, b0, y0, wm, wn, fr, fq, part, ctr)
+    if (a.bnb_x) {
+      if (a.bnb_store_g) DCG_IG4_EPI(ACT_NONE, 2);
+      else DCG_IG4_EPI(ACT_NONE, 1);
+    } else {
+      switch (a.act) {
+        case ACT_RELU: DCG_IG4_EPI(ACT_RELU, 0); break;
+        case ACT_LRELU: DCG_IG4_EPI(ACT_LRELU, 0); break;
+        case ACT_TANH: DCG_IG4_EPI(ACT_TANH, 0); break;
+        default: DCG_IG4_EPI(ACT_NONE, 0); break;
+      }
+    }
+#undef DCG_IG4_EPI
+#pragma unroll
+    for (int jn = 0; jn < FN; ++jn)
+#pragma unroll
+      for (int im = 0; im < FM; ++im) acc[jn][im] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  };
+
+  Cur k, k1;
+  cur_init<NSB>(k, q);
+  k1 = k;
+  cur_next<NSB>(k1, q);
+  elem8 a0[FM], w0[FN], a1[FM], w1[FN];
+  barrier();  // B_0: stages 0, 1 and window 0 landed
+  bool have0 = false;  // the first k-half of step s was read ahead (during step s-1)
+  if (k.t >= 0 && !(a.ablate & 1)) { read_frags(0, k, 0, a0, w0); have0 = true; }
+  for (int s = 0; s < S_; ++s) {
+    if (s > 0) barrier();  // B_s: stage s+1 landed, every compute wave done with step s-1
+    if (k.t >= 0 && (a.ablate & 1)) {  // timing study: no fragment reads / MFMAs
+      if (k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1) epilogue(k.p);
+    } else if (k.t >= 0) {
+      if (!have0) read_frags(0, k, s % NSB, a0, w0);  // first step after empty steps
+      read_frags(1, k, s % NSB, a1, w1);
+      mfmas(a0, w0);
+      const bool phase_end = k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1;
+      have0 = s + 1 < S_ && k1.t >= 0;
+      if (have0 && !phase_end) read_frags(0, k1, (s + 1) % NSB, a0, w0);
+      mfmas(a1, w1);
+      if (phase_end) {  // (the next step's first fragments after the epilogue: fewer live registers)
+        epilogue(k.p);
+        if (have0) read_frags(0, k1, (s + 1) % NSB, a0, w0);
+      }
+    }
+    k = k1;
+    cur_next<NSB>(k1, q);
+  }
+}
+
+}  // namespace dcg
+
+// ---------------------------------------------------------------------------- host launch
+// cfg = 500 + 10 * k + id, B ring stages NSB = {4, 3}[k]; tile id -> (BM, BN, compute waves WMC x WNC),
+// 64x64 per compute wave, + 4 loader waves
+#define DCG_IGEMM4_TILES(X)                                                                  \
+  X(0, 128, 128, 2, 2) X(1, 256, 64, 4, 1) X(2, 256, 128, 4, 2) X(3, 128, 256, 2, 4) X(4, 512, 64, 8, 1) \
+  X(5, 64, 256, 1, 4) X(6, 128, 64, 2, 1) X(7, 64, 128, 1, 2)
+
+#ifdef DCG_ONE_CFG  // kernel studies: compile one tile only
+#define DCG_IGEMM4_TILES_SEL(X) X(0, 128, 128, 2, 2)
+#else
+#define DCG_IGEMM4_TILES_SEL(X) DCG_IGEMM4_TILES(X)
+#endif
+
+static constexpr int kIgemm4Stages[2] = {4, 3};
+
+extern "C" int DCG_API(dcg_igemm4_tile)(int cfg, int* bm, int* bn, int* nsb, int* wm, int* wn) {
+  if (cfg < 500 || cfg >= 520) return -1;
+  const int id = cfg % 10;
+  *nsb = kIgemm4Stages[(cfg - 500) / 10];
+#define X(id_, BM_, BN_, WM_, WN_) \
+  if (id == id_) { *bm = BM_; *bn = BN_; *wm = WM_; *wn = WN_; return 0; }
+  DCG_IGEMM4_TILES_SEL(X)
+#undef X
+  return -1;
+}
+
+template <int BM, int BN, int WM, int WN, int NSB, int BKN>
+static int launch4(const dcg::IG4Args* a, unsigned blocks, size_t shm, hipStream_t s) {
+  auto k = dcg::igemm4_kernel<BM, BN, WM, WN, NSB, BKN>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * (WM * WN + dcg::ig4::NL)), shm, s, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int DCG_API(dcg_igemm4_launch)(const dcg::IG4Args* a, int cfg, int bkn, unsigned blocks, size_t shm,
+                                          hipStream_t s) {
+  int bm, bn, nsb, wm, wn;
+  if (DCG_API(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wm, &wn) || shm > 160 * 1024) return -1;
+  const int id = cfg % 10;
+#define X(id_, BM_, BN_, WM_, WN_)                                                         \
+  if (id == id_) {                                                                         \
+    if (nsb == 3) return bkn ? launch4<BM_, BN_, WM_, WN_, 3, 1>(a, blocks, shm, s)        \
+                             : launch4<BM_, BN_, WM_, WN_, 3, 0>(a, blocks, shm, s);       \
+    return bkn ? launch4<BM_, BN_, WM_, WN_, 4, 1>(a, blocks, shm, s)                      \
+               : launch4<BM_, BN_, WM_, WN_, 4, 0>(a, blocks, shm, s);                     \
+  }
+  DCG_IGEMM4_TILES_SEL(X)
+#undef X
+  return -1;
+}

@@ -80,6 +80,8 @@ struct IGemmArgs {
   const BnFin* fin;         // igemm3: BN finalize fused into the epilogue (nullptr = separate kernel)
 };
 
+struct IG4Args;  // igemm4.hip (csrc/hip/ig4.h)
+
 struct WGradArgs {
   const elem_t* G; int Hg, Wg, Mc;     // gathered operand [B][Hg][Wg][Mc] (plain: [K][Mc])
   const elem_t* Dm; int Nc;            // direct operand [K][Nc]

@@ -120,7 +120,9 @@ class Loader {
     if (!error_.empty()) throw std::runtime_error(error_);
     // draw the batch's slots under the lock (RandomShuffleQueue semantics), copy them out with
     // the lock released (the readers keep decoding meanwhile), then hand the slots back
-    std::vector<int>& taken = taken_;
+    // the drawn slots live in a thread-local scratch vector (no allocation per batch, and two
+    // consumers calling next_batch at once never share it)
+    thread_local std::vector<int> taken;
     taken.clear();
     while ((int)taken.size() < batch_ && !filled_.empty()) {
       std::uniform_int_distribution<size_t> dist(0, filled_.size() - 1);
@@ -261,7 +263,6 @@ class Loader {
   std::string feature_;
   SrcType src_ = SRC_AUTO;
   OutType out_ = OUT_F32;
-  std::vector<int> taken_;
   size_t elems_;
   int batch_, min_after_, capacity_;
   bool loop_, verify_;

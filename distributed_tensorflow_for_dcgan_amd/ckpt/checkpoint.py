@@ -81,6 +81,9 @@ def latest_checkpoint(ckpt_dir: str) -> Optional[str]:
     return None
 
 
+BN_STEPS_KEYS = ("g_bn/ExponentialMovingAverage/local_step", "d_bn/ExponentialMovingAverage/local_step")
+
+
 def collect_state(engine) -> "OrderedDict[str, np.ndarray]":
     """TF-named numpy tensors of everything a resume needs."""
     engine.sync_state_for_checkpoint()
@@ -95,6 +98,10 @@ def collect_state(engine) -> "OrderedDict[str, np.ndarray]":
         out[k] = v.detach().cpu().numpy().astype(np.float32)
     for k, v in m.d_bn.tf_names().items():
         out[k] = v.detach().cpu().numpy().astype(np.float32)
+    # moving-average update counts (the --bn_zero_debias divisor 1 - decay^t; TF keeps a
+    # local_step per average for the same purpose)
+    out[BN_STEPS_KEYS[0]] = m.g_bn.steps.numpy().astype(np.float64)
+    out[BN_STEPS_KEYS[1]] = m.d_bn.steps.numpy().astype(np.float64)
     for opt in (engine.opt_d, engine.opt_g):
         for k, v in opt.tf_slot_tensors().items():
             a = v.detach().cpu().numpy().astype(np.float32)
@@ -114,6 +121,13 @@ def apply_state(engine, sd: Dict[str, np.ndarray], strict: bool = True) -> Dict[
             for k, v in names.items():
                 if k in tsd:
                     v.copy_(tsd[k].to(v.dtype).reshape(v.shape))
+        # EMA update counts: saved ones, else one update per synchronous step (older checkpoints)
+        step_now = int(np.asarray(sd["Variable"]).reshape(-1)[0]) if "Variable" in sd else 0
+        for key, bn in zip(BN_STEPS_KEYS, (m.g_bn, m.d_bn)):
+            if key in tsd and tsd[key].numel() == bn.steps.numel():
+                bn.steps.copy_(tsd[key].to(torch.float64).reshape(bn.steps.shape))
+            else:
+                bn.steps.fill_(float(step_now))
     info["adam_d"] = engine.opt_d.load_tf_slots(tsd)
     info["adam_g"] = engine.opt_g.load_tf_slots(tsd)
     if "Variable" in tsd:

@@ -26,12 +26,14 @@ LOADER_DTYPE = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f1
 ENGINE_DTYPE = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
 
 
-def batch_dtype(flags, device) -> torch.dtype:
-    """The dtype batches are decoded into: the training compute dtype on a GPU (bf16 batches
-    halve the H2D bytes and need no on-device cast), fp32 on the CPU."""
-    if torch.device(device).type != "cuda":
+def batch_dtype(device, engine_dtype: Optional[str] = None) -> torch.dtype:
+    """The dtype batches are decoded into: the compute dtype of the engine that was BUILT
+    (``engine.dtype_name``) on a GPU -- bf16 batches halve the H2D bytes and need no on-device
+    cast -- and fp32 on the CPU or when the engine is unknown (the fp32 reference engine must
+    never see quantized inputs)."""
+    if torch.device(device).type != "cuda" or engine_dtype is None:
         return torch.float32
-    return ENGINE_DTYPE.get(str(getattr(flags, "dtype", "bf16")), torch.float32)
+    return ENGINE_DTYPE.get(str(engine_dtype), torch.float32)
 
 
 class SyntheticSource:
@@ -275,9 +277,11 @@ class ImageFolderSource:
 
 
 def make_source(flags, batch: int, shape, device, rank: int = 0, world: int = 1, data_dir: Optional[str] = None,
-                seed_offset: int = 0, loop: bool = True, shuffle_buffer: Optional[int] = None):
+                seed_offset: int = 0, loop: bool = True, shuffle_buffer: Optional[int] = None,
+                engine_dtype: Optional[str] = None):
     """Pick the input source from the flags: --synthetic, a TFRecord directory (reference
-    default ``--data_dir=train``), or a folder of images."""
+    default ``--data_dir=train``), or a folder of images. engine_dtype: the built engine's
+    ``dtype_name`` (TFRecord batches are decoded into it on a GPU; fp32 when None)."""
     seed = int(flags.seed) + seed_offset
     if flags.synthetic:
         return SyntheticSource(batch, shape, device, seed=seed + 1000 * rank)
@@ -288,7 +292,7 @@ def make_source(flags, batch: int, shape, device, rank: int = 0, world: int = 1,
             return ImageFolderSource(d, batch, shape, device, is_crop=bool(flags.is_crop),
                                      image_size=int(flags.image_size), rank=rank, world=world,
                                      shard=bool(flags.shard_data), seed=seed)
-    dt = batch_dtype(flags, device)
+    dt = batch_dtype(device, engine_dtype)
     if bool(getattr(flags, "cache_on_device", False)) and data_dir is None:
         return DeviceCachedSource(d, batch, shape, device, rank=rank, world=world, shard=bool(flags.shard_data),
                                   seed=seed, threads=int(flags.loader_threads), dtype=dt)

@@ -120,7 +120,8 @@ class HipEngine:
     def __init__(self, cfg: DCGANConfig, batch_size: int, device: torch.device, dtype: str = "bf16",
                  seed: int = 0, lr: float = 2e-4, beta1: float = 0.5, zero_debias: bool = False, rank: int = 0,
                  world: int = 1, graph: bool = True, allreduce_dtype: str = "fp32", bucket_mb: float = 32.0,
-                 rank_seeded_z: bool = True, schedule: Optional[str] = None, dry_run: bool = False, **_):
+                 rank_seeded_z: bool = True, schedule: Optional[str] = None, dry_run: bool = False,
+                 ddp: Optional[bool] = None, **_):
         if dtype not in DTYPES:
             raise ValueError("HIP engine dtype must be one of %s" % sorted(DTYPES))
         self.dtype_name = dtype
@@ -135,6 +136,9 @@ class HipEngine:
         self.B = int(batch_size)
         self.device = device
         self.rank, self.world = rank, world
+        # data-parallel path (collectives on the comm stream, segmented step): any W > 1, or a
+        # forced one-rank process group (DCGAN_FORCE_DDP=1 / ddp=True: RCCL on a one-GPU box)
+        self.ddp = world > 1 or (D.ddp_forced() if ddp is None else bool(ddp))
         self.seed = int(seed)
         self.rank_seeded_z = bool(rank_seeded_z)  # False only in equivalence tests
         self.lr, self.beta1 = float(lr), float(beta1)
@@ -144,7 +148,7 @@ class HipEngine:
             raise ValueError("schedule must be one of %s" % (SCHEDULES,))
         self._sched_req = schedule
         self.model = DCGAN(cfg, device=device, seed=seed, zero_debias=zero_debias)
-        if world > 1 and not self.dry:
+        if self.ddp and not self.dry:
             D.broadcast_tensors([self.model.g.flat, self.model.d.flat, self.model.g_bn.flat, self.model.d_bn.flat])
         self.opt_d = TFAdam(self.model.d, lr, beta1, power_suffix="")
         self.opt_g = TFAdam(self.model.g, lr, beta1, power_suffix="_1")
@@ -157,7 +161,7 @@ class HipEngine:
         self.graph_enabled = False
         self._timing = False
         self._graphs: List[Optional[torch.cuda.CUDAGraph]] = []
-        self.comm_stream = torch.cuda.Stream(device=device) if (world > 1 and not self.dry) else None
+        self.comm_stream = torch.cuda.Stream(device=device) if (self.ddp and not self.dry) else None
         self.allreduce_dtype = allreduce_dtype
         self.bucket_mb = bucket_mb
         self._exec = None
@@ -1001,7 +1005,7 @@ class HipEngine:
 
     def _schedule(self) -> str:
         req = self._sched_req
-        if self.world > 1 or self._timing:  # collectives / phase timers need the segmented step
+        if self.ddp or self._timing:  # collectives / phase timers need the segmented step
             return req if req in ("concurrent", "serial") else "concurrent"
         return req or "fused"
 
@@ -1096,13 +1100,13 @@ class HipEngine:
     def _ar_launch(self, ex, which: str, src) -> None:
         """All-reduce one gradient slice ("g", "dtop", "drest") on the comm stream once `src`'s
         queued work is done."""
-        if self.world > 1:
+        if self.ddp:
             ex.wait(ex.comm, src)
             ex.collective(getattr(self, "_ar_" + which), ex.comm)
 
     def _ar_join(self, ex, dst) -> None:
         """dst waits for every collective issued so far (the 1/W scale is folded into Adam)."""
-        if self.world > 1:
+        if self.ddp:
             ex.wait(dst, ex.comm)
 
     def _run_step(self, ex):
@@ -1130,7 +1134,7 @@ class HipEngine:
             # the D chain ends first: D's last bucket goes on the wire before G's, and Adam(D)
             # runs while G's all-reduce is in flight
             self._ar_launch(ex, "drest", alt)
-            d_done = ex.mark(ex.comm) if self.world > 1 else None
+            d_done = ex.mark(ex.comm) if self.ddp else None
             self._ar_launch(ex, "g", cs)
             if d_done is not None:
                 ex.wait_mark(cs, d_done)       # dtop + drest collectives
@@ -1145,7 +1149,7 @@ class HipEngine:
         self._seg(ex, 0, cs)                   # fwd, g_loss chain through D(fake), G backward -> grad_g final
         self._tick(1, cs)
         self._ar_launch(ex, "g", cs)
-        g_done = ex.mark(ex.comm) if self.world > 1 else None
+        g_done = ex.mark(ex.comm) if self.ddp else None
         self._seg(ex, 1, cs)                   # D backward: head + top layer (overlaps the G all-reduce)
         self._tick(2, cs)
         self._ar_launch(ex, "dtop", cs)
@@ -1161,12 +1165,12 @@ class HipEngine:
         self._tick(5, cs)
 
     def _ensure_comm(self):
-        if self.world > 1 and not hasattr(self, "_ar_g"):
+        if self.ddp and not hasattr(self, "_ar_g"):
             o = self._d_top_off
             cs, mb, wd = self.comm_stream, self.bucket_mb, self.allreduce_dtype
-            self._ar_g = D.GradAllReducer(self.grad_g.flat, mb, wd, stream=cs)
-            self._ar_dtop = D.GradAllReducer(self.grad_d.flat[o:], mb, wd, stream=cs)
-            self._ar_drest = D.GradAllReducer(self.grad_d.flat[:o], mb, wd, stream=cs)
+            self._ar_g = D.GradAllReducer(self.grad_g.flat, mb, wd, stream=cs, force=True)
+            self._ar_dtop = D.GradAllReducer(self.grad_d.flat[o:], mb, wd, stream=cs, force=True)
+            self._ar_drest = D.GradAllReducer(self.grad_d.flat[:o], mb, wd, stream=cs, force=True)
 
     def _capture(self):
         """Capture each step segment into its own hipGraph (collectives stay outside, issued

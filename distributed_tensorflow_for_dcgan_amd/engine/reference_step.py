@@ -65,10 +65,9 @@ class ReferenceStep:
 
     def step(self, real: torch.Tensor, z: torch.Tensor) -> Dict[str, float]:
         out, gd, gg = self.compute_grads(real, z)
-        if self.model.d_bn.zero_debias:
-            for s in range(2):
-                self.model.d_bn.count_step(s)
-            self.model.g_bn.count_step(0)
+        for s in range(2):  # one EMA update per BN slot per step (as the HIP engine counts)
+            self.model.d_bn.count_step(s)
+        self.model.g_bn.count_step(0)
         if self.grad_hook is not None:
             self.grad_hook("d", gd)
             self.grad_hook("g", gg)

@@ -40,13 +40,33 @@ def rank() -> int:
     return dist.get_rank() if is_initialized() else 0
 
 
+def ddp_forced() -> bool:
+    """DCGAN_FORCE_DDP=1: run the data-parallel path (process group, collectives on the comm
+    stream, segmented step) even for a single process -- a one-rank RCCL group exercises the
+    real collective code on a one-GPU machine."""
+    return os.environ.get("DCGAN_FORCE_DDP", "") == "1"
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def init_distributed(world: int, rank_: int, device: torch.device, master_addr: Optional[str] = None,
-                     master_port: Optional[int] = None, timeout_s: float = 600.0):
-    """Create the default process group when world > 1 (no-op for a single process)."""
+                     master_port: Optional[int] = None, timeout_s: float = 600.0, force: Optional[bool] = None):
+    """Create the default process group when world > 1, or for one process when forced
+    (``force`` / DCGAN_FORCE_DDP=1); otherwise a no-op."""
     global _PG_INITIALISED_HERE
-    if world <= 1 or is_initialized():
+    force = ddp_forced() if force is None else bool(force)
+    if (world <= 1 and not force) or is_initialized():
         return dist.group.WORLD if is_initialized() else None
     os.environ.setdefault("MASTER_ADDR", master_addr or "127.0.0.1")
+    if world <= 1 and "MASTER_PORT" not in os.environ and master_port is None:
+        os.environ["MASTER_PORT"] = str(_free_port())  # a lone rank: any free port
     os.environ.setdefault("MASTER_PORT", str(master_port or 29500))
     backend = "nccl" if device.type == "cuda" else "gloo"
     # gloo over GPU tensors lets several ranks share ONE GPU (RCCL refuses that): used by the
@@ -157,9 +177,11 @@ class GradAllReducer:
     """
 
     def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 32.0, wire_dtype: str = "fp32",
-                 reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None):
+                 reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None, force: bool = False):
         self.flat = flat_grad
         self.world = world_size()
+        # collectives are issued when there is a peer -- or on a forced one-rank group
+        self.active = is_initialized() and (self.world > 1 or force)
         esize = 2 if wire_dtype == "bf16" else 4
         self.buckets = make_buckets(flat_grad.numel(), int(bucket_mb * 1024 * 1024 / esize))
         if reverse:  # gradients of the last layers are final first
@@ -173,7 +195,7 @@ class GradAllReducer:
         self._works = []
 
     def launch(self) -> None:
-        if self.world <= 1:
+        if not self.active:
             return
         if self.stream is not None:
             cur = torch.cuda.current_stream(self.flat.device)
@@ -187,7 +209,7 @@ class GradAllReducer:
     def issue(self) -> None:
         """The bucket collectives on the CURRENT stream (the caller has ordered it after the
         producers of the gradients; the HIP engine's executor does this)."""
-        if self.world <= 1:
+        if not self.active:
             return
         for s, e in self.buckets:
             if self.wire is not None:
@@ -206,7 +228,7 @@ class GradAllReducer:
         return out
 
     def wait(self, scale_in_place: bool = True) -> None:
-        if self.world <= 1:
+        if not self.active:
             return
         if self.stream is not None:
             torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)

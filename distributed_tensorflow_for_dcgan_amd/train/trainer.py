@@ -143,11 +143,13 @@ def run(flags: Flags, out=None) -> int:
     if bool(flags.timing) and hasattr(engine, "enable_timing"):
         engine.enable_timing()
 
-    source = make_source(flags, B, shape, device, rank=rank, world=world)
+    edt = getattr(engine, "dtype_name", None)
+    source = make_source(flags, B, shape, device, rank=rank, world=world, engine_dtype=edt)
     sample_source = None
     if chief and not flags.synthetic and os.path.isdir(flags.sample_image_dir):
         sample_source = make_source(flags, B, shape, device, rank=0, world=1, data_dir=flags.sample_image_dir,
-                                    seed_offset=99, shuffle_buffer=min(int(flags.shuffle_buffer), 4 * B))
+                                    seed_offset=99, shuffle_buffer=min(int(flags.shuffle_buffer), 4 * B),
+                                    engine_dtype=edt)
     gen = torch.Generator().manual_seed(int(flags.seed) + 4242)
     sample_z = (torch.rand(B, cfg.z_dim, generator=gen) * 2 - 1).to(device)  # fixed (image_train.py:77)
 
@@ -232,6 +234,7 @@ def run(flags: Flags, out=None) -> int:
                 if not D.params_in_sync([engine.model.g.flat, engine.model.d.flat], device):
                     raise RuntimeError("DDP divergence: parameters differ across ranks at step %d" % step)
             if fault_at >= 0 and step == fault_at:
+                emit(losslog.ready(flush=True))  # the last step lines before a crash are the useful ones
                 print("DCGAN_FAULT_AT_STEP=%d: simulated failure" % fault_at, file=out, flush=True)
                 out.flush()
                 os._exit(3)
@@ -242,6 +245,10 @@ def run(flags: Flags, out=None) -> int:
             path = ckpt.save(engine)
             print("saved %s" % path, file=out)
     finally:
+        try:  # pending step lines (a no-op after the normal flush above; kept on any exception)
+            emit(losslog.ready(flush=True))
+        except Exception:  # pragma: no cover - a dead device must not mask the original error
+            pass
         source.close()
         if sample_source is not None:
             sample_source.close()

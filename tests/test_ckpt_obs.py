@@ -101,6 +101,9 @@ def test_resume_is_exact(tmp_path):
     assert torch.allclose(a.model.d.flat, c.model.d.flat, atol=1e-6)
     assert torch.allclose(a.model.g_bn.flat, c.model.g_bn.flat, atol=1e-6)
     assert torch.allclose(a.opt_g.m.flat, c.opt_g.m.flat, atol=1e-7)
+    # the moving-average update counts (zero-debias divisor) survive the restore as well
+    assert torch.equal(a.model.g_bn.steps, c.model.g_bn.steps) and torch.equal(a.model.d_bn.steps, c.model.d_bn.steps)
+    assert float(c.model.g_bn.steps[0]) > 0
 
 
 def test_keep_last_n_and_reference_style_restore(tmp_path):
@@ -114,7 +117,7 @@ def test_keep_last_n_and_reference_style_restore(tmp_path):
     assert not os.path.exists(str(tmp_path / "model.ckpt-1.index"))
     # a reference-style checkpoint: weights + EMA + global_step, no Adam slots
     sd = CK.collect_state(e)
-    ref_sd = {k: v for k, v in sd.items() if "Adam" not in k and not k.startswith("beta")}
+    ref_sd = {k: v for k, v in sd.items() if "Adam" not in k and not k.startswith("beta") and "local_step" not in k}
     ref_sd["Variable"] = np.array(9, np.int32)
     TB.write_bundle(str(tmp_path / "model.ckpt-9"), ref_sd)
     CK.write_index(str(tmp_path), "model.ckpt-9", ["model.ckpt-9"])
@@ -123,6 +126,8 @@ def test_keep_last_n_and_reference_style_restore(tmp_path):
     assert info["global_step"] == 9 and info["adam_d"] is False
     assert torch.equal(f.model.d.flat, e.model.d.flat)
     assert float(f.opt_d.powers[0]) == 0.5
+    # no saved update counts: one EMA update per synchronous step is assumed
+    assert float(f.model.g_bn.steps[0]) == 9.0 and float(f.model.d_bn.steps[1]) == 9.0
 
 
 def test_event_file_contents(tmp_path):
@@ -162,3 +167,15 @@ def test_png_and_grid(tmp_path):
     raw = IM.encode_png(np.zeros((3, 4, 3), np.uint8))
     assert np.asarray(Image.open(__import__("io").BytesIO(raw))).shape == (3, 4, 3)
     assert IM.grid_size(64) == (8, 8)
+
+
+def test_batch_dtype_follows_the_built_engine():
+    """TFRecord batches are decoded into the compute dtype of the engine that was built -- never
+    into bf16 for the fp32 reference engine (pipeline.batch_dtype)."""
+    from distributed_tensorflow_for_dcgan_amd.data import pipeline as PL
+    assert PL.batch_dtype("cuda", "bf16") == torch.bfloat16
+    assert PL.batch_dtype("cuda", "fp16") == torch.float16
+    assert PL.batch_dtype("cuda", "fp32") == torch.float32
+    assert PL.batch_dtype("cuda", None) == torch.float32
+    assert PL.batch_dtype("cpu", "bf16") == torch.float32
+    assert ReferenceEngine.dtype_name == "fp32"

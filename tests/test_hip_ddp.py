@@ -119,3 +119,57 @@ def test_bench_two_ranks_json_contract(tmp_path):
     assert res["n_gpus"] == 2 and res["steps"] == 4 and res["warmup"] == 2
     assert res["config"]["global_batch"] == 256 and res["config"]["parallelism"] == "dp2"
     assert res["value"] > 0 and res["higher_is_better"] is True and res["scaling"] == "weak"
+
+
+def _rccl_worker(out_dir, graph, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DCGAN_FORCE_DDP"] = "1"
+    os.environ.pop("DCGAN_DIST_BACKEND", None)
+    torch.cuda.set_device(0)
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    import torch.distributed as tdist
+    D.init_distributed(1, 0, torch.device("cuda", 0))
+    eng = _make(1, 0, graph)
+    assert eng.ddp and eng._schedule() == "concurrent"
+    d, g, step = _run(eng)
+    torch.save({"d": d, "g": g, "step": step, "backend": tdist.get_backend(), "world": tdist.get_world_size(),
+                "graph": eng.graph_enabled}, os.path.join(out_dir, "rccl.pt"))
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph):
+    """The REAL collective path on a one-GPU box: a one-rank RCCL (backend "nccl") process group
+    (DCGAN_FORCE_DDP=1), the segmented concurrent schedule with the gradient all-reduces issued
+    on the comm stream between graph segments -- bit-identical to the fused single-graph step."""
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port()))
+    p.start()
+    p.join(timeout=600)
+    assert p.exitcode == 0, "RCCL rank exited with %s" % p.exitcode
+    r = torch.load(tmp_path / "rccl.pt", weights_only=True)
+    assert r["backend"] == "nccl" and r["world"] == 1 and r["step"] == STEPS and r["graph"] == graph
+    eng = _make(1, 0, True)
+    assert not eng.ddp and eng._schedule() == "fused"
+    d, g, _ = _run(eng)
+    assert torch.equal(r["d"], d), (r["d"] - d).abs().max()
+    assert torch.equal(r["g"], g), (r["g"] - g).abs().max()
+
+
+def test_bench_force_ddp_reports_rccl():
+    """bench.py --force_ddp at N=1: the timed step runs the DDP path over a one-rank RCCL group
+    and the JSON line says so (backend nccl, world_size 1)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("DCGAN_DIST_BACKEND", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "5", "--warmup", "2",
+                          "--force_ddp"], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
+    assert res["n_gpus"] == 1 and res["value"] > 0
