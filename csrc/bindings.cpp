@@ -439,6 +439,45 @@ class Program {
     if (S == 2) { g.HX = (g.WX + 1) / 2; g.WXP = 2 * g.HX; } else { g.HX = 0; g.WXP = g.WX; }
     g.win_oy = miny; g.win_ox = minx;
     g.nphases = (int)ry.size();
+    // window row pitch (LDS pixels): the smallest >= the row width for which every activation
+    // fragment read (16 output pixels x one 16-byte chunk per lane, 160-byte LDS pixels, every
+    // tap) is free of ds_read_b128 bank conflicts (MI355X_MICROARCH.md LDS lane groups)
+    {
+      static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                     {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                     {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                     {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+      const int base_w = g.WXP;
+      int best_w = base_w, best_c = 1 << 30;
+      for (int wxp = base_w; wxp < base_w + 16; ++wxp) {
+        int worst = 0;
+        for (int m0 = 0; m0 < std::min(bm, 64 * 8); m0 += 16) {  // fragment row blocks (one per 16 rows)
+          int pix[16];
+          for (int fr = 0; fr < 16; ++fr) {
+            const int ml = m0 + fr, bl = ml / (TR * Wq), rem = ml % (TR * Wq), ty = rem / Wq, x = rem % Wq;
+            pix[fr] = (bl * g.WY + S * ty) * wxp + x;
+          }
+          for (size_t p = 0; p < ry.size(); ++p)
+            for (size_t t = 0; t < ry[p].size(); ++t) {
+              const int wy = ry[p][t] - miny, wx = rx[p][t] - minx;
+              const int toff = wy * wxp + (S == 2 ? (wx & 1) * g.HX + (wx >> 1) : wx);
+              for (int gi = 0; gi < 4; ++gi) {
+                int cnt[16] = {0};
+                int c = 0;
+                for (int i = 0; i < 16; ++i) {
+                  const int l = grp[gi][i];
+                  const int slot = ((pix[l & 15] + toff) * 10 + (l >> 4)) % 16;
+                  c = std::max(c, ++cnt[slot]);
+                }
+                worst = std::max(worst, c);
+              }
+            }
+        }
+        if (worst < best_c) { best_c = worst; best_w = wxp; }
+        if (best_c == 1) break;
+      }
+      g.WXP = best_w;
+    }
     for (int p = 0; p < 4; ++p) { g.ntaps[p] = 0; g.oy_off[p] = 0; g.ox_off[p] = 0; }
     for (int p = 0; p < g.nphases; ++p) {
       g.ntaps[p] = (int)ry[p].size();
@@ -451,7 +490,7 @@ class Program {
       }
     }
     g.wpix = NI * g.WY * g.WXP;
-    g.npw = (g.wpix + 7) / 8;
+    g.npw = (g.wpix * 10 + 63) / 64;  // 160-byte LDS pixels (igemm4.hip PIXS)
     g.win_bytes = g.npw * 1024;
     g.nch = Kc / 64;
     g.shared_win = g.nch == 1;
@@ -526,6 +565,7 @@ class Program {
       }
     }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
+    if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
     last_mtiles_ = a.mtiles;
     last_nphases_ = a.nphases;
     const size_t shm = (size_t)a.ring_bytes + (size_t)a.nwb * a.win_bytes + (size_t)wmc * bn * 8 + 64;

@@ -28,7 +28,9 @@ struct IG4Args {
   int bnb_rpg, bnb_act; float bnb_leak; int bnb_store_g;
   int ntaps[4], oy_off[4], ox_off[4];
   int tap[4][25];               // window pixel offset | weight tap << 16
-  int ablate;                   // timing studies (DCGAN_IGEMM_ABLATE): 1 no fragment reads / MFMAs, 2 no DMA
+  unsigned long long* stamps;   // timing studies (DCGAN_IGEMM_STAMPS): s_memtime per workgroup, 8 slots
+  int ablate;                   // timing studies (DCGAN_IGEMM_ABLATE): 1 no fragment reads / MFMAs, 2 no DMA,
+                                // 4 no epilogue, 8 no barriers
 };
 
 }  // namespace dcg

@@ -71,10 +71,20 @@ __device__ __forceinline__ void wvm_dyn(int n) {
 }
 
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+__device__ __forceinline__ void barrier_study(int ablate) {  // ablate bit 8: no barriers (timing only)
+  if (!(ablate & 8)) barrier();
+}
 
 // 16-byte chunk XOR of a 128-byte LDS row r (window pixel or B row): rows r, r+1 share a 256-byte
 // bank row, so XOR bits 1..3 of r -> 16 consecutive rows x one chunk = 16 distinct bank slots
 __device__ __forceinline__ int sw8(int r) { return (r >> 1) & 7; }
+
+// Window pixels are 160 bytes apart in LDS (the 128 bytes of a 64-channel chunk + 32 bytes of
+// padding): 16 lanes reading 16 consecutive pixels then hit 16 distinct bank slots for ANY first
+// pixel (a pure XOR swizzle of 128-byte pixels is 2-way conflicted when the run starts at an odd
+// or 2 mod 4 pixel), and a fragment address is one add: lane base + the tap's pixel offset x 160.
+constexpr int PIXS = 10;          // 16-byte slots per window pixel
+constexpr int PIXB = PIXS * 16;
 
 template <int S>
 __device__ __forceinline__ int kn_swz(int r) {  // as igemm3.hip (k-major B rows of S bytes)
@@ -150,11 +160,18 @@ __device__ __forceinline__ f32x4 unpack4(uint2 u) {
   return (f32x4){(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 
-__device__ __forceinline__ float red16(float v) {  // sum over the 16 lanes of a row (lane & 15)
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+
+// sum over the 16 lanes of a DPP row (lane & 15), every lane gets it: quad_perm xor 1 / xor 2,
+// then row_half_mirror and row_mirror -- VALU only (__shfl_xor lowers to LDS permutes here)
+__device__ __forceinline__ float red16(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
   return v;
 }
 
@@ -318,10 +335,10 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       const uint32_t dst0 = lbase + win0 + (uint32_t)buf * a.win_bytes;
       for (int q = q0 + lid; q < q1; q += NL, ++n) {
         const int L = q * 64 + lane;
-        const int P = L >> 3;
-        const int j = (L & 7) ^ sw8(P);
+        const int P = L / PIXS;
+        const int j = L - P * PIXS;  // 8, 9: padding slots (zero-filled)
         uint32_t off = OOB;
-        if (P < a.wpix) {
+        if (P < a.wpix && j < 8) {
           const int bl = (int)fdiv((uint32_t)P, a.fd_wimg);
           const int rem = P - bl * a.WY * a.WXP;
           const int wy = (int)fdiv((uint32_t)rem, a.fd_wxp);
@@ -378,6 +395,8 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       return n;
     };
 
+    unsigned long long* st = (a.stamps && lid == 0 && lane == 0) ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
+    if (st) st[4] = __builtin_amdgcn_s_memtime();
     Cur ki;
     cur_init<NSB>(ki, q);
     int cnt[NSB];
@@ -390,7 +409,9 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     // stages 0 and 1 (and window 0) landed at barrier 0
     if constexpr (NSB == 4) wvm_dyn(cnt[2]);
     else wvm<0>();
-    barrier();
+    if (st) st[5] = __builtin_amdgcn_s_memtime();
+    barrier_study(a.ablate);
+    if (st) st[6] = __builtin_amdgcn_s_memtime();
     for (int s = 0; s + 1 < S_; ++s) {
       const int x = s + NSB - 1;
       int cx = 0;
@@ -398,8 +419,9 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       // stage s+2 landed at barrier s+1 (stage s+3 = x may stay in flight when NSB = 4)
       if constexpr (NSB == 4) wvm_dyn(cx);
       else wvm<0>();
-      barrier();
+      barrier_study(a.ablate);
     }
+    if (st) st[7] = __builtin_amdgcn_s_memtime();
     wvm<0>();
     return;
   }
@@ -408,8 +430,9 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
   const int wm = wave / WNC, wn = wave % WNC;
   const int fr = lane & 15, fq = lane >> 4;
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  // window pixel of each activation-fragment row of this lane at tap offset 0
-  int pbase[FM];
+  // LDS byte offset (in a window buffer, tap offset 0) of each activation fragment of this lane:
+  // window pixel of the fragment row x 160 + the lane's 16-byte k chunk
+  int pb[FM];
 #pragma unroll
   for (int im = 0; im < FM; ++im) {
     const int ml = wm * TM + im * 16 + fr;
@@ -417,7 +440,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     const int rem = ml - bl * a.TR * a.Wq;
     const int ty = (int)fdiv((uint32_t)rem, a.fd_wq);
     const int x = rem - ty * a.Wq;
-    pbase[im] = (bl * a.WY + a.S * ty) * a.WXP + x;
+    pb[im] = ((bl * a.WY + a.S * ty) * a.WXP + x) * PIXB + fq * 16;
   }
   // BKN = 0: weight-fragment row byte offsets in a stage (chunk fq of row r, XOR-swizzled)
   int wrow[FN];
@@ -435,14 +458,11 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
 
   // fragments of k-half h (32 of the 64 k rows) of the step at cursor k
   auto read_frags = [&](int h, const Cur& k, int slot, elem8 (&af)[FM], elem8 (&wf)[FN]) {
-    const lds_char* wb = l3 + win0 + (uint32_t)(a.nwb == 2 ? k.wl & 1 : 0) * a.win_bytes;
-    const int toff = tap_of(vt0, vt1, k.p, k.t) & 0xffff;
+    const int toff = tap_of(vt0, vt1, k.p, max(k.t, 0)) & 0xffff;
+    // wave-uniform part: window buffer + tap offset + k half (scalar)
+    const lds_char* wb = l3 + win0 + (uint32_t)(a.nwb == 2 ? k.wl & 1 : 0) * a.win_bytes + toff * PIXB + h * 64;
 #pragma unroll
-    for (int im = 0; im < FM; ++im) {
-      const int P = pbase[im] + toff;
-      const uint32_t o = (uint32_t)(P * 128 + ((fq ^ sw8(P)) << 4)) ^ (uint32_t)(h * 64);
-      af[im] = *LDS_PTR(const elem8, wb + o);
-    }
+    for (int im = 0; im < FM; ++im) af[im] = *LDS_PTR(const elem8, wb + pb[im]);
     const lds_char* sb = l3 + slot * BSTAGE;
     if constexpr (BKN) {
 #pragma unroll
@@ -471,6 +491,13 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     __builtin_amdgcn_s_setprio(0);
   };
   auto epilogue = [&](int p) {
+    if (a.ablate & 4) {  // timing study: no epilogue (keep the accumulators live)
+#pragma unroll
+      for (int jn = 0; jn < FN; ++jn)
+#pragma unroll
+        for (int im = 0; im < FM; ++im) asm volatile("" ::"v"(acc[jn][im]));
+      return;
+    }
 #define DCG_IG4_EPI(ACT_, EPI_) \
   ig4_epilogue<FM, FN, TM, TN, WMC, BN, ACT_, EPI_>(acc, a, p, mt, m0, n0, b0, y0, wm, wn, fr, fq, part, ctr)
     if (a.bnb_x) {
@@ -491,30 +518,39 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       for (int im = 0; im < FM; ++im) acc[jn][im] = (f32x4){0.f, 0.f, 0.f, 0.f};
   };
 
+  unsigned long long* stc = (a.stamps && wave == 0 && lane == 0) ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  if (stc) stc[0] = __builtin_amdgcn_s_memtime();
   Cur k, k1;
   cur_init<NSB>(k, q);
   k1 = k;
   cur_next<NSB>(k1, q);
   elem8 a0[FM], w0[FN], a1[FM], w1[FN];
-  barrier();  // B_0: stages 0, 1 and window 0 landed
-  bool have0 = false;  // the first k-half of step s was read ahead (during step s-1)
-  if (k.t >= 0 && !(a.ablate & 1)) { read_frags(0, k, 0, a0, w0); have0 = true; }
+  barrier_study(a.ablate);  // B_0: stages 0, 1 and window 0 landed
+  if (stc) stc[1] = __builtin_amdgcn_s_memtime();
+  const bool study_nomfma = (a.ablate & 1) != 0;
+  // every step ends by reading the first k-half of the NEXT step (stage s+1 landed at B_s); for
+  // the last step, or ahead of empty steps, the read is clamped to the current step (unused).
+  // Empty steps do the same, so the first real step after them finds its fragments ready.
+  if (!study_nomfma) read_frags(0, k, 0, a0, w0);
   for (int s = 0; s < S_; ++s) {
-    if (s > 0) barrier();  // B_s: stage s+1 landed, every compute wave done with step s-1
-    if (k.t >= 0 && (a.ablate & 1)) {  // timing study: no fragment reads / MFMAs
-      if (k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1) epilogue(k.p);
+    if (s > 0) barrier_study(a.ablate);  // B_s: stage s+1 landed, every compute wave done with step s-1
+    const bool nxt = s + 1 < S_ && k1.t >= 0;
+    const Cur kp = nxt ? k1 : k;
+    const int slotp = (nxt ? s + 1 : s) % NSB;
+    if (study_nomfma) {  // timing study: no fragment reads / MFMAs
+      if (k.t >= 0 && k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1) epilogue(k.p);
     } else if (k.t >= 0) {
-      if (!have0) read_frags(0, k, s % NSB, a0, w0);  // first step after empty steps
       read_frags(1, k, s % NSB, a1, w1);
       mfmas(a0, w0);
-      const bool phase_end = k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1;
-      have0 = s + 1 < S_ && k1.t >= 0;
-      if (have0 && !phase_end) read_frags(0, k1, (s + 1) % NSB, a0, w0);
+      read_frags(0, kp, slotp, a0, w0);
       mfmas(a1, w1);
-      if (phase_end) {  // (the next step's first fragments after the epilogue: fewer live registers)
+      if (k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1) {
+        if (stc) stc[2] = __builtin_amdgcn_s_memtime();
         epilogue(k.p);
-        if (have0) read_frags(0, k1, (s + 1) % NSB, a0, w0);
+        if (stc) stc[3] = __builtin_amdgcn_s_memtime();
       }
+    } else {
+      read_frags(0, kp, slotp, a0, w0);
     }
     k = k1;
     cur_next<NSB>(k1, q);

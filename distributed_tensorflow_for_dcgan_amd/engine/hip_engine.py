@@ -1376,6 +1376,22 @@ class HipEngine:
         """Call after loading weights/slots from a checkpoint: refresh the 16-bit weight mirrors."""
         self._repack_weights_now()
 
+    def placement(self) -> List[str]:
+        """--log_device_placement lines: every recorded op of the step runs on this rank's HIP
+        device; which stream slots / graphs carry it."""
+        progs = [("forward+G backward", self.progA), ("D backward", self.progB), ("G weight grads", self.progW),
+                 ("optimisers", self.progC)]
+        out = ["HIP engine (%s): %d kernels per step, schedule %s, hipGraph %s%s" % (
+            self.dtype_name, self.kernel_count(), self._schedule(), "captured" if self.graph_enabled else
+            ("requested" if self.graph_requested else "off"),
+            ", comm stream for all-reduces" if self.ddp else "")]
+        for label, p in progs:
+            if p is None:
+                continue
+            slots = sorted({p.op_info(i)[1] for i in range(p.size())})
+            out.append("  %-20s %3d ops on %s, stream slots %s" % (label, p.size(), self.device, slots))
+        return out
+
     def op_names(self) -> List[str]:
         out = []
         for p in (self.progA, self.progB, self.progW, self.progC):

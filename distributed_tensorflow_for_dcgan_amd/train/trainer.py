@@ -18,7 +18,7 @@ import os
 import pprint
 import sys
 import time
-from typing import Optional
+from typing import List, Optional
 
 import numpy as np
 import torch
@@ -31,7 +31,7 @@ from ..obs import images as IM
 from ..obs import summaries as SUM
 from ..obs.events import SummaryWriter
 from ..parallel import dist as D
-from ..utils.flags import Flags, cluster_from_flags
+from ..utils.flags import Flags, apply_dataset_preset, cluster_from_flags
 
 STEP_LINE = "Epoch: [%2d] step: [%2d] time: %4.4f, d_loss: %.8f, g_loss: %.8f"
 SYNC_EVERY = 10  # steps between collective checks of the chief's time-based save decision
@@ -92,9 +92,36 @@ def _device(flags: Flags, local_rank: int) -> torch.device:
     return torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
 
 
+def placement_report(engine, device, rank: int, world: int) -> List[str]:
+    """--log_device_placement (reference ``image_train.py:36``, defined there but never passed to
+    a session): where this rank's work runs -- the TF-style device name, the HIP device, the
+    process group, and the engine's streams / graphs."""
+    lines = []
+    if device.type == "cuda":
+        pr = torch.cuda.get_device_properties(device)
+        lines.append("/job:worker/replica:0/task:%d/device:GPU:%d -> HIP device %d: %s, %d CUs, %.0f GiB, arch %s"
+                     % (rank, device.index or 0, device.index or 0, pr.name, pr.multi_processor_count,
+                        pr.total_memory / 2 ** 30, getattr(pr, "gcnArchName", "?")))
+    else:
+        lines.append("/job:worker/replica:0/task:%d/device:CPU:0 -> host CPU" % rank)
+    if D.is_initialized():
+        import torch.distributed as tdist
+        lines.append("process group: backend %s, rank %d of %d" % (tdist.get_backend(), rank, tdist.get_world_size()))
+    else:
+        lines.append("process group: none (single process, world %d)" % world)
+    rep = getattr(engine, "placement", None)
+    if callable(rep):
+        lines.extend(rep())
+    return ["[placement] " + l for l in lines]
+
+
 def run(flags: Flags, out=None) -> int:
     out = sys.stdout if out is None else out
+    preset = apply_dataset_preset(flags)
     pprint.pprint(flags.as_dict(), stream=out)
+    if preset:
+        print("--dataset=%s preset: %s" % (flags.dataset, ", ".join("%s=%s" % kv for kv in sorted(preset.items()))),
+              file=out)
     if flags.job_name == "ps":
         print("--job_name=ps: this framework trains with synchronous data parallelism over RCCL; "
               "there is no parameter server to run. Launch one worker per GPU instead "
@@ -124,6 +151,9 @@ def run(flags: Flags, out=None) -> int:
                           world=world, graph=bool(flags.graph), allreduce_dtype=flags.allreduce_dtype,
                           lr=float(flags.learning_rate), beta1=float(flags.beta1),
                           zero_debias=bool(flags.bn_zero_debias), bucket_mb=float(flags.bucket_mb))
+    if flags.log_device_placement:
+        for line in placement_report(engine, device, rank, world):
+            print(line, file=out, flush=True)
     ckpt = CheckpointManager(flags.checkpoint_dir, keep=int(flags.keep_checkpoints),
                              save_secs=float(flags.save_model_secs))
     info = ckpt.restore_latest(engine)

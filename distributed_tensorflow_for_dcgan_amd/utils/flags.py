@@ -164,6 +164,35 @@ def parse_flags(argv: Optional[Sequence[str]] = None,
     return Flags(vars(ns), explicit)
 
 
+# --dataset presets (carpedm20/DCGAN-tensorflow naming, which the reference's flag help lists:
+# "celebA, mnist, lsun"): image shape for the flags the command line did not set, and the
+# ``data/<dataset>`` directory when --data_dir is left at its default and that directory exists.
+DATASET_PRESETS: Dict[str, Dict[str, Any]] = {
+    "celebA": {"output_size": 64, "c_dim": 3},
+    "lsun": {"output_size": 64, "c_dim": 3},
+    "mnist": {"output_size": 28, "c_dim": 1},
+    "cifar10": {"output_size": 32, "c_dim": 3},
+}
+
+
+def apply_dataset_preset(flags: Flags) -> Dict[str, Any]:
+    """Apply the --dataset preset in place; returns what it changed (name -> value). Unknown
+    names are kept (they label checkpoints / logs) and change nothing."""
+    changed: Dict[str, Any] = {}
+    name = str(flags.dataset)
+    preset = DATASET_PRESETS.get(name) or {k.lower(): v for k, v in DATASET_PRESETS.items()}.get(name.lower())
+    for k, v in (preset or {}).items():
+        if not flags.explicitly_set(k) and getattr(flags, k) != v:
+            setattr(flags, k, v)
+            changed[k] = v
+    if not flags.explicitly_set("data_dir"):
+        d = os.path.join("data", name)
+        if not os.path.isdir(flags.data_dir) and os.path.isdir(d):
+            flags.data_dir = d
+            changed["data_dir"] = d
+    return changed
+
+
 def default_flags(**overrides: Any) -> Flags:
     values = {name: default for name, _, default, _ in ALL_FLAGS}
     for k, v in overrides.items():

@@ -72,3 +72,36 @@ def test_bad_job_name():
     from distributed_tensorflow_for_dcgan_amd.train.trainer import run
     with pytest.raises(SystemExit):
         run(F.parse_flags(["--job_name=chief"]))
+
+
+def test_dataset_preset(tmp_path, monkeypatch):
+    """--dataset (reference image_train.py:19, read nowhere there): the named preset sets the image
+    shape the command line left at its default, never an explicit flag; unknown names are labels."""
+    fl = F.parse_flags(["--dataset=mnist"])
+    assert F.apply_dataset_preset(fl) == {"output_size": 28, "c_dim": 1}
+    assert (fl.output_size, fl.c_dim) == (28, 1)
+    fl = F.parse_flags(["--dataset=mnist", "--output_size=32"])
+    assert F.apply_dataset_preset(fl) == {"c_dim": 1} and fl.output_size == 32
+    fl = F.parse_flags([])  # celebA: the reference shape, nothing to change
+    assert F.apply_dataset_preset(fl) == {} and (fl.output_size, fl.c_dim) == (64, 3)
+    fl = F.parse_flags(["--dataset=my_faces"])
+    assert F.apply_dataset_preset(fl) == {}
+    # data/<dataset> (carpedm20 layout) when --data_dir is left at a missing default
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "data" / "lsun").mkdir(parents=True)
+    fl = F.parse_flags(["--dataset=lsun"])
+    assert F.apply_dataset_preset(fl) == {"data_dir": "data/lsun"} and fl.data_dir == "data/lsun"
+
+
+def test_log_device_placement_report(tmp_path, capsys):
+    """--log_device_placement (reference image_train.py:36, default True, never used there): each
+    rank prints where its work runs; --nolog_device_placement silences it."""
+    from distributed_tensorflow_for_dcgan_amd.train import trainer
+    base = ["--synthetic", "--max_steps=1", "--batch_size=4", "--output_size=28", "--c_dim=1", "--engine=reference",
+            "--device=cpu", "--checkpoint_dir=%s" % (tmp_path / "ck"), "--sample_dir=%s" % (tmp_path / "s"),
+            "--nosummaries", "--sample_every=0"]
+    assert trainer.run(F.parse_flags(base)) == 0
+    out = capsys.readouterr().out
+    assert "[placement] /job:worker/replica:0/task:0/device:CPU:0" in out and "[placement] process group" in out
+    assert trainer.run(F.parse_flags(base + ["--nolog_device_placement"])) == 0
+    assert "[placement]" not in capsys.readouterr().out
