@@ -20,6 +20,9 @@ template <int N_> __device__ __forceinline__ void wvm() { asm volatile("s_waitcn
 
 // PAT 0: 1 KiB contiguous per piece; 1: 64 B of each of 16 lines (stride 128); 2: 32 B of 32 lines;
 // 3: like 2 but 4 consecutive pieces cover the 4 quarters of the same 32 lines (L1 reuse)
+// 4: lockstep -- every block walks the SAME piece sequence (all CUs streaming one weight matrix
+//    in the same K order, as a conv GEMM's B operand does); 5: like 4 with the sequence rotated
+//    by a per-block offset (the K-step order staggered over workgroups)
 template <int PAT, int DEPTH>
 __global__ void dma_kernel(const char* src, uint32_t span, int iters, int* sink) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -34,6 +37,8 @@ __global__ void dma_kernel(const char* src, uint32_t span, int iters, int* sink)
     if (PAT == 0) off = (q * 1024u) % span + lane * 16;
     else if (PAT == 1) off = (q * 2048u) % span + (lane >> 2) * 128 + (lane & 3) * 16;
     else if (PAT == 2) off = (q * 4096u) % span + (lane >> 1) * 128 + (lane & 1) * 16;
+    else if (PAT == 4) off = (((uint32_t)i * nw + wave) * 1024u) % span + lane * 16;
+    else if (PAT == 5) off = (((uint32_t)i * nw + wave + blockIdx.x * 16u) * 1024u) % span + lane * 16;
     else { const uint32_t g = gid * 7919u + (uint32_t)(i >> 2) * 131u; off = (g * 4096u) % span + (lane >> 1) * 128 + (lane & 1) * 16 + (i & 3) * 32; }
     dma16(r, lbase + (i % DEPTH) * 1024, off);
     wvm<DEPTH - 1>();
@@ -65,10 +70,17 @@ int run(const char* src, uint32_t span, int waves, int blocks, const char* tag) 
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   char* src; const size_t big = (size_t)1 << 30;
   CK(hipMalloc(&src, big)); CK(hipMemset(src, 1, big));
   const uint32_t l2 = 2u << 20, hbm = (uint32_t)big;
+  if (argc > 1) {  // lockstep study: one 400 KiB weight matrix streamed by every CU
+    const uint32_t w = 400u << 10;
+    run<0, 8>(src, w, 4, 256, "W400"); run<4, 8>(src, w, 4, 256, "W400"); run<5, 8>(src, w, 4, 256, "W400");
+    run<0, 8>(src, w, 4, 512, "W400"); run<4, 8>(src, w, 4, 512, "W400"); run<5, 8>(src, w, 4, 512, "W400");
+    run<4, 16>(src, w, 4, 256, "W400"); run<5, 16>(src, w, 4, 256, "W400");
+    return 0;
+  }
   for (uint32_t span : {l2, hbm}) {
     const char* tag = span == l2 ? "L2" : "HBM";
     run<0, 4>(src, span, 4, 256, tag); run<0, 8>(src, span, 4, 256, tag); run<0, 16>(src, span, 4, 256, tag);

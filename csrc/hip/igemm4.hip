@@ -139,7 +139,22 @@ __device__ __forceinline__ void cur_next(Cur& k, const Sched& q) {
 // 64 + i of the flat [4][25] table (v_readlane: no memory access in the K loop)
 __device__ __forceinline__ int tap_of(int v0, int v1, int p, int t) {
   const int i = p * 25 + t;
-  return i < 64 ? __builtin_amdgcn_readlane(v0, i) : __builtin_amdgcn_readlane(v1, i - 64);
+  // both lanes read, then a scalar select: no branch splits the K-loop body's basic block
+  const int x0 = __builtin_amdgcn_readlane(v0, i & 63);
+  const int x1 = __builtin_amdgcn_readlane(v1, max(i - 64, 0));
+  return i < 64 ? x0 : x1;
+}
+
+// scheduling recipe of an MFMA cluster (NM MFMAs) and NR fragment reads for the next one:
+// read / MFMA alternate until the reads are out, then the remaining MFMAs
+template <int NM, int NR>
+__device__ __forceinline__ void interleave() {
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
 }
 
 template <int ACT>
@@ -208,39 +223,40 @@ __device__ __forceinline__ void ig4_epilogue(f32x4 (&acc)[FN][FM], const IG4Args
       mu = *reinterpret_cast<const f32x4*>(a.bnb_mean + g * a.N + n);
       rs = *reinterpret_cast<const f32x4*>(a.bnb_rstd + g * a.N + n);
     }
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int im = 0; im < FM; ++im) {
       const f32x4 v = acc[jn][im] + bv;
-      f32x4 vs;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) vs[r] = (float)f2bf(v[r]);  // statistics of exactly the stored tensor
+      // the stored (rounded) values; statistics are of exactly the stored tensor
+      const uint2 pv = ig4::pack4(v[0], v[1], v[2], v[3]);
+      const f32x4 vs = ig4::unpack4(pv);
       elem_t* dst = a.C + off[im] + n;
       if constexpr (EPI == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { s[r] += vs[r]; s2[r] += vs[r] * vs[r]; }
-        *reinterpret_cast<uint2*>(dst) = ig4::pack4(ig4::act_f<ACT>(v[0], a.leak), ig4::act_f<ACT>(v[1], a.leak),
-                                                    ig4::act_f<ACT>(v[2], a.leak), ig4::act_f<ACT>(v[3], a.leak));
+        s += vs;
+        s2 += vs * vs;
+        if constexpr (ACT == ACT_NONE) {
+          *reinterpret_cast<uint2*>(dst) = pv;
+        } else {
+          *reinterpret_cast<uint2*>(dst) = ig4::pack4(ig4::act_f<ACT>(v[0], a.leak), ig4::act_f<ACT>(v[1], a.leak),
+                                                      ig4::act_f<ACT>(v[2], a.leak), ig4::act_f<ACT>(v[3], a.leak));
+        }
       } else if constexpr (EPI == 1) {
         const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
         const f32x4 xv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_x + off[im] + n));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gv = vs[r] * (yv[r] > 0.f ? 1.f : slope);
-          s[r] += gv;
-          s2[r] += gv * (xv[r] - mu[r]) * rs[r];
-        }
-        *reinterpret_cast<uint2*>(dst) = ig4::pack4(vs[0], vs[1], vs[2], vs[3]);
-      } else {
-        const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
         f32x4 gv;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = a.bnb_act == ACT_TANH ? 1.f - yv[r] * yv[r] : (yv[r] > 0.f ? 1.f : slope);
-          gv[r] = (float)f2bf(vs[r] * d);
-          s[r] += gv[r];
-        }
-        *reinterpret_cast<uint2*>(dst) = ig4::pack4(gv[0], gv[1], gv[2], gv[3]);
+        for (int r = 0; r < 4; ++r) gv[r] = vs[r] * (yv[r] > 0.f ? 1.f : slope);
+        s += gv;
+        s2 += gv * (xv - mu) * rs;
+        *reinterpret_cast<uint2*>(dst) = pv;
+      } else {
+        const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
+        f32x4 d;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r] = a.bnb_act == ACT_TANH ? 1.f - yv[r] * yv[r] : (yv[r] > 0.f ? 1.f : slope);
+        const uint2 pg = ig4::pack4(vs[0] * d[0], vs[1] * d[1], vs[2] * d[2], vs[3] * d[3]);
+        s += ig4::unpack4(pg);
+        *reinterpret_cast<uint2*>(dst) = pg;
       }
     }
     if (do_stats) {
@@ -323,36 +339,37 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
 
   if (tid < 64 && lane < WNC) ctr[lane] = 0;
 
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a.a_bytes);
+// window pieces [q0, q1) of chunk `ch` into window buffer `buf`: wave `wid` of `nw` takes q = wid mod nw
+  auto issue_win_w = [&](int q0, int q1, int buf, int ch, int wid, int nw) -> int {
+    int n = 0;
+    const uint32_t dst0 = lbase + win0 + (uint32_t)buf * a.win_bytes;
+    for (int q = q0 + wid; q < q1; q += nw, ++n) {
+      const int L = q * 64 + lane;
+      const int P = L / PIXS;
+      const int j = L - P * PIXS;  // 8, 9: padding slots (zero-filled)
+      uint32_t off = OOB;
+      if (P < a.wpix && j < 8) {
+        const int bl = (int)fdiv((uint32_t)P, a.fd_wimg);
+        const int rem = P - bl * a.WY * a.WXP;
+        const int wy = (int)fdiv((uint32_t)rem, a.fd_wxp);
+        const int X = rem - wy * a.WXP;
+        const int wx = a.S == 2 ? (X < a.HX ? 2 * X : 2 * (X - a.HX) + 1) : X;
+        const int iy = y0 * a.S + a.win_oy + wy, ix = a.win_ox + wx;
+        const int b = b0 + bl;
+        if (wx < a.WX && b < a.Bn && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+          off = (uint32_t)((((b * a.H + iy) * a.W + ix) * a.Kc + ch * 64 + j * 8) * 2);
+      }
+      dma16_asm_la(ra, dst0 + q * 1024, off);
+    }
+    return n;
+  };
   if (wave >= NC) {
     // =============================================================== loader waves
     const int lid = wave - NC;
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a.a_bytes);
     const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.Bw, a.b_bytes);
     const int Kc = a.Kc, N = a.N;
-    // window pieces [q0, q1) of chunk `ch` into window buffer `buf`: this loader takes q = lid mod NL
-    auto issue_win = [&](int q0, int q1, int buf, int ch) -> int {
-      int n = 0;
-      const uint32_t dst0 = lbase + win0 + (uint32_t)buf * a.win_bytes;
-      for (int q = q0 + lid; q < q1; q += NL, ++n) {
-        const int L = q * 64 + lane;
-        const int P = L / PIXS;
-        const int j = L - P * PIXS;  // 8, 9: padding slots (zero-filled)
-        uint32_t off = OOB;
-        if (P < a.wpix && j < 8) {
-          const int bl = (int)fdiv((uint32_t)P, a.fd_wimg);
-          const int rem = P - bl * a.WY * a.WXP;
-          const int wy = (int)fdiv((uint32_t)rem, a.fd_wxp);
-          const int X = rem - wy * a.WXP;
-          const int wx = a.S == 2 ? (X < a.HX ? 2 * X : 2 * (X - a.HX) + 1) : X;
-          const int iy = y0 * a.S + a.win_oy + wy, ix = a.win_ox + wx;
-          const int b = b0 + bl;
-          if (wx < a.WX && b < a.Bn && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-            off = (uint32_t)((((b * a.H + iy) * a.W + ix) * Kc + ch * 64 + j * 8) * 2);
-        }
-        dma16_asm_la(ra, dst0 + q * 1024, off);
-      }
-      return n;
-    };
+    auto issue_win = [&](int q0, int q1, int buf, int ch) -> int { return issue_win_w(q0, q1, buf, ch, lid, NL); };
     // B pieces of step k (one 64-deep k slice of weight tap wt) into ring slot `slot`
     auto issue_b = [&](const Cur& k, int slot) {
       const int wt = tap_of(vt0, vt1, k.p, k.t) >> 16;
@@ -400,7 +417,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     Cur ki;
     cur_init<NSB>(ki, q);
     int cnt[NSB];
-    if (!(a.ablate & 2)) issue_win(0, a.npw, 0, 0);
+    if (!(a.ablate & 2)) issue_win_w(0, a.npw, 0, 0, wave, NC + NL);  // window 0: every wave issues a share
 #pragma unroll
     for (int x = 0; x < NSB - 1; ++x) {
       cnt[x] = 0;
@@ -457,10 +474,16 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     for (int im = 0; im < FM; ++im) acc[jn][im] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // fragments of k-half h (32 of the 64 k rows) of the step at cursor k
+  const int win_bytes = __builtin_amdgcn_readfirstlane(a.win_bytes);
+  const int wl_mask = __builtin_amdgcn_readfirstlane(a.nwb == 2 ? 1 : 0);
   auto read_frags = [&](int h, const Cur& k, int slot, elem8 (&af)[FM], elem8 (&wf)[FN]) {
-    const int toff = tap_of(vt0, vt1, k.p, max(k.t, 0)) & 0xffff;
-    // wave-uniform part: window buffer + tap offset + k half (scalar)
-    const lds_char* wb = l3 + win0 + (uint32_t)(a.nwb == 2 ? k.wl & 1 : 0) * a.win_bytes + toff * PIXB + h * 64;
+    // wave-uniform part (window buffer + tap offset + k half) computed in SGPRs (the cursor
+    // fields are pinned scalar: a select of them in VGPRs cost a v_mul_lo_u32 per read block)
+    const int kp_ = __builtin_amdgcn_readfirstlane(k.p), kt_ = __builtin_amdgcn_readfirstlane(k.t);
+    const int kwl = __builtin_amdgcn_readfirstlane(k.wl);
+    const int toff = tap_of(vt0, vt1, kp_, max(kt_, 0)) & 0xffff;
+    const int uoff = (int)win0 + (kwl & wl_mask) * win_bytes + toff * PIXB + h * 64;
+    const lds_char* wb = l3 + uoff;
 #pragma unroll
     for (int im = 0; im < FM; ++im) af[im] = *LDS_PTR(const elem8, wb + pb[im]);
     const lds_char* sb = l3 + slot * BSTAGE;
@@ -482,13 +505,13 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       for (int jn = 0; jn < FN; ++jn) wf[jn] = *LDS_PTR(const elem8, sb + (wrow[jn] ^ (h * 64)));
     }
   };
+  // (no s_setprio around the MFMAs: with one compute wave per SIMD the cluster form serialises
+  // the fragment reads / address adds behind the matrix pipe; left free, hipcc interleaves them)
   auto mfmas = [&](const elem8 (&af)[FM], const elem8 (&wf)[FN]) {
-    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int jn = 0; jn < FN; ++jn)
 #pragma unroll
       for (int im = 0; im < FM; ++im) acc[jn][im] = DCG_MFMA_16x16x32(wf[jn], af[im], acc[jn][im], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
   };
   auto epilogue = [&](int p) {
     if (a.ablate & 4) {  // timing study: no epilogue (keep the accumulators live)
@@ -520,6 +543,11 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
 
   unsigned long long* stc = (a.stamps && wave == 0 && lane == 0) ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
   if (stc) stc[0] = __builtin_amdgcn_s_memtime();
+  // the compute waves' share of window 0 (they are idle until barrier 0 anyway)
+  if (!(a.ablate & 2)) {
+    issue_win_w(0, a.npw, 0, 0, wave, NC + NL);
+    ig4::wvm<0>();
+  }
   Cur k, k1;
   cur_init<NSB>(k, q);
   k1 = k;
@@ -532,28 +560,37 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
   // the last step, or ahead of empty steps, the read is clamped to the current step (unused).
   // Empty steps do the same, so the first real step after them finds its fragments ready.
   if (!study_nomfma) read_frags(0, k, 0, a0, w0);
-  for (int s = 0; s < S_; ++s) {
-    if (s > 0) barrier_study(a.ablate);  // B_s: stage s+1 landed, every compute wave done with step s-1
-    const bool nxt = s + 1 < S_ && k1.t >= 0;
-    const Cur kp = nxt ? k1 : k;
-    const int slotp = (nxt ? s + 1 : s) % NSB;
-    if (study_nomfma) {  // timing study: no fragment reads / MFMAs
-      if (k.t >= 0 && k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1) epilogue(k.p);
-    } else if (k.t >= 0) {
-      read_frags(1, k, s % NSB, a1, w1);
-      mfmas(a0, w0);
-      read_frags(0, kp, slotp, a0, w0);
-      mfmas(a1, w1);
-      if (k.t == q.ntaps(k.p) - 1 && k.c == q.nch - 1) {
-        if (stc) stc[2] = __builtin_amdgcn_s_memtime();
-        epilogue(k.p);
-        if (stc) stc[3] = __builtin_amdgcn_s_memtime();
+  // phases outer, steps inner: the epilogue code sits between the loops, so the hot loop body
+  // stays a few hundred bytes of code (inlined into the step loop, the epilogue variants spread
+  // every iteration over tens of KiB: instruction-cache misses cost more than the MFMAs)
+  int s = 0;
+  for (int p = 0; p < q.nph; ++p) {
+    for (; s < S_ && k.p == p; ++s) {
+      if (s > 0) barrier_study(a.ablate);  // B_s: stage s+1 landed, every compute wave done with step s-1
+      const bool nxt = s + 1 < S_ && k1.t >= 0;
+      const Cur kp = nxt ? k1 : k;
+      const int slotp = (nxt ? s + 1 : s) % NSB;
+      if (!study_nomfma) {
+        // the k-half-1 fragment reads are interleaved with the first MFMA cluster (they land
+        // long before the second needs them): one compute wave per SIMD, so an un-interleaved
+        // read / address block would leave the matrix core idle. The next step's k-half-0 reads
+        // run on every path (an empty step's are what the first real step after it consumes):
+        // one definition of a0 / w0, so no register copies at the join.
+        const bool real = k.t >= 0;
+        if (real) {
+          read_frags(1, k, s % NSB, a1, w1);
+          mfmas(a0, w0);
+          ig4::interleave<FM * FN, FM + FN>();
+        }
+        read_frags(0, kp, slotp, a0, w0);
+        if (real) mfmas(a1, w1);
       }
-    } else {
-      read_frags(0, kp, slotp, a0, w0);
+      k = k1;
+      cur_next<NSB>(k1, q);
     }
-    k = k1;
-    cur_next<NSB>(k1, q);
+    if (stc) stc[2] = __builtin_amdgcn_s_memtime();
+    epilogue(p);
+    if (stc) stc[3] = __builtin_amdgcn_s_memtime();
   }
 }
 
