@@ -3,7 +3,7 @@
 
 For every conv-shaped GEMM of the DCGAN training step (D forward on 2B, D dgrads, G forward,
 G dgrads, at per-GPU batch B) time every tile configuration -- igemm.hip (both staging
-variants), igemm3.hip (every tile, 2..5 LDS stages, split-K 1..8) and igemmh.hip (halo window,
+variants), igemm3.hip (every tile, 2..5 LDS stages, split-K 1..8) and igemm4.hip (halo window,
 every tile that fits) with the weight layout
 the engine reads for that GEMM -- in ONE process, interleaved (guide §5.4 rule 24), and
 report TF/s. ``--write`` stores the fastest "cfg:splits" per shape in ops/igemm_tuned.json,
@@ -69,13 +69,6 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     phases = 4 if mode == 1 else 1
     M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
     kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
-    if mode in (0, 1) and N % 64 == 0:  # igemmh: halo window in LDS
-        for c in range(400, 430):
-            if H.igemmh_shm(c, mode, Hout, Wout, Kc) is None:
-                continue
-            if H.IGEMMH_TILES[c % 10][1] > N:
-                continue
-            out.append((c, 1))
     if mode in (0, 1) and IG4:  # igemm4: halo window + loader waves (geometry checked per shape)
         pad = same_pads(Hout)[0] if mode == 1 else same_pads(2 * Hout)[0]
         for c in range(500, 520):

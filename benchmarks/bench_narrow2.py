@@ -34,13 +34,11 @@ def main():
         w = (torch.rand(5, 5, 3, 64, device=dev) * 0.1).to(torch.bfloat16)
         bias = torch.rand(64, device=dev)
         y = torch.empty(B, 32, 32, 64, device=dev, dtype=torch.bfloat16)
-        p_old = ext.Program()
-        p_old.conv3_direct("c3", H._p(x), H._p(w), H._p(bias), H._p(y), B, 64, 64, 3, 32, 32, 64, 1, 1, 2, 0.2, 0)
         p_new = ext.Program()
         grid = H.nconv_grid(p_new, B, 32, 32)
         p_new.nconv("nc", H._p(x), H._p(w), H._p(bias), H._p(y), B, 64, 64, 3, 32, 32, 1, 1, 2, 0.2, grid,
                     0, 0, 0, 0, 0, 0.2, 0, 0)
-        res[name] = {"conv3_direct_us": timeit(p_old, a.reps), "nconv_us": timeit(p_new, a.reps)}
+        res[name] = {"nconv_us": timeit(p_new, a.reps)}
         if name.startswith("G4"):
             bx = torch.rand(B, 32, 32, 64, device=dev).to(torch.bfloat16)
             st = torch.rand(64, device=dev)

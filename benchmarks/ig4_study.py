@@ -72,28 +72,31 @@ def main():
                 e1.record(s)
                 times[c].append((e0, e1))
         torch.cuda.synchronize()
-        if a.stamps:  # one extra launch per igemm4 cfg (ablate 0) with stamps on
+        if a.stamps:  # one extra launch per igemm4 cfg and ablation with stamps on
             for c in cands:
-                if c[0] < 500 or c[2] != 0:
+                if c[0] < 500:
                     continue
                 st = torch.zeros(1 << 20, dtype=torch.int64, device=dev)
                 os.environ["DCGAN_IGEMM_STAMPS"] = str(st.data_ptr())
+                os.environ["DCGAN_IGEMM_ABLATE"] = str(c[2])
                 p = ext.Program()
                 p.igemm_ex(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad,
                            pad, c[0], 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn, -1, 1)
                 os.environ.pop("DCGAN_IGEMM_STAMPS")
+                os.environ.pop("DCGAN_IGEMM_ABLATE")
                 H.run(p)
                 torch.cuda.synchronize()
                 nwg = p.last_mtiles() * (N // H.tile_of(c[0])[1])
-                v = st[:nwg * 8].view(nwg, 8).cpu().double()
-                t0 = v[:, 0].min()
+                v = st[:nwg * 12].view(nwg, 12).cpu().double()
+                t0 = v[:, 8].min()
                 med = lambda x: float(x.median())  # noqa: E731
-                print("%-12s cfg %d stamps (median cycles over %d WGs): compute prologue->B0 %.0f, loop %.0f, "
+                print("%-12s cfg %d ablate %2d stamps (median cycles over %d WGs): entry->taps %.0f, taps->compute %.0f, "
+                      "compute prologue->B0 %.0f, loop %.0f, "
                       "epilogue %.0f | loader issue-prologue %.0f, wait B0 %.0f, loop %.0f | WG span %.0f, "
-                      "launch spread %.0f" % (name, c[0], nwg, med(v[:, 1] - v[:, 0]), med(v[:, 2] - v[:, 1]),
+                      "launch spread %.0f" % (name, c[0], c[2], nwg, med(v[:, 9] - v[:, 8]), med(v[:, 0] - v[:, 9]), med(v[:, 1] - v[:, 0]), med(v[:, 2] - v[:, 1]),
                                               med(v[:, 3] - v[:, 2]), med(v[:, 5] - v[:, 4]), med(v[:, 6] - v[:, 5]),
-                                              med(v[:, 7] - v[:, 6]), med(v[:, 3] - v[:, 0]),
-                                              float(v[:, 0].max() - t0)), flush=True)
+                                              med(v[:, 7] - v[:, 6]), med(v[:, 3] - v[:, 8]),
+                                              float(v[:, 8].max() - t0)), flush=True)
         for c in cands:
             ts = sorted(e0.elapsed_time(e1) / a.inner for e0, e1 in times[c])
             med = ts[len(ts) // 2] * 1e3

@@ -47,7 +47,7 @@ def main():
             os.environ["DCGAN_IGEMM_STAMPS"] = str(stamps.data_ptr())
         p = ext.Program()
         p.igemm_ex(name, mode, A.data_ptr(), Bw.data_ptr(), C.data_ptr(), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad,
-                   c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn if c >= 200 else 0, kb if c >= 200 else -1, sp)
+                   c, 0, N, 0, 0, 0, 0.2, stats.data_ptr(), 0, bkn if c >= 200 else 0, kb if 200 <= c < 400 else -1, sp)
         H.run(p)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -178,26 +178,20 @@ class Program {
                int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int out_f32, int ldc, int cofs,
                uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
-               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0, int fin = -1) {
+               int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
     if (cfg >= 500) {
-      if (out_f32 || splits != 1 || fin >= 0 || (kb_valid >= 0 && kb_valid != Kc))
-        throw std::runtime_error("igemm4: elem_t output, no split-K, no fused finalize");
+      if (out_f32 || splits != 1 || (kb_valid >= 0 && kb_valid != Kc))
+        throw std::runtime_error("igemm4: elem_t output, no split-K");
       return igemm4_ex(name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad_y, pad_x, cfg, ldc, cofs, bias,
                        act, leak, stats, stream, bkn, bnb_x, bnb_y, bnb_mean, bnb_rstd, bnb_rpg, bnb_act, bnb_leak,
                        bnb_store_g);
     }
     int bm = 0, bn = 0, ns = 0;
-    const bool hh = cfg >= 400;          // igemmh.hip (halo window in LDS)
-    const bool v3 = cfg >= 200 && !hh;
-    if (hh && dt_ == 2) throw std::runtime_error("igemmh: 16-bit builds only");
-    if (hh ? KF(dcg_igemmh_tile)(cfg, &bm, &bn, &ns)
-           : v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
+    const bool v3 = cfg >= 200;
+    if (cfg >= 400) throw std::runtime_error("bad igemm cfg " + std::to_string(cfg));
+    if (v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
       throw std::runtime_error("bad igemm cfg " + std::to_string(cfg) + " for this element type");
-    if (hh && (mode == 2 || splits != 1 || (Kc != 64 && Kc != 128 && Kc != 256 && Kc != 512) ||
-               (kb_valid >= 0 && kb_valid != Kc)))
-      throw std::runtime_error("igemmh: conv / deconv with Kc in {64,128,256,512}, no split-K");
-    if (!hh && !v3 && cfg >= 200) throw std::runtime_error("bad igemm cfg");
-    if (!v3 && !hh && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
+    if (!v3 && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
     if (splits < 1) throw std::runtime_error("splits must be >= 1");
     const int kal = (int)(16 / es_);  // 16-byte A rows
     if (Kc % kal) throw std::runtime_error("igemm needs 16-byte A rows (Kc % " + std::to_string(kal) + " == 0)");
@@ -270,45 +264,6 @@ class Program {
       k.oy_off = q.oy_off; k.ox_off = q.ox_off; k.ntaps = q.ntaps; k.fd_hw = q.fd_hw; k.fd_w = q.fd_w;
       for (int t = 0; t < 25; ++t) k.tap[t] = q.tap[t];
     }
-    size_t h_shm = 0;
-    if (hh) {  // per-phase input window of a tile and tap offsets inside it (igemmh.hip header)
-      int wp_max = 0, tb = 0;
-      for (int i = 0; i < a.nphases; ++i) {
-        const IGemmPhase& q = ph[i];
-        IGemmPhaseK& k = a.phk[i];
-        const int hwq = q.Hq * q.Wq;
-        int TB, TH;
-        if (bm % q.Wq) throw std::runtime_error("igemmh: tile rows must be whole grid rows");
-        if (bm <= hwq) {
-          if (hwq % bm) throw std::runtime_error("igemmh: tile rows must divide the image grid");
-          TB = 1; TH = bm / q.Wq;
-        } else {
-          if (bm % hwq) throw std::runtime_error("igemmh: tile rows must be whole images");
-          TB = bm / hwq; TH = q.Hq;
-        }
-        if (tb && TB != tb) throw std::runtime_error("igemmh: phases with different tile geometry");
-        tb = TB;
-        int dymin = 1 << 20, dymax = -(1 << 20), dxmin = 1 << 20, dxmax = -(1 << 20);
-        for (int t = 0; t < q.ntaps; ++t) {
-          dymin = std::min(dymin, (int)q.dy[t]); dymax = std::max(dymax, (int)q.dy[t]);
-          dxmin = std::min(dxmin, (int)q.dx[t]); dxmax = std::max(dxmax, (int)q.dx[t]);
-        }
-        k.win_h = a.sstride * (TH - 1) + dymax - dymin + 1;
-        k.win_w = a.sstride * (q.Wq - 1) + dxmax - dxmin + 1;
-        k.win_oy = q.iy0_off + dymin; k.win_ox = q.ix0_off + dxmin;
-        k.fd_whw = fastdiv_make(k.win_h * k.win_w); k.fd_ww = fastdiv_make(k.win_w);
-        for (int t = 0; t < q.ntaps; ++t)
-          k.tap[t] = ((q.dy[t] - dymin) * k.win_w + (q.dx[t] - dxmin)) | ((int)q.wtap[t] << 16);
-        wp_max = std::max(wp_max, TB * k.win_h * k.win_w);
-      }
-      a.h_tb = tb;
-      a.h_wbytes = (int)((((size_t)wp_max * (Kc / 8) + 63) / 64) * 1024);
-      h_shm = (size_t)a.h_wbytes + (size_t)ns * bn * 128;
-      const size_t epi = (size_t)(bm + 8 * bn) * 4 + (size_t)bm * (bn + 8) * 2 + (bnb_x ? 16384 : 0);
-      h_shm = std::max(h_shm, epi);
-      if (h_shm > 160 * 1024)
-        throw std::runtime_error("igemmh: window + B ring need " + std::to_string(h_shm) + " B of LDS (> 160 KiB)");
-    }
     int maxM = 0;
     for (auto& p : ph) maxM = std::max(maxM, p.M);
     const int mtiles = (maxM + bm - 1) / bm, ntiles = (N + bn - 1) / bn;
@@ -324,15 +279,15 @@ class Program {
         .w(C, (c_rows - 1) * ldc * out_es + (size_t)(cofs + N) * out_es)
         .w(stats, (size_t)mtiles * a.nphases * 2 * N * 4);
     if (bnb_x) {
-      const size_t lds = hh ? h_shm : (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
+      const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
       const size_t nt = v3 ? (size_t)KF(dcg_igemm3_threads)(cfg) : 256;
       // igemm3 (waves along M per tile id, igemm3.hip DCG_IGEMM3_TILES): the row-lane scratch may
-      // alias the C tile; v1 / igemmh keep them apart
+      // alias the C tile; v1 keeps them apart
       static const int kWM3[10] = {2, 4, 1, 2, 2, 2, 4, 2, 8, 2};
-      const size_t wm = v3 && !hh ? (size_t)kWM3[cfg % 10] : 4;
+      const size_t wm = v3 ? (size_t)kWM3[cfg % 10] : 4;
       const size_t ct = (size_t)bm * (bn + 8) * 2, r2 = 64 * nt;
-      const size_t need = (bm + 2 * wm * bn) * 4 + (v3 && !hh ? std::max(ct, r2) : ct + r2);
+      const size_t need = (bm + 2 * wm * bn) * 4 + (v3 ? std::max(ct, r2) : ct + r2);
       if (need > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");
       const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
@@ -355,15 +310,7 @@ class Program {
     }
     if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
     if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
-    if (fin >= 0 && hh) throw std::runtime_error("igemm fin: igemm / igemm3 tiles only");
-    if (hh) {
-      const unsigned blocks = (unsigned)((size_t)mtiles * ntiles * a.nphases);
-      return add(name, stream, [this, a, cfg, bkn, blocks, h_shm](hipStream_t s) {
-        return KF(dcg_igemmh_launch)(&a, cfg, bkn, blocks, h_shm, s);
-      }, acc.v);
-    }
     if (!v3) {
-      if (fin >= 0) attach_fin(a, fin, ntiles, acc);
       return add(name, stream, [this, a, cfg, mtiles, ntiles](hipStream_t s) {
         return KF(dcg_igemm_launch)(&a, cfg, mtiles, ntiles, s);
       }, acc.v);
@@ -374,7 +321,6 @@ class Program {
       a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
       acc.w((uintptr_t)a.ws, tiles * splits * (size_t)bm * bn * sizeof(float)).w((uintptr_t)a.counters, tiles * 4);
     }
-    if (fin >= 0) attach_fin(a, fin, ntiles, acc);
     const unsigned blocks = (unsigned)(tiles * splits);
     return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); },
                acc.v);
@@ -575,64 +521,7 @@ class Program {
     }, acc.v);
   }
 
-  // ------------------------------------------------------------------ fused BN finalize (finalize.h)
-  // A spec recorded here is attached to ONE igemm_ex op (fin=<handle>): that GEMM's workgroups
-  // reduce the partial rows they write and evaluate the finalize, instead of a separate
-  // bn_finalize / bn_bwd_finalize / sum_partials launch. Returns the handle.
-  int bn_fin_fwd(int groups, int ppg, int C, double count, uintptr_t gamma, uintptr_t beta, float eps,
-                 uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift, uintptr_t ema_mean,
-                 uintptr_t ema_var, float decay) {
-    BnFin f{};
-    f.mode = 1; f.groups = groups; f.ppg = ppg; f.C = C; f.count = count; f.eps = eps; f.decay = decay;
-    f.gamma = P<const float>(gamma); f.beta = P<const float>(beta);
-    f.mean = P<float>(mean); f.rstd = P<float>(rstd); f.scale = P<float>(scale); f.shift = P<float>(shift);
-    f.ema_mean = P<float>(ema_mean); f.ema_var = P<float>(ema_var);
-    const size_t gc = (size_t)groups * C * 4;
-    AccList acc;
-    acc.r(gamma, (size_t)C * 4).r(beta, (size_t)C * 4).w(mean, gc).w(rstd, gc).w(scale, gc).w(shift, gc)
-        .w(ema_mean, gc).w(ema_var, gc);
-    fins_.push_back({f, acc.v});
-    return (int)fins_.size() - 1;
-  }
-  int bn_fin_bwd(int groups, int ppg, int C, float count, uintptr_t gamma, uintptr_t mean, uintptr_t rstd,
-                 uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef) {
-    BnFin f{};
-    f.mode = 2; f.groups = groups; f.ppg = ppg; f.C = C; f.count = count;
-    f.gamma = P<const float>(gamma); f.mean_in = P<const float>(mean); f.rstd_in = P<const float>(rstd);
-    f.dgamma = P<float>(dgamma); f.dbeta = P<float>(dbeta); f.coef = P<float>(coef);
-    const size_t gc = (size_t)groups * C * 4;
-    AccList acc;
-    acc.r(gamma, (size_t)C * 4).r(mean, gc).r(rstd, gc).w(dgamma, (size_t)C * 4).w(dbeta, (size_t)C * 4)
-        .w(coef, 3 * gc);
-    fins_.push_back({f, acc.v});
-    return (int)fins_.size() - 1;
-  }
-  int bn_fin_sum(int groups, int ppg, int C, uintptr_t dst) {
-    BnFin f{};
-    f.mode = 3; f.groups = groups; f.ppg = ppg; f.C = C; f.count = 1.0;
-    f.dbeta = P<float>(dst);
-    fins_.push_back({f, AccList().w(dst, (size_t)C * 4).v});
-    return (int)fins_.size() - 1;
-  }
-  void attach_fin(IGemmArgs& a, int fin, int ntiles, AccList& acc) {
-    if (fin >= (int)fins_.size()) throw std::runtime_error("igemm: bad fin handle");
-    if (dt_ == 2 || !a.stats) throw std::runtime_error("igemm fin: 16-bit igemm3 with statistics only");
-    BnFin f = fins_[fin].first;
-    const int rows = a.mtiles * a.nphases;
-    if (f.groups < 1 || f.ppg < 1 || f.groups * f.ppg != rows || f.C != a.N)
-      throw std::runtime_error("igemm fin: groups x rows-per-group must equal the GEMM's partial rows");
-    int F = 1;  // rows per level-1 group: a power of two dividing ppg, ~sqrt(ppg), <= 32
-    while (F * F < f.ppg && f.ppg % (2 * F) == 0 && F < 32) F *= 2;
-    f.F = F;
-    f.ntn = ntiles;
-    f.part = a.stats;
-    const size_t nl1 = (size_t)f.groups * (f.ppg / F);
-    f.l1 = reinterpret_cast<double*>(dev_alloc(nl1 * 2 * f.C * sizeof(double)));
-    f.ctr = reinterpret_cast<unsigned*>(dev_alloc((nl1 + 1) * ntiles * sizeof(unsigned), nullptr, true));
-    a.fin = reinterpret_cast<const BnFin*>(dev_alloc(sizeof(BnFin), &f));
-    acc.w((uintptr_t)f.l1, nl1 * 2 * f.C * 8).w((uintptr_t)f.ctr, (nl1 + 1) * ntiles * 4);
-    for (auto& x : fins_[fin].second) acc.v.push_back(x);
-  }
+
   int last_mtiles() const { return last_mtiles_; }
   int last_nphases() const { return last_nphases_; }
 
@@ -812,18 +701,14 @@ class Program {
                                  P<float>(coef), s);
     }, acc.v);
   }
-  // fscale / fshift (optional): the forward BN coefficients -- act' from x instead of reading y
   int bn_bwd_apply(std::string name, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t coef, uintptr_t dx, int R,
-                   int C, int rows_per_group, int act, float leak, int stream, uintptr_t fscale, uintptr_t fshift) {
+                   int C, int rows_per_group, int act, float leak, int stream) {
     const size_t t = (size_t)R * C * es_, gc = (size_t)((R + rows_per_group - 1) / rows_per_group) * C * 4;
     AccList acc;
-    acc.r(dy, t).r(x, t).r(coef, 3 * gc).w(dx, t);
-    if (fscale) acc.r(fscale, gc).r(fshift, gc);
-    else acc.r(y, t);
+    acc.r(dy, t).r(x, t).r(y, t).r(coef, 3 * gc).w(dx, t);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_bwd_apply)(P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x), P<const float>(coef),
-                              P<elem_t>(dx), R, C, rows_per_group, act, leak, P<const float>(fscale),
-                              P<const float>(fshift), s);
+                              P<elem_t>(dx), R, C, rows_per_group, act, leak, s);
     }, acc.v);
   }
   int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
@@ -1034,15 +919,6 @@ class Program {
                            P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
     }, acc.v);
   }
-  // TF-SAME stride-2 5x5 conv with 1..4 input and 64 output channels (direct MFMA kernel, conv3.hip)
-  int conv3_direct(std::string name, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int H, int W,
-                   int Cin, int Ho, int Wo, int Cout, int pad_y, int pad_x, int act, float leak, int stream) {
-    return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_conv3_direct)(P<const elem_t>(x), P<const elem_t>(w), P<const float>(bias), P<elem_t>(y), B, H,
-                                  W, Cin, Ho, Wo, Cout, pad_y, pad_x, act, leak, s);
-    }, AccList().r(x, (size_t)B * H * W * Cin * es_).r(w, (size_t)25 * Cin * Cout * es_).r(bias, (size_t)Cout * 4)
-           .w(y, (size_t)B * Ho * Wo * Cout * es_).v);
-  }
   // narrow2.hip: TF-SAME stride-2 5x5 conv, 1..4 input -> 64 output channels, persistent `grid`
   // workgroups (<= tiles: nconv_tiles). bx != 0: fused BN-backward statistics of the layer below
   // (x = bx, y = by, one BN group), one partial row [2][64] per workgroup into part.
@@ -1219,7 +1095,6 @@ class Program {
   std::vector<void*> dev_allocs_;
   std::vector<hipEvent_t> events_;
   int last_mtiles_ = 0, last_nphases_ = 0;
-  std::vector<std::pair<BnFin, std::vector<Acc>>> fins_;  // fused-finalize specs (bn_fin_*)
   int dt_ = 0;       // element type of every activation / weight-mirror pointer
   size_t es_ = 2;    // its size in bytes
   bool dry_ = false;
@@ -1229,7 +1104,11 @@ static py::tuple igemm_tile(int cfg, int dtype) {
   int bm = 0, bn = 0, ns = 0;
   int rc;
 #define DT(fn) (dtype == 2 ? fn##_f32 : dtype == 1 ? fn##_f16 : fn)
-  if (cfg >= 400) rc = DT(dcg_igemmh_tile)(cfg, &bm, &bn, &ns);
+  if (cfg >= 500) {
+    int wm = 0, wn = 0;
+    if (dtype == 2) throw std::runtime_error("igemm4: 16-bit builds only");
+    rc = (dtype == 1 ? dcg_igemm4_tile_f16 : dcg_igemm4_tile)(cfg, &bm, &bn, &ns, &wm, &wn);
+  } else if (cfg >= 400) rc = -1;
   else if (cfg >= 200) rc = DT(dcg_igemm3_tile)(cfg, &bm, &bn, &ns);
   else rc = DT(dcg_igemm_tile)(cfg, &bm, &bn);
 #undef DT
@@ -1285,10 +1164,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("bias"), py::arg("act"), py::arg("leak"), py::arg("stats"), py::arg("stream"), py::arg("bkn"),
            py::arg("kb_valid"), py::arg("splits"), py::arg("bnb_x") = 0, py::arg("bnb_y") = 0,
            py::arg("bnb_mean") = 0, py::arg("bnb_rstd") = 0, py::arg("bnb_rpg") = 0, py::arg("bnb_act") = 0,
-           py::arg("bnb_leak") = 0.f, py::arg("bnb_store_g") = 0, py::arg("fin") = -1)
-      .def("bn_fin_fwd", &Program::bn_fin_fwd)
-      .def("bn_fin_bwd", &Program::bn_fin_bwd)
-      .def("bn_fin_sum", &Program::bn_fin_sum)
+           py::arg("bnb_leak") = 0.f, py::arg("bnb_store_g") = 0)
       .def("igemm4_plan", &Program::igemm4_plan)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
@@ -1303,7 +1179,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("bn_bwd_finalize", &Program::bn_bwd_finalize)
       .def("bn_bwd_apply", &Program::bn_bwd_apply, py::arg("name"), py::arg("dy"), py::arg("y"), py::arg("x"),
            py::arg("coef"), py::arg("dx"), py::arg("R"), py::arg("C"), py::arg("rows_per_group"), py::arg("act"),
-           py::arg("leak"), py::arg("stream"), py::arg("fscale") = 0, py::arg("fshift") = 0)
+           py::arg("leak"), py::arg("stream"))
       .def("act_bwd", &Program::act_bwd)
       .def("sum_partials", &Program::sum_partials)
       .def("act_bwd_dbias", &Program::act_bwd_dbias)
@@ -1333,7 +1209,6 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("adam2", &Program::adam2)
       .def("nonfinite_check", &Program::nonfinite_check)
       .def("narrow_deconv", &Program::narrow_deconv)
-      .def("conv3_direct", &Program::conv3_direct)
       .def("nconv", &Program::nconv)
       .def("nconv_tiles", &Program::nconv_tiles)
       .def("narrow_deconv_dact", &Program::narrow_deconv_dact)

@@ -267,35 +267,22 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   }
 }
 
-// fscale / fshift (optional, [groups][C], the forward BN coefficients; ReLU / LeakyReLU only):
-// act'(y) from the sign of x * fscale + fshift -- the forward's pre-activation -- instead of
-// reading y: one tensor less to stream (y > 0 exactly when that value is > 0)
+// dx = (a * dy * act'(y) + b * x + c) per group (a, b, c: bn_bwd_finalize's coefficients)
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const elem_t* __restrict__ dy, const elem_t* __restrict__ y,
                                                            const elem_t* __restrict__ x,
                                                            const float* __restrict__ coef, elem_t* __restrict__ dx,
                                                            uint32_t nv, int C, FastDiv fd_c8, FastDiv fd_rpg, int act,
-                                                           float leak, const float* __restrict__ fscale,
-                                                           const float* __restrict__ fshift) {
-  const float slope = act == ACT_LRELU ? leak : 0.f;
+                                                           float leak) {
   for (uint32_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += gridDim.x * 256) {
     const uint32_t r = fdiv(v, fd_c8);
     const int c = (int)(v - r * fd_c8.d) * 8;
     const int g = (int)fdiv(r, fd_rpg);
-    float dv[8], ag[8], xv[8], ca[8], cb[8], cc[8];
+    float dv[8], ag[8], xv[8], yv[8], ca[8], cb[8], cc[8];
     load8(dy + (size_t)v * 8, dv);
     load8(x + (size_t)v * 8, xv);
-    if (fscale) {
-      float fs[8], fh[8];
-      load8f(fscale + g * C + c, fs);
-      load8f(fshift + g * C + c, fh);
+    load8(y + (size_t)v * 8, yv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) ag[i] = xv[i] * fs[i] + fh[i] > 0.f ? 1.f : slope;
-    } else {
-      float yv[8];
-      load8(y + (size_t)v * 8, yv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ag[i] = act_grad_from_out(yv[i], act, leak);
-    }
+    for (int i = 0; i < 8; ++i) ag[i] = act_grad_from_out(yv[i], act, leak);
     load8f(coef + (g * 3 + 0) * C + c, ca);
     load8f(coef + (g * 3 + 1) * C + c, cb);
     load8f(coef + (g * 3 + 2) * C + c, cc);
@@ -689,14 +676,12 @@ extern "C" int DCG_API(dcg_bn_bwd_finalize)(const float* part, int ppg, int grou
 }
 
 extern "C" int DCG_API(dcg_bn_bwd_apply)(const elem_t* dy, const elem_t* y, const elem_t* x, const float* coef, elem_t* dx, int R,
-                                int C, int rows_per_group, int act, float leak, const float* fscale,
-                                const float* fshift, hipStream_t s) {
-  if (fscale && (!fshift || (act != ACT_RELU && act != ACT_LRELU))) return -2;
+                                int C, int rows_per_group, int act, float leak, hipStream_t s) {
   if (C % 8) return -2;
   const size_t nv = (size_t)R * C / 8;
   if (nv >= 0x80000000ull) return -3;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nv)), dim3(256), 0, s, dy, y, x, coef, dx, (uint32_t)nv, C,
-                     fastdiv_make(C / 8), fastdiv_make(rows_per_group), act, leak, fscale, fshift);
+                     fastdiv_make(C / 8), fastdiv_make(rows_per_group), act, leak);
   return (int)hipGetLastError();
 }
 

@@ -29,7 +29,6 @@
 // (relu / lrelu / tanh), pixel scatter of the phase, output staged through LDS and written as
 // 16-byte row segments (elem_t, N % 8 == 0) or element-wise (fp32 / narrow N).
 #include "epilogue.h"
-#include "finalize.h"
 
 namespace dcg {
 
@@ -60,7 +59,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.stats + (size_t)row * 2 * p.N, (uint32_t)(2 * p.N * 4));
       for (int nl = threadIdx.x; nl < BN; nl += 256)
         if (n0 + nl < p.N) { st_sc1_f32(rs, (uint32_t)(n0 + nl) * 4u, 0.f); st_sc1_f32(rs, (uint32_t)(p.N + n0 + nl) * 4u, 0.f); }
-      if (p.fin) tile_bn_finalize<BN, 256>(*p.fin, row, blockIdx.y, n0, reinterpret_cast<int*>(lds));
     }
     return;
   }
@@ -243,8 +241,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       __syncthreads();
       float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + BM * CPAD * 2);
       vec_store_bnb<BM, BN>(p, rowoff, ctile, red2, n0, m0, p.stats + (size_t)(blockIdx.x * p.nphases + phase) * 2 * N);
-      if (p.fin) tile_bn_finalize<BN, 256>(*p.fin, blockIdx.x * p.nphases + phase, blockIdx.y, n0,
-                                           reinterpret_cast<int*>(lds));
     } else {
       __builtin_trap();  // the host only requests fused statistics on tiles with the LDS for them
     }
@@ -274,11 +270,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       }
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.stats + (size_t)(blockIdx.x * p.nphases + phase) * 2 * N,
                                                   (uint32_t)(2 * N * 4));
-      st_sc1_f32(rs, (uint32_t)n * 4u, s);  // write-through: the fused finalize reads it on another CU
+      st_sc1_f32(rs, (uint32_t)n * 4u, s);  // write-through (read by the finalize kernel)
       st_sc1_f32(rs, (uint32_t)(N + n) * 4u, s2);
     }
-    if (p.fin) tile_bn_finalize<BN, 256>(*p.fin, blockIdx.x * p.nphases + phase, blockIdx.y, n0,
-                                         reinterpret_cast<int*>(lds));
   }
 }
 

@@ -28,7 +28,6 @@
 // XCDs, so workgroup b works on tile (b % 8) * (T / 8) + b / 8, which gives every XCD a
 // contiguous run of tiles (neighbouring output pixels share input rows in that XCD's L2).
 #include "epilogue.h"
-#include "finalize.h"
 
 namespace dcg {
 
@@ -121,7 +120,6 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.stats + (size_t)row * 2 * p.N, (uint32_t)(2 * p.N * 4));
       for (int nl = tid; nl < BN; nl += NT)
         if (n0 + nl < p.N) { st_sc1_f32(rs, (uint32_t)(n0 + nl) * 4u, 0.f); st_sc1_f32(rs, (uint32_t)(p.N + n0 + nl) * 4u, 0.f); }
-      if (p.fin) tile_bn_finalize<BN, NT>(*p.fin, row, nt, n0, reinterpret_cast<int*>(lds));
     }
     return;
   }
@@ -383,7 +381,6 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
       float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + (kSep ? kCt : 0));
       vec_store_bnb<BM, BN, NT, kAlias>(p, rowoff, ctile, red2, n0, m0,
                                         p.stats + (size_t)(mt * p.nphases + phase) * 2 * N);
-      if (p.fin) tile_bn_finalize<BN, NT>(*p.fin, mt * p.nphases + phase, nt, n0, reinterpret_cast<int*>(lds));
     } else {
       __builtin_trap();  // the host only requests fused statistics on tiles with the LDS for them
     }
@@ -414,10 +411,9 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
       }
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.stats + (size_t)(mt * p.nphases + phase) * 2 * N,
                                                   (uint32_t)(2 * N * 4));
-      st_sc1_f32(rs, (uint32_t)n * 4u, s);  // write-through: the fused finalize reads it on another CU
+      st_sc1_f32(rs, (uint32_t)n * 4u, s);  // write-through (read by the finalize kernel)
       st_sc1_f32(rs, (uint32_t)(N + n) * 4u, s2);
     }
-    if (p.fin) tile_bn_finalize<BN, NT>(*p.fin, mt * p.nphases + phase, nt, n0, reinterpret_cast<int*>(lds));
   }
   if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memtime();
 }

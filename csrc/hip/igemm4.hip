@@ -109,30 +109,35 @@ __device__ __forceinline__ Sched sched_of(const IG4Args& a) {
 }
 
 // Step cursor (wave-uniform): phase p, channel chunk c, tap t (t < 0: empty step ahead of a
-// reloaded window when only one window buffer fits), window load ordinal wl, steps taken in the
-// current window sw, steps in it wlen.
+// reloaded window when only one window buffer fits), taps in this phase nt, window load ordinal
+// wl, steps taken in the current window sw, steps in it wlen.
 struct Cur {
-  int p, c, t, wl, sw, wlen;
+  int p, c, t, nt, wl, sw, wlen;
 };
 
 template <int NSB>
 __device__ __forceinline__ void cur_init(Cur& k, const Sched& q) {
-  k.p = 0; k.c = 0; k.t = 0; k.wl = 0; k.sw = 0; k.wlen = q.nt0;
+  k.p = 0; k.c = 0; k.t = 0; k.nt = q.nt0; k.wl = 0; k.sw = 0; k.wlen = q.nt0;
 }
 
+// one step: the common case is a compare and a (rarely taken) branch -- with the phase's tap
+// count re-derived on every step (a switch) the loop's scalar work was ~400 cycles per step.
+// (Kept one function: split into an inlined helper with an early return, the cursor lost its
+// uniformity -- the whole step loop went to VGPRs and exec-mask branches.)
 template <int NSB>
 __device__ __forceinline__ void cur_next(Cur& k, const Sched& q) {
   ++k.t;
   ++k.sw;
-  if (k.t < q.ntaps(k.p)) return;
+  if (__builtin_expect(k.t < k.nt, 1)) return;
   if (++k.c == q.nch) { k.c = 0; ++k.p; }
-  if (k.p >= q.nph) { k.p = q.nph - 1; k.t = 1 << 20; return; }  // past the end (never consumed)
+  if (k.p >= q.nph) { k.p = q.nph - 1; k.t = 0; k.nt = 1 << 20; return; }  // past the end: a valid tap, never consumed
   const bool load = !q.shared;
   if (load) ++k.wl;
   const int pre = (load && q.nwb == 1) ? NSB - 1 : 0;
+  k.nt = q.ntaps(k.p);
   k.t = -pre;
   k.sw = 0;
-  k.wlen = pre + q.ntaps(k.p);
+  k.wlen = pre + k.nt;
 }
 
 // tap table entry (phase p, tap t) from a lane-distributed copy: lane i of v0 / v1 holds entry i /
@@ -190,19 +195,36 @@ __device__ __forceinline__ float red16(float v) {
   return v;
 }
 
+// B stage row -> channel (n-major B): inside each 32-row group, row bits (h, f1, f0, r1, r0) hold
+// channel bits (f1, f0, h, r1, r0) -- MFMA blocks 2P / 2P+1 then give lane group f the channels
+// P*32 + 8f + [0, 8), contiguous for one 16-byte store
+__device__ __forceinline__ int pair_perm(int r) {
+  return (r & ~31) | (((r >> 2) & 3) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
+}
+
 }  // namespace ig4
 
 // EPI: 0 plain (+bias, statistics of the stored value, activation), 1 BN-backward statistics of
-// the layer whose dL/da this GEMM produces, 2 activation backward only (store g, sums of g)
-template <int FM, int FN, int TM, int TN, int WMC, int BN, int ACT, int EPI>
+// the layer whose dL/da this GEMM produces, 2 activation backward only (store g, sums of g).
+// PAIR (B in n-major rows): the loader permuted the weight rows inside every 32-row group so that
+// MFMA blocks 2P and 2P+1 hold channels P*32 + fq*8 + [0,4) and + [4,8) in lane group fq: one
+// 16-byte store per (pixel, 8 channels) instead of two 8-byte ones -- the epilogue is store-issue
+// bound (MI355X_MICROARCH.md, epilogue store tail), so half the store instructions.
+template <int FM, int FN, int TM, int TN, int WMC, int BN, int ACT, int EPI, bool PAIR>
 __device__ __forceinline__ void ig4_epilogue(f32x4 (&acc)[FN][FM], const IG4Args& a, int p, int mt, int m0, int n0,
                                              int b0, int y0, int wm, int wn, int fr, int fq, lds_f32* part,
                                              lds_i32* ctr) {
+  constexpr int NPJ = PAIR ? 2 : 1;  // MFMA column blocks per store
+  static_assert(FN % NPJ == 0, "pairs of column blocks");
   const int lane = threadIdx.x & 63;
+  // laundered: nothing below is loop-invariant to the compiler, so none of it is hoisted out of
+  // the phase loop to sit in registers (and spill) across the K loop
+  int mlb = wm * TM + fr, nlb = wn * TN + fq * (PAIR ? 8 : 4);
+  asm volatile("" : "+v"(mlb), "+v"(nlb));
   int off[FM];
 #pragma unroll
   for (int im = 0; im < FM; ++im) {
-    const int ml = wm * TM + im * 16 + fr;
+    const int ml = mlb + im * 16;
     const int bl = (int)fdiv((uint32_t)ml, a.fd_tw);
     const int rem = ml - bl * a.TR * a.Wq;
     const int ty = (int)fdiv((uint32_t)rem, a.fd_wq);
@@ -213,66 +235,105 @@ __device__ __forceinline__ void ig4_epilogue(f32x4 (&acc)[FN][FM], const IG4Args
   const bool do_stats = a.stats != nullptr;
   const float slope = a.bnb_act == ACT_LRELU ? a.bnb_leak : 0.f;
   const int g = EPI == 1 ? m0 / a.bnb_rpg : 0;
+  using vst = std::conditional_t<PAIR, uint4, uint2>;
 #pragma unroll
-  for (int jn = 0; jn < FN; ++jn) {
-    const int n = n0 + wn * TN + jn * 16 + fq * 4;
-    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-    if (EPI == 0 && a.bias) bv = *reinterpret_cast<const f32x4*>(a.bias + n);
-    f32x4 mu = bv, rs = bv;
-    if constexpr (EPI == 1) {
-      mu = *reinterpret_cast<const f32x4*>(a.bnb_mean + g * a.N + n);
-      rs = *reinterpret_cast<const f32x4*>(a.bnb_rstd + g * a.N + n);
+  for (int jp = 0; jp < FN / NPJ; ++jp) {
+    // this lane's first channel of the block group (local to the workgroup's BN columns)
+    const int nl0 = nlb + (PAIR ? jp * 32 : jp * 16);
+    const int n = n0 + nl0;
+    f32x4 bv[NPJ], mu[NPJ], rs[NPJ], s[NPJ], s2[NPJ];
+#pragma unroll
+    for (int h = 0; h < NPJ; ++h) {
+      bv[h] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (EPI == 0 && a.bias) bv[h] = *reinterpret_cast<const f32x4*>(a.bias + n + 4 * h);
+      mu[h] = bv[h];
+      rs[h] = bv[h];
+      if constexpr (EPI == 1) {
+        mu[h] = *reinterpret_cast<const f32x4*>(a.bnb_mean + g * a.N + n + 4 * h);
+        rs[h] = *reinterpret_cast<const f32x4*>(a.bnb_rstd + g * a.N + n + 4 * h);
+      }
+      s[h] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      s2[h] = s[h];
     }
-    f32x4 s = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+    // the backward epilogues' y / x tiles of this block group, all issued before any is used
+    // (one memory round trip per group; the group barrier below keeps the next group's loads
+    // from being hoisted here, which would double the live registers and spill)
+    vst yall[EPI != 0 ? FM : 1], xall[EPI == 1 ? FM : 1];
+    if constexpr (EPI != 0) {
+#pragma unroll
+      for (int im = 0; im < FM; ++im) yall[im] = *reinterpret_cast<const vst*>(a.bnb_y + off[im] + n);
+    }
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int im = 0; im < FM; ++im) xall[im] = *reinterpret_cast<const vst*>(a.bnb_x + off[im] + n);
+    }
 #pragma unroll
     for (int im = 0; im < FM; ++im) {
-      const f32x4 v = acc[jn][im] + bv;
-      // the stored (rounded) values; statistics are of exactly the stored tensor
-      const uint2 pv = ig4::pack4(v[0], v[1], v[2], v[3]);
-      const f32x4 vs = ig4::unpack4(pv);
       elem_t* dst = a.C + off[im] + n;
-      if constexpr (EPI == 0) {
-        s += vs;
-        s2 += vs * vs;
-        if constexpr (ACT == ACT_NONE) {
-          *reinterpret_cast<uint2*>(dst) = pv;
-        } else {
-          *reinterpret_cast<uint2*>(dst) = ig4::pack4(ig4::act_f<ACT>(v[0], a.leak), ig4::act_f<ACT>(v[1], a.leak),
-                                                      ig4::act_f<ACT>(v[2], a.leak), ig4::act_f<ACT>(v[3], a.leak));
-        }
-      } else if constexpr (EPI == 1) {
-        const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
-        const f32x4 xv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_x + off[im] + n));
-        f32x4 gv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gv[r] = vs[r] * (yv[r] > 0.f ? 1.f : slope);
-        s += gv;
-        s2 += gv * (xv - mu) * rs;
-        *reinterpret_cast<uint2*>(dst) = pv;
-      } else {
-        const f32x4 yv = ig4::unpack4(*reinterpret_cast<const uint2*>(a.bnb_y + off[im] + n));
-        f32x4 d;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) d[r] = a.bnb_act == ACT_TANH ? 1.f - yv[r] * yv[r] : (yv[r] > 0.f ? 1.f : slope);
-        const uint2 pg = ig4::pack4(vs[0] * d[0], vs[1] * d[1], vs[2] * d[2], vs[3] * d[3]);
-        s += ig4::unpack4(pg);
-        *reinterpret_cast<uint2*>(dst) = pg;
+      uint2 out[NPJ];
+      uint2 yin[NPJ], xin[NPJ];
+      if constexpr (EPI != 0) {
+        const vst yy = yall[im];
+        if constexpr (PAIR) { yin[0] = make_uint2(yy.x, yy.y); yin[NPJ - 1] = make_uint2(yy.z, yy.w); }
+        else yin[0] = *reinterpret_cast<const uint2*>(&yy);
       }
+      if constexpr (EPI == 1) {
+        const vst xx = xall[im];
+        if constexpr (PAIR) { xin[0] = make_uint2(xx.x, xx.y); xin[NPJ - 1] = make_uint2(xx.z, xx.w); }
+        else xin[0] = *reinterpret_cast<const uint2*>(&xx);
+      }
+#pragma unroll
+      for (int h = 0; h < NPJ; ++h) {
+        const f32x4 v = acc[jp * NPJ + h][im] + bv[h];
+        // the stored (rounded) values; statistics are of exactly the stored tensor
+        const uint2 pv = ig4::pack4(v[0], v[1], v[2], v[3]);
+        const f32x4 vs = ig4::unpack4(pv);
+        if constexpr (EPI == 0) {
+          s[h] += vs;
+          s2[h] += vs * vs;
+          if constexpr (ACT == ACT_NONE) out[h] = pv;
+          else
+            out[h] = ig4::pack4(ig4::act_f<ACT>(v[0], a.leak), ig4::act_f<ACT>(v[1], a.leak),
+                                ig4::act_f<ACT>(v[2], a.leak), ig4::act_f<ACT>(v[3], a.leak));
+        } else if constexpr (EPI == 1) {
+          const f32x4 yv = ig4::unpack4(yin[h]), xv = ig4::unpack4(xin[h]);
+          f32x4 gv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gv[r] = vs[r] * (yv[r] > 0.f ? 1.f : slope);
+          s[h] += gv;
+          s2[h] += gv * (xv - mu[h]) * rs[h];
+          out[h] = pv;
+        } else {
+          const f32x4 yv = ig4::unpack4(yin[h]);
+          f32x4 d;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[r] = a.bnb_act == ACT_TANH ? 1.f - yv[r] * yv[r] : (yv[r] > 0.f ? 1.f : slope);
+          const uint2 pg = ig4::pack4(vs[0] * d[0], vs[1] * d[1], vs[2] * d[2], vs[3] * d[3]);
+          s[h] += ig4::unpack4(pg);
+          out[h] = pg;
+        }
+      }
+      if constexpr (PAIR) *reinterpret_cast<uint4*>(dst) = make_uint4(out[0].x, out[0].y, out[NPJ - 1].x, out[NPJ - 1].y);
+      else *reinterpret_cast<uint2*>(dst) = out[0];
     }
     if (do_stats) {
       // sums over the wave's TM rows: in registers over im, then over the 16 pixel lanes; lanes
-      // 0, 16, 32, 48 put 4 channels each into this wave's partial row part[wm][BN][2]
+      // 0, 16, 32, 48 put 4 * NPJ channels each into this wave's partial row part[wm][BN][2]
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[r] = ig4::red16(s[r]);
-        s2[r] = EPI == 2 ? 0.f : ig4::red16(s2[r]);
-      }
-      if (fr == 0) {
-        lds_f32* q = part + (wm * BN + wn * TN + jn * 16 + fq * 4) * 2;
+      for (int h = 0; h < NPJ; ++h) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { q[2 * r] = s[r]; q[2 * r + 1] = s2[r]; }
+        for (int r = 0; r < 4; ++r) {
+          s[h][r] = ig4::red16(s[h][r]);
+          s2[h][r] = EPI == 2 ? 0.f : ig4::red16(s2[h][r]);
+        }
+        if (fr == 0) {
+          lds_f32* q = part + (wm * BN + nl0 + 4 * h) * 2;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { q[2 * r] = s[h][r]; q[2 * r + 1] = s2[h][r]; }
+        }
       }
     }
+    if constexpr (EPI != 0) __builtin_amdgcn_sched_barrier(0);
   }
   if (!do_stats) return;
   // the last compute wave of column wn to arrive sums the partial rows in wave order
@@ -319,6 +380,10 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // diagnostics: 12 s_memtime stamps per workgroup (8 kernel entry, 9 tap table loaded,
+  // 0-3 compute wave 0, 4-7 loader wave 0)
+  unsigned long long* const stw = a.stamps ? a.stamps + (size_t)blockIdx.x * 12 : nullptr;
+  if (stw && wave == 0 && lane == 0) stw[8] = __builtin_amdgcn_s_memtime();
 
   // ---- tile: n fastest (tiles of one window on one XCD), XCD-aware bijective remap
   int t = blockIdx.x;
@@ -336,6 +401,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
   const int* tflat = &a.tap[0][0];
   int vt0 = tflat[lane], vt1 = lane < 36 ? tflat[64 + lane] : 0;
   asm volatile("" : "+v"(vt0), "+v"(vt1));  // loaded (and waited for) here, not re-loaded in the K loop
+  if (stw && wave == 0 && lane == 0) stw[9] = __builtin_amdgcn_s_memtime() + (unsigned)(vt0 & 0);
 
   if (tid < 64 && lane < WNC) ctr[lane] = 0;
 
@@ -386,7 +452,8 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
         } else {
           const int r = q * 8 + (lane >> 3);
           const int j = (lane & 7) ^ sw8(r);
-          off = (uint32_t)(((wt * N + n0 + r) * Kc + k0 + j * 8) * 2);
+          // stage row r holds channel n0 + ig4::pair_perm(r) (the epilogue's 16-byte stores)
+          off = (uint32_t)(((wt * N + n0 + ig4::pair_perm(r)) * Kc + k0 + j * 8) * 2);
         }
         dma16_asm_la(rb, dst0 + q * 1024, off);
       }
@@ -412,7 +479,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       return n;
     };
 
-    unsigned long long* st = (a.stamps && lid == 0 && lane == 0) ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
+    unsigned long long* st = (lid == 0 && lane == 0) ? stw : nullptr;
     if (st) st[4] = __builtin_amdgcn_s_memtime();
     Cur ki;
     cur_init<NSB>(ki, q);
@@ -522,7 +589,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       return;
     }
 #define DCG_IG4_EPI(ACT_, EPI_) \
-  ig4_epilogue<FM, FN, TM, TN, WMC, BN, ACT_, EPI_>(acc, a, p, mt, m0, n0, b0, y0, wm, wn, fr, fq, part, ctr)
+  ig4_epilogue<FM, FN, TM, TN, WMC, BN, ACT_, EPI_, BKN == 0>(acc, a, p, mt, m0, n0, b0, y0, wm, wn, fr, fq, part, ctr)
     if (a.bnb_x) {
       if (a.bnb_store_g) DCG_IG4_EPI(ACT_NONE, 2);
       else DCG_IG4_EPI(ACT_NONE, 1);
@@ -541,7 +608,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
       for (int im = 0; im < FM; ++im) acc[jn][im] = (f32x4){0.f, 0.f, 0.f, 0.f};
   };
 
-  unsigned long long* stc = (a.stamps && wave == 0 && lane == 0) ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  unsigned long long* stc = (wave == 0 && lane == 0) ? stw : nullptr;
   if (stc) stc[0] = __builtin_amdgcn_s_memtime();
   // the compute waves' share of window 0 (they are idle until barrier 0 anyway)
   if (!(a.ablate & 2)) {

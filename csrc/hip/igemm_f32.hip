@@ -15,7 +15,7 @@
 // that are k-major in memory (the BKN weight layout, both wgrad operands) are transposed on the
 // LDS write, with chunk -> thread maps that keep those scalar writes bank-conflict free.
 //
-// The 16-bit-only kernels of the library (igemm v1, wgrad3, conv3_direct, narrow_deconv) have no
+// The 16-bit-only kernels of the library (igemm v1, wgrad3, narrow_deconv) have no
 // fp32 build: their fp32 entry points report "unsupported" and the engine takes the im2col /
 // implicit-GEMM paths instead.
 #include "kernels.h"
@@ -434,17 +434,11 @@ extern "C" int DCG_API(dcg_wgrad_launch)(const dcg::WGradArgs* a, int cfg, int s
 // 16-bit-only kernels: no fp32 build (the engine does not select them for fp32)
 extern "C" int DCG_API(dcg_igemm_tile)(int, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_igemm_launch)(const dcg::IGemmArgs*, int, int, int, hipStream_t) { return -2; }
-extern "C" int DCG_API(dcg_igemmh_tile)(int, int*, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_igemm4_tile)(int, int*, int*, int*, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_igemm4_launch)(const dcg::IG4Args*, int, int, unsigned, size_t, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_igemm3_threads)(int) { return 256; }
-extern "C" int DCG_API(dcg_igemmh_launch)(const dcg::IGemmArgs*, int, int, unsigned, size_t, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_wgrad3_tile)(int, int*, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_wgrad3_launch)(const dcg::WGrad3Args*, int, hipStream_t) { return -2; }
-extern "C" int DCG_API(dcg_conv3_direct)(const elem_t*, const elem_t*, const float*, elem_t*, int, int, int, int, int,
-                                         int, int, int, int, int, float, hipStream_t) {
-  return -2;
-}
 extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t*, const elem_t*, const float*, elem_t*, int, int, int, int, int,
                                           int, int, int, int, float, hipStream_t) {
   return -2;

@@ -23,26 +23,6 @@ struct IGemmPhaseK {
   int Hq, Wq, M, iy0_off, ix0_off, oy_off, ox_off, ntaps;
   FastDiv fd_hw, fd_w;
   int tap[25];              // packed (dy & 0xff) | (dx & 0xff) << 8 | wtap << 16
-                            // (igemmh: window pixel offset of the tap | wtap << 16)
-  // igemmh (halo) only: the input window of a tile -- row / column of window pixel 0 relative
-  // to (sstride * first tile row, 0), window height / width, and their fast divisors
-  int win_oy, win_ox, win_h, win_w;
-  FastDiv fd_whw, fd_ww;
-};
-
-// BN finalize fused into the statistics-producing GEMM (finalize.h). mode 1 forward (mean /
-// rstd / scale / shift / EMA), 2 backward (dx coefficients, dgamma, dbeta), 3 bias-gradient sum.
-struct BnFin {
-  int mode, groups, ppg, F, C, ntn;       // partial rows per group, rows per L1 group, channels, column tiles
-  double count;                           // rows per group
-  float eps, decay;
-  const float* part;                      // the partial rows [groups * ppg][2][C] (= IGemmArgs::stats)
-  double* l1;                             // [groups * ppg / F][2][C]
-  unsigned* ctr;                          // [(groups * ppg / F + 1) * ntn], zero between launches
-  const float* gamma; const float* beta;
-  float* mean; float* rstd; float* scale; float* shift; float* ema_mean; float* ema_var;  // forward out
-  const float* mean_in; const float* rstd_in;                                            // backward in
-  float* dgamma; float* dbeta; float* coef;                                              // backward out
 };
 
 struct IGemmArgs {
@@ -74,10 +54,6 @@ struct IGemmArgs {
   // activation-only backward (layer without BN): store g = dL/da * act'(y) instead of dL/da and
   // emit (sum g, 0) per channel -- the bias gradient partials. bnb_x aliases y, mean/rstd unused.
   int bnb_store_g;
-  // igemmh (halo): LDS bytes reserved for the input window (whole 1 KiB DMA pieces, max over
-  // phases) and images per tile (1 when a tile is a band of rows of one image)
-  int h_wbytes, h_tb;
-  const BnFin* fin;         // igemm3: BN finalize fused into the epilogue (nullptr = separate kernel)
 };
 
 struct IG4Args;  // igemm4.hip (csrc/hip/ig4.h)

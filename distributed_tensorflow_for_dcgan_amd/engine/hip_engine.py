@@ -322,12 +322,11 @@ class HipEngine:
     # ---- helpers
     def _igemm(self, prog, name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad, out_f32=False, ldc=None,
                cofs=0, bias=None, act=NONE, stats=None, rows_per_group=None, bkn=False, kb_valid=-1, bnb=None,
-               stream=0, fin=None):
+               stream=0):
         """One conv-shaped GEMM. Bw is a weight view; bkn=True reads it as [tap][K][N] (D
         forward, G dgrad, im2col'd layers), else as [tap][N][K]. bnb = (x, y, mean, rstd,
         rows_per_group, act[, store_g]): the epilogue also emits the BN-backward partial sums of
-        the layer whose dL/da this GEMM produces (see _dgrad_bnb). fin: callable cfg -> handle of a
-        fused-finalize spec (Program.bn_fin_*) or -1 (see _fin_ok)."""
+        the layer whose dL/da this GEMM produces (see _dgrad_bnb)."""
         plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group, bkn, dtype=self.dt)
         if plan is None:
             raise RuntimeError("no igemm tile for %s (mode %d, N %d, bkn %d)" % (name, mode, N, bkn))
@@ -338,35 +337,10 @@ class HipEngine:
             bx, by, bm, br = _p(bnb[0]), _p(bnb[1]), _p(bnb[2]), _p(bnb[3])
             brpg, bact = bnb[4], bnb[5]
             bstore = int(len(bnb) > 6 and bnb[6])
-        fh = fin(cfg) if fin is not None else -1
         prog.igemm_ex(name, mode, _p(A), _p(Bw), _p(C), Bn, Hin, Win, Kc, Hout, Wout, N, pad, pad, cfg, int(out_f32),
                       ldc or N, cofs, _p(bias), act, self.cfg.lrelu_leak, _p(stats), stream, int(bkn), kb_valid, splits,
-                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak, bstore, fh)
+                      bx, by, bm, br, brpg, bact, self.cfg.lrelu_leak, bstore)
         return cfg
-
-    def _fin_ok(self, cfg: int) -> bool:
-        """DCGAN_FUSED_FIN=1: the BN finalize (or bias-gradient sum) runs inside the statistics GEMM
-        (csrc/hip/finalize.h, 16-bit igemm / igemm3 tiles) instead of a separate launch. Off by
-        default: measured 1.389 vs 1.321 ms/step (profiles/r2/ab_fused_finalize_r2.txt) -- the
-        per-workgroup arrival (vmcnt(0) on the C-tile stores + one agent-scope atomic round trip)
-        costs more than the 14 launches it removes."""
-        return (not self.f32 and cfg < 400 and os.environ.get("DCGAN_FUSED_FIN") == "1")
-
-    def _fin_fwd(self, prog, name, rows, C, groups, P, update_ema, holder):
-        """fin callable for the GEMM producing BN ``name``'s forward statistics."""
-        def make(cfg):
-            if not self._fin_ok(cfg):
-                return -1
-            cfgm, st = self.cfg, self.bn[name]
-            bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
-            Pm = self.model.d if name.startswith("d_") else self.model.g
-            ema_m = bnstate.mean[name] if update_ema else None
-            ema_v = bnstate.var[name] if update_ema else None
-            holder["fused"] = True
-            return prog.bn_fin_fwd(groups, P // groups, C, float(rows // groups), _p(Pm[name + "/gamma"]),
-                                   _p(Pm[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]),
-                                   _p(st["scale"]), _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum)
-        return make
 
     def _stats_tiles(self, mode, Bn, Hin, Win, Kc, Hout, Wout, N, rows_per_group=None, bkn=False):
         """Number of partial-statistics rows a stats-emitting igemm writes (tiles x phases)."""
@@ -381,13 +355,13 @@ class HipEngine:
         return -(-M // bm) * phases
 
     def _dgrad_bnb(self, prog, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, bn_name, x, y, groups, act,
-                   group_offset=0, fin=None):
+                   group_offset=0):
         """Fused BN-backward statistics for the data-gradient GEMM that writes dL/da of BN layer
         ``bn_name`` (x = its pre-BN input, y = its activation output, same layout as the GEMM
         output). Returns (igemm kwargs, partials, partials per group) or None when no tile keeps
         the real/fake groups apart (odd sizes) or in fp32 -- the BN backward then runs its own
-        statistics pass. fin = (param set, grads or None, coef buffer): also fuse the BN-backward
-        finalize into the GEMM where the tile allows (the returned holder then says "fused")."""
+        statistics pass. (The BN-backward finalize stays a separate kernel: fusing it into the GEMM
+        through a per-workgroup arrival measured slower, profiles/r2/ab_fused_finalize_r2.txt.)"""
         if self.f32:
             return None
         if mode == 1:
@@ -406,28 +380,13 @@ class HipEngine:
         st = self.bn[bn_name]
         mean, rstd = st["mean"][group_offset:], st["rstd"][group_offset:]
         kw = dict(stats=part, rows_per_group=rpg, bnb=(x, y, mean, rstd, rpg, act))
-        hold = {}
-        if fin is not None:
-            Pm, grads, coef = fin
+        return kw, part, P // groups
 
-            def make(cfg):
-                if not self._fin_ok(cfg):
-                    return -1
-                hold["fused"] = True
-                dg = grads[bn_name + "/gamma"] if grads is not None else None
-                db = grads[bn_name + "/beta"] if grads is not None else None
-                # BN count = ALL rows of a group (a deconv-shaped dgrad's rpg counts one phase)
-                return prog.bn_fin_bwd(groups, P // groups, N, float(M * phases // groups),
-                                       _p(Pm[bn_name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef))
-            kw["fin"] = make
-        return kw, part, P // groups, hold
-
-    def _dgrad_actb(self, prog, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, name, y, act, db=None):
+    def _dgrad_actb(self, prog, mode, Bn, Hin, Win, Kc, Hout, Wout, N, bkn, name, y, act):
         """Fused activation backward for the data-gradient GEMM that produces dL/da of a layer
         WITHOUT BN: the GEMM stores dx = dL/da * act'(y) directly and emits per-tile partial
         column sums of dx (the bias gradient). Returns (igemm kwargs, partials, #partials) or
-        None (fp32, or no vectorizable tile: the caller runs the separate act backward). db: the
-        bias-gradient buffer -- the column sum is then fused into the GEMM where the tile allows."""
+        None (fp32, or no vectorizable tile: the caller runs the separate act backward)."""
         if self.f32:
             return None
         plan = H.igemm_cfg_for(mode, Bn, Hin, Win, Kc, Hout, Wout, N, None, bkn, dtype=self.dt)
@@ -441,15 +400,7 @@ class HipEngine:
         P = -(-M // bm) * phases
         part = self._stats_buf(name + ".actb", P, N)
         kw = dict(stats=part, bnb=(y, y, None, None, 0, act, True))
-        hold = {}
-        if db is not None:
-            def make(cfg):
-                if not self._fin_ok(cfg):
-                    return -1
-                hold["fused"] = True
-                return prog.bn_fin_sum(1, P, N, _p(db))
-            kw["fin"] = make
-        return kw, part, P, hold
+        return kw, part, P
 
     def _deconv_out(self, prog, name, x, w, y, B, L, pad, bias, act):
         """G's output layer: the direct narrow kernel for RGB / gray outputs (16-bit), else the
@@ -461,19 +412,18 @@ class HipEngine:
             self._igemm(prog, name, 1, x, w, y, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, pad,
                         bias=bias, act=act)
 
-    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema, fused=False, apply=True):
-        """BN finalize (+EMA) -- unless the statistics GEMM already ran it (fused) -- and
-        apply+act over `groups` row groups (apply=False: the consumer applies it, e.g. the head)."""
+    def _bn_fwd(self, prog, name, x, y, rows, C, groups, act, part, ppg, update_ema, apply=True):
+        """BN finalize (+EMA) and apply+act over `groups` row groups (apply=False: the consumer
+        applies it, e.g. the head)."""
         cfgm = self.cfg
         st = self.bn[name]
         bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
         P = self.model.d if name.startswith("d_") else self.model.g
         ema_m = bnstate.mean[name] if update_ema else None
         ema_v = bnstate.var[name] if update_ema else None
-        if not fused:
-            prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
-                             _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
-                             _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
+        prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
+                         _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
+                         _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
         if apply:
             prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
                               rows // groups, act, cfgm.lrelu_leak, 0)
@@ -542,13 +492,11 @@ class HipEngine:
                 P = self._stats_tiles(1, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout)
                 part = self._stats_buf(L.bn, P, L.cout)
                 rows = B * L.out_hw ** 2
-                hold = {}
                 self._igemm(prog, L.name, 1, a_prev, nat, self.g_x[L.name], B, L.in_hw, L.in_hw, L.cin, L.out_hw,
-                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part,
-                            fin=self._fin_fwd(prog, L.bn, rows, L.cout, 1, P, update_ema, hold))
+                            L.out_hw, L.cout, pad, bias=Pg[L.name + "/biases"], stats=part)
                 out_applies = L is self.gl[-2] and self._gout_applies_bn()
                 self._bn_fwd(prog, L.bn, self.g_x[L.name], self.g_a[L.name], rows, L.cout, 1, RELU, part, P,
-                             update_ema, fused=bool(hold), apply=not out_applies)
+                             update_ema, apply=not out_applies)
                 a_prev = self.g_a[L.name]
             elif self._gout_applies_bn():
                 # RGB layer: the lower layer's BN apply + ReLU in its halo staging (writes that
@@ -583,14 +531,13 @@ class HipEngine:
             else:
                 rpg = B * L.out_hw ** 2
                 P = self._stats_tiles(0, B2, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rpg, True)
-                hold = {}
                 if P is not None:
                     # BN partial statistics straight from the conv epilogue (tiles never straddle
                     # the real/fake boundary)
                     part = self._stats_buf(L.bn, P, L.cout)
                     self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                 L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part, rows_per_group=rpg,
-                                bkn=True, fin=self._fin_fwd(prog, L.bn, rows, L.cout, 2, P, update_ema, hold))
+                                bkn=True)
                 else:  # odd sizes: no tile divides the group -> separate group-aligned stats pass
                     self._igemm(prog, L.name, 0, prev, w, self.d_x[L.name], B2, L.in_hw, L.in_hw, L.cin, L.out_hw,
                                 L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], bkn=True)
@@ -601,7 +548,7 @@ class HipEngine:
                                   rpg, _p(part), 0)
                 head_bn = i == len(self.dl) - 1 and self._head_applies_bn()
                 self._bn_fwd(prog, L.bn, self.d_x[L.name], self.d_a[L.name], rows, L.cout, 2, LRELU, part, P // 2,
-                             update_ema, fused=bool(hold), apply=not head_bn)
+                             update_ema, apply=not head_bn)
             prev = self.d_a[L.name]
         lin = cfg.d_lin_name
         last = self.dl[-1]
@@ -639,8 +586,7 @@ class HipEngine:
                              self.coef[L.bn], write_param_grads=True, fused=fused_next)
             elif fused_next is not None:  # dx already stored by the upper dgrad GEMM; db from its partials
                 part, Pn = fused_next[0], fused_next[1]
-                if not (len(fused_next) > 2 and fused_next[2].get("fused")):  # (else summed by the GEMM)
-                    prog.sum_partials(L.name + ".dbias", _p(part), Pn, 2 * L.cout, L.cout, _p(gD[L.name + "/biases"]), 0)
+                prog.sum_partials(L.name + ".dbias", _p(part), Pn, 2 * L.cout, L.cout, _p(gD[L.name + "/biases"]), 0)
             else:  # live bias (no BN after it): db = sum over rows of dx, fused with the act backward
                 self._act_bwd_dbias(prog, L.name + ".act_bwd", da, a, dx, rows, L.cout, LRELU, gD[L.name + "/biases"],
                                     "d")
@@ -676,26 +622,22 @@ class HipEngine:
                     out = self.d_da[P_.name]
                     if P_.bn:
                         r = self._dgrad_bnb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
-                                            P_.bn, self.d_x[P_.name], self.d_a[P_.name], 2, LRELU,
-                                            fin=(Pd, gD, self.coef[P_.bn]))
+                                            P_.bn, self.d_x[P_.name], self.d_a[P_.name], 2, LRELU)
                         if r is not None:
-                            kw, fused = r[0], (r[1], r[2], r[3])
+                            kw, fused = r[0], (r[1], r[2])
                     else:
                         r = self._dgrad_actb(prog, 1, B2, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
-                                             P_.name, self.d_a[P_.name], LRELU, db=gD[P_.name + "/biases"])
+                                             P_.name, self.d_a[P_.name], LRELU)
                         if r is not None:
-                            kw, fused, out = r[0], (r[1], r[2], r[3]), self.d_dx[P_.name]
+                            kw, fused, out = r[0], (r[1], r[2]), self.d_dx[P_.name]
                     self._igemm(prog, L.name + ".dgrad", 1, dx, nat, out, B2, L.out_hw, L.out_hw, L.cout,
                                 L.in_hw, L.in_hw, L.cin, pad, **kw)
                 return fused
 
-            # (below the top layer, the data gradient first: it leads the chain, the weight gradient is a leaf)
-            if self.D_DGRAD_FIRST and i < len(self.dl) - 1:
-                fused_next = emit_dgrad()
-                emit_wgrad()
-            else:
-                emit_wgrad()
-                fused_next = emit_dgrad()
+            # weight gradient, then data gradient (dgrad-first measured neutral:
+            # profiles/r2/ab_d_dgrad_first_r2.txt)
+            emit_wgrad()
+            fused_next = emit_dgrad()
 
     def _w_mark(self, prog, progw, begin: int) -> None:
         """progW[begin:] (one layer's weight gradient) needs progA up to its current end."""
@@ -777,10 +719,8 @@ class HipEngine:
             mean = mean[row_offset_groups:row_offset_groups + 1]
             rstd = rstd[row_offset_groups:row_offset_groups + 1]
         rpg = rows // groups
-        done = False
         if fused is not None:
             part, ppg = fused[0], fused[1]
-            done = len(fused) > 2 and bool(fused[2].get("fused"))  # finalize ran inside the GEMM
             Pn = ppg * groups
         else:
             rpb = self._rows_per_block(rpg, C)
@@ -790,17 +730,10 @@ class HipEngine:
                           self.cfg.lrelu_leak, rows, C, rpb, rpg, _p(part), 0)
         dg = grads[name + "/gamma"] if write_param_grads else None
         db = grads[name + "/beta"] if write_param_grads else None
-        if not done:
-            prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg),
-                                 _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
-        # act' from the sign of the forward's pre-activation x * scale + shift (no read of y)
-        fsc, fsh = st["scale"], st["shift"]
-        if row_offset_groups is not None:
-            fsc = fsc[row_offset_groups:row_offset_groups + 1]
-            fsh = fsh[row_offset_groups:row_offset_groups + 1]
-        recompute = act in (RELU, LRELU) and self.BWD_ACT_FROM_X
+        prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg),
+                             _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
         prog.bn_bwd_apply(name + ".bwd_apply", _p(dy), _p(y), _p(x), _p(coef), _p(dx), rows, C, rpg, act,
-                          self.cfg.lrelu_leak, 0, _p(fsc) if recompute else 0, _p(fsh) if recompute else 0)
+                          self.cfg.lrelu_leak, 0)
 
     # ---- g_loss back through D(fake) (fake rows only, no D grads) and G backward
     def _build_gloss_and_g_backward(self, prog, progw):
@@ -833,14 +766,14 @@ class HipEngine:
                 if P_.bn:
                     r = self._dgrad_bnb(prog, 1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
                                         P_.bn, half(self.d_x[P_.name]), half(self.d_a[P_.name]), 1, LRELU,
-                                        group_offset=1, fin=(Pd, None, self.coef_g[P_.bn]))
+                                        group_offset=1)
                     if r is not None:
-                        kw, fused_next = r[0], (r[1], r[2], r[3])
+                        kw, fused_next = r[0], (r[1], r[2])
                 else:
                     r = self._dgrad_actb(prog, 1, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, False,
                                          "g." + P_.name, half(self.d_a[P_.name]), LRELU)
                     if r is not None:
-                        kw, fused_next, out = r[0], (r[1], r[2], r[3]), self.gc_dx[P_.name]
+                        kw, fused_next, out = r[0], (r[1], r[2]), self.gc_dx[P_.name]
                 self._igemm(prog, "g." + L.name + ".dgrad", 1, dx, nat, out, B, L.out_hw,
                             L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad, **kw)
             else:
@@ -893,11 +826,11 @@ class HipEngine:
                         0, gG[Lg.name + "/w"])
             self._w_mark(prog, progw, w0)
             r = self._dgrad_bnb(prog, 2, B, 1, 1, self.kp_g, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev,
-                                a_prev, 1, RELU, fin=(Pg, gG, self.coef[bn_prev]))
+                                a_prev, 1, RELU)
             fused_next = None
             kw = {}
             if r is not None:
-                kw, fused_next = r[0], (r[1], r[2], r[3])
+                kw, fused_next = r[0], (r[1], r[2])
             self._igemm(prog, Lg.name + ".dgrad", 2, self.g_last_col, wL, da_prev, B, 1, 1, self.kp_g, Lg.in_hw,
                         Lg.in_hw, Lg.cin, 0, bkn=True, kb_valid=25 * Lg.cout, **kw)
         else:
@@ -906,11 +839,11 @@ class HipEngine:
                         Lg.cin, padL, gG[Lg.name + "/w"])
             self._w_mark(prog, progw, w0)
             r = self._dgrad_bnb(prog, 0, B, Lg.out_hw, Lg.out_hw, Lg.cout, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev,
-                                x_prev, a_prev, 1, RELU, fin=(Pg, gG, self.coef[bn_prev]))
+                                x_prev, a_prev, 1, RELU)
             fused_next = None
             kw = {}
             if r is not None:
-                kw, fused_next = r[0], (r[1], r[2], r[3])
+                kw, fused_next = r[0], (r[1], r[2])
             self._igemm(prog, Lg.name + ".dgrad", 0, self.img_g, wL, da_prev, B, Lg.out_hw, Lg.out_hw, Lg.cout,
                         Lg.in_hw, Lg.in_hw, Lg.cin, padL, bkn=True, **kw)
         for j in range(n - 2, -1, -1):
@@ -929,11 +862,11 @@ class HipEngine:
                         gG[L.name + "/w"])
             self._w_mark(prog, progw, w0)
             r = self._dgrad_bnb(prog, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc,
-                                src, 1, RELU, fin=(Pg, gG, self.coef[bsrc]))
+                                src, 1, RELU)
             fused_next = None
             kw = {}
             if r is not None:
-                kw, fused_next = r[0], (r[1], r[2], r[3])
+                kw, fused_next = r[0], (r[1], r[2])
             self._igemm(prog, L.name + ".dgrad", 0, dx, self.wbf_g[L.name + "/w"], dsrc, B, L.out_hw, L.out_hw,
                         L.cout, L.in_hw, L.in_hw, L.cin, pad, bkn=True, **kw)
         # g_bn0 backward + projection gradients
@@ -995,13 +928,11 @@ class HipEngine:
     # 5.84 vs 5.70 ms, 256x256 106.2 vs 104.6 ms -- at the larger sizes the D chain (2B rows of
     # the bigger images) is the longer one already
     G_WGRAD_ON_D_STREAM: Optional[bool] = None
-    BWD_ACT_FROM_X = False  # act' from x and the forward coefficients: measured slower, ab_bwd_act_from_x_r2.txt
 
     def _g_wgrad_on_d_stream(self) -> bool:
         if self.G_WGRAD_ON_D_STREAM is not None:
             return bool(self.G_WGRAD_ON_D_STREAM)
         return self.cfg.output_size <= 64
-    D_DGRAD_FIRST = False  # A/B switch (profiles/r2/ab_d_dgrad_first_r2.txt)
 
     def _schedule(self) -> str:
         req = self._sched_req

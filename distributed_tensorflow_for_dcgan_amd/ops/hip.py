@@ -81,58 +81,6 @@ def igemm3_lds(cfg: int) -> int:
     return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
 
 
-# igemmh.hip (halo window in LDS, only the weights stream): cfg 400 + 10k + id, NS = (3, 2, 4)[k]
-IGEMMH_TILES = {0: (128, 128), 1: (128, 64), 2: (256, 64), 3: (64, 128), 4: (64, 64)}
-IGEMMH_STAGES = (3, 2, 4)
-
-
-def igemmh_shm(cfg: int, mode: int, Hout: int, Wout: int, Kc: int, pad_y: int = 1, pad_x: int = 1,
-               bnb: bool = False) -> Optional[int]:
-    """Dynamic LDS bytes of an igemmh launch (window of the largest phase + B ring, at least
-    the epilogue scratch), or None when the tile geometry is illegal for the shape or the LDS
-    exceeds 160 KiB. Mirrors the host checks of Program.igemm_ex (csrc/bindings.cpp)."""
-    if cfg < 400 or cfg % 10 not in IGEMMH_TILES or (cfg - 400) // 10 >= len(IGEMMH_STAGES):
-        return None
-    if mode not in (0, 1) or Kc not in (64, 128, 256, 512):
-        return None
-    bm, bn = IGEMMH_TILES[cfg % 10]
-    ns = IGEMMH_STAGES[(cfg - 400) // 10]
-    if mode == 0:
-        phases = [(Hout, Wout, 5, 5)]
-        ss = 2
-    else:
-        phases = []
-        for py in range(2):
-            for px in range(2):
-                hq, wq = (Hout - py + 1) // 2, (Wout - px + 1) // 2
-                if hq * wq == 0:
-                    continue
-                spy = 3 if (py + pad_y) % 2 == 0 else 2
-                spx = 3 if (px + pad_x) % 2 == 0 else 2
-                phases.append((hq, wq, spy, spx))
-        ss = 1
-    wp, tb = 0, None
-    for hq, wq, spy, spx in phases:
-        hw = hq * wq
-        if bm % wq:
-            return None
-        if bm <= hw:
-            if hw % bm:
-                return None
-            t_b, th = 1, bm // wq
-        else:
-            if bm % hw:
-                return None
-            t_b, th = bm // hw, hq
-        if tb is not None and t_b != tb:
-            return None
-        tb = t_b
-        wp = max(wp, t_b * (ss * (th - 1) + spy) * (ss * (wq - 1) + spx))
-    shm = -(-wp * (Kc // 8) // 64) * 1024 + ns * bn * 128
-    shm = max(shm, (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + (16384 if bnb else 0))
-    return shm if shm <= 160 * 1024 else None
-
-
 # igemm4.hip (halo window + loader waves): cfg 500 + 10k + id, B ring stages NSB = (4, 3)[k]; the
 # compute waves are 64x64 each (+ 4 loader waves); the window geometry is checked per shape by
 # Program.igemm4_plan (csrc/bindings.cpp)
@@ -159,14 +107,12 @@ IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)
 
 
 def tile_of(cfg: int, dtype: int = 0) -> Tuple[int, int]:
-    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..219 igemm3.hip; dtype 2
-    (fp32): igemm_f32.hip."""
+    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..239 igemm3.hip, 500..519
+    igemm4.hip; dtype 2 (fp32): igemm_f32.hip."""
     if dtype == 2:
         return IGEMM_F32_TILES[cfg]
     if cfg >= 500:
         return IGEMM4_TILES[cfg % 10]
-    if cfg >= 400:
-        return IGEMMH_TILES[cfg % 10]
     if cfg >= 200:
         return IGEMM3_TILES[cfg % 10]
     return IGEMM_CFGS[cfg % 100]
@@ -190,7 +136,7 @@ def pick_igemm_f32(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
 
 def bnb_fits(cfg: int) -> bool:
     """True when the tile's LDS can hold the fused BN-backward statistics scratch (epilogue.h)."""
-    if cfg >= 400:  # igemmh / igemm4 size their LDS per launch; igemm4's epilogue needs no C tile in LDS
+    if cfg >= 500:  # igemm4 sizes its LDS per launch; its epilogue needs no C tile in LDS
         return True
     bm, bn = tile_of(cfg)
     if cfg < 200:
@@ -261,7 +207,7 @@ TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "igemm_tun
 def tuned_table() -> dict:
     """Per-layer tile choices measured on MI355X by ``benchmarks/bench_kernels.py --write``
     (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> "cfg:splits" (or a bare cfg): cfg < 200 is
-    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip, 400..429 igemmh.hip)."""
+    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip, 500..519 igemm4.hip)."""
     global _TUNED
     if _TUNED is None:
         _TUNED = {}
@@ -462,22 +408,6 @@ def conv2d_transpose_same(x: torch.Tensor, w_packed: torch.Tensor, cout: int, ou
                   cout, 0, _p(bias), ACT[act], leak, _p(st), 0, int(bkn), -1, splits)
     run(prog)
     return (y, st) if stats else y
-
-
-def conv3_direct(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
-                 leak: float = 0.2) -> torch.Tensor:
-    """TF-SAME stride-2 5x5 conv with Cin <= 4 and Cout = 64 on the direct MFMA kernel
-    (conv3.hip: image tile staged in LDS, no column matrix). x [B,H,W,Cin], w HWIO [5,5,Cin,64]."""
-    _check_bf16(x, w)
-    B, Hh, Ww, C = x.shape
-    N = w.shape[-1]
-    Ho, Wo = -(-Hh // 2), -(-Ww // 2)
-    y = torch.empty(B, Ho, Wo, N, device=x.device, dtype=x.dtype)
-    prog = ext().Program(x.dtype == torch.float16)
-    prog.conv3_direct("conv3", _p(x), _p(w), _p(bias), _p(y), B, Hh, Ww, C, Ho, Wo, N, same_pads(Hh)[0],
-                      same_pads(Ww)[0], ACT[act], leak, 0)
-    run(prog)
-    return y
 
 
 NCONV_MAX_GRID = 512  # persistent workgroups of nconv (2 per CU: the kernel's occupancy)

@@ -183,11 +183,11 @@ def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
             close(out, gx, 2e-3, "G dgrad cfg%d s%d" % (cfg, splits))
 
 
-@pytest.mark.parametrize("cfg", [200, 211, 213, 206, 216, 217, 218, 403, 414])
+@pytest.mark.parametrize("cfg", [200, 211, 213, 206, 216, 217, 218])
 def test_igemm_fused_bn_backward_stats(cfg):
     """Data-gradient GEMM with the BN-backward statistics fused into its store pass (epilogue.h
     vec_store_bnb): stored dL/da == the plain GEMM's, partials sum to (sum g, sum g * xhat) with
-    g = dL/da * lrelu'(y), for 4- and 8-wave igemm3 tiles and igemmh."""
+    g = dL/da * lrelu'(y), for 4- and 8-wave igemm3 tiles."""
     h = H()
     B, Hi, Ci, Co = 4, 16, 128, 64
     Ho = 2 * Hi
@@ -197,9 +197,7 @@ def test_igemm_fused_bn_backward_stats(cfg):
     y = bf(rnd(B, Ho, Ho, Co, seed=63) - 0.3)
     mean = rnd(1, Co, scale=0.2, seed=64)
     rstd = rnd(1, Co, seed=65).abs() + 0.5
-    if cfg >= 400 and h.igemmh_shm(cfg, 1, Ho, Ho, Ci, bnb=True) is None:
-        pytest.skip("tile does not fit this shape")
-    if cfg < 400 and not h.bnb_fits(cfg):
+    if not h.bnb_fits(cfg):
         pytest.skip("tile has no LDS for the fused statistics")
     bm = h.tile_of(cfg)[0]
     mph = B * Hi * Hi
@@ -231,83 +229,6 @@ def test_igemm3_plain_im2col_bkn():
     for cfg in (201, 203, 205, 211):
         y = h.gemm_plain(col, w.reshape(75, Co).contiguous(), out_f32=True, cfg=cfg, bkn=True)
         close(y, ref, 2e-3, "im2col bkn cfg%d" % cfg)
-
-
-IGH = [400, 401, 402, 403, 404, 410, 411, 414, 420, 422, 424]
-IGH_TWIN = {0: 200, 1: 203, 2: 201, 3: 204, 4: 205}  # igemm3 tile with the same waves / fragments
-
-
-@pytest.mark.parametrize("B,Hs,Ci,Co", [(3, 16, 64, 128), (2, 32, 64, 128), (2, 16, 128, 256), (3, 8, 128, 64)])
-def test_igemmh_conv_tiles_layouts(B, Hs, Ci, Co):
-    """igemmh.hip (input window staged in LDS once per tile): every legal tile / ring depth, both
-    weight layouts, fused lrelu + BN statistics; band tiles (part of one image), whole-image
-    tiles and a last tile that runs past the batch (B = 3)."""
-    h = H()
-    Ho = -(-Hs // 2)
-    x = bf(rnd(B, Hs, Hs, Ci, seed=90))
-    w = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=91))
-    wt = h.pack_conv_weight(w.float(), "conv", "fwd")
-    ref_pre = R.conv2d_same(x.float(), w.float())
-    n = 0
-    for cfg in IGH:
-        if h.igemmh_shm(cfg, 0, Ho, Ho, Ci) is None or h.tile_of(cfg)[1] > Co:
-            continue
-        for bkn in (0, 1):
-            wp = w.reshape(25, Ci, Co).contiguous() if bkn else wt
-            y, st = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn))
-            tag = "igemmh cfg%d bkn%d" % (cfg, bkn)
-            close(y, R.lrelu(ref_pre), 1.5e-2, tag)
-            s = st.sum(0)
-            close(s[0], ref_pre.reshape(-1, Co).sum(0), 4e-3, "sum " + tag)
-            close(s[1], ref_pre.reshape(-1, Co).pow(2).sum(0), 4e-3, "sumsq " + tag)
-            # same k order, fragments and epilogue as the igemm3 tile of the same shape: same bits
-            y3, st3 = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=IGH_TWIN[cfg % 10], bkn=bool(bkn))
-            assert torch.equal(y, y3) and torch.equal(st, st3), "igemmh != igemm3 twin: " + tag
-            n += 1
-    assert n >= 1
-
-
-@pytest.mark.parametrize("B,Hi,Ci,Co", [(3, 8, 128, 64), (2, 16, 128, 64), (2, 4, 512, 256), (2, 8, 256, 128)])
-def test_igemmh_deconv_and_g_dgrad(B, Hi, Ci, Co):
-    """igemmh deconv (4 sub-pixel phases, 9/6/6/4-tap windows) with bias, and the G data
-    gradient (stride-2 conv of dY with the k-major deconv weight)."""
-    h = H()
-    Ho = 2 * Hi
-    x = bf(rnd(B, Hi, Hi, Ci, seed=92))
-    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=93))
-    bias = rnd(Co, scale=0.1, seed=94)
-    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
-    n = 0
-    for cfg in IGH:
-        if h.igemmh_shm(cfg, 1, Ho, Ho, Ci) is None or h.tile_of(cfg)[1] > Co:
-            continue
-        y, st = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True,
-                                        stats=True, cfg=cfg)
-        close(y, ref, 2e-3, "igemmh deconv cfg%d" % cfg)
-        close(st.sum(0)[0], ref.reshape(-1, Co).sum(0), 4e-3, "igemmh deconv stats cfg%d" % cfg)
-        y3, st3 = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True,
-                                          stats=True, cfg=IGH_TWIN[cfg % 10])
-        assert torch.equal(y, y3) and torch.equal(st, st3), "igemmh deconv != igemm3 twin cfg%d" % cfg
-        n += 1
-    assert n >= 1
-    xd = rnd(B, Hi, Hi, Ci, seed=95).requires_grad_(True)
-    yd = R.conv2d_transpose_same(xd, w.float(), (Ho, Ho))
-    dy = bf(rnd(B, Ho, Ho, Co, seed=96))
-    (gx,) = torch.autograd.grad(yd, xd, dy.float())
-    for cfg in IGH:
-        if h.igemmh_shm(cfg, 0, Hi, Hi, Co) is None or h.tile_of(cfg)[1] > Ci:
-            continue
-        out = h.conv2d_same(dy, w.reshape(25, Co, Ci), Ci, out_f32=True, cfg=cfg, bkn=True)
-        close(out, gx, 2e-3, "igemmh G dgrad cfg%d" % cfg)
-
-
-def test_igemmh_rejects_illegal_geometry():
-    h = H()
-    x = bf(rnd(2, 12, 12, 64, seed=97))   # 6x6 output grid: 64-row tiles are not whole grid rows
-    w = bf(rnd(25, 64, 128, scale=0.05, seed=98))
-    with pytest.raises(RuntimeError):
-        h.conv2d_same(x, w, 128, cfg=404, bkn=True)
-    assert h.igemmh_shm(404, 0, 6, 6, 64) is None
 
 
 def test_wgrad_conv_and_deconv():
@@ -443,13 +364,6 @@ def test_bn_forward_backward_groups():
     close(dgam, gg, 2e-2, "dgamma")
     close(dbet, gb, 2e-2, "dbeta")
     close(dx, gx, 3e-2, "dx")
-    # act' from the sign of x * scale + shift (no read of y): the same dx, bit for bit
-    dx2 = torch.empty_like(x)
-    pr = _prog()
-    pr.bn_bwd_apply("bapp2", _p(dy), 0, _p(x), _p(coef), _p(dx2), R_, C, R_ // groups, 2, 0.2, 0, _p(scale), _p(shift))
-    h.run(pr)
-    torch.cuda.synchronize()
-    assert torch.equal(dx2, dx)
 
 
 def test_adam_matches_tf_formula():
@@ -589,21 +503,6 @@ def test_narrow_deconv(B, Hi, Ho, C, N, dtype):
     yc = R.conv2d_same(xg, w.float())
     (gx,) = torch.autograd.grad(yc, xg, x.float())
     close(h.narrow_deconv(x, w, (Ho, Ho)), gx, 1e-2, "narrow as conv dgrad")
-
-
-@pytest.mark.parametrize("B,Hh,C,dtype", [(4, 64, 3, "bf16"), (2, 28, 1, "bf16"), (3, 33, 4, "bf16"),
-                                          (2, 64, 3, "fp16"), (1, 7, 3, "bf16")])
-def test_conv3_direct(B, Hh, C, dtype):
-    """Direct MFMA conv for D layer 0 (Cin <= 4 -> 64, + bias + lrelu): RGB, gray, 4-channel,
-    odd sizes (partial tiles, pad 2 at 7), fp16 build; vs the fp32 TF-SAME oracle."""
-    h = H()
-    edt = torch.float16 if dtype == "fp16" else torch.bfloat16
-    x = rnd(B, Hh, Hh, C, seed=70).to(edt)
-    w = rnd(5, 5, C, 64, scale=0.1, seed=71).to(edt)
-    bias = rnd(64, scale=0.1, seed=72)
-    y = h.conv3_direct(x, w, bias=bias, act="lrelu")
-    ref = R.lrelu(R.conv2d_same(x.float(), w.float(), bias))
-    close(y, ref, 1e-2, "conv3 direct")
 
 
 @pytest.mark.parametrize("B,Hi,Ho,N", [(4, 32, 64, 3), (3, 14, 28, 1), (2, 9, 17, 4)])
