@@ -332,8 +332,18 @@ class Program {
   // tile's input window at a constant pixel offset (tap table), stride-2 windows stored
   // column-split by parity. Returns the LDS bytes of the launch through *shm_out when non-null
   // (igemm4_plan, for the tile policy) without recording anything.
-  static bool igemm4_geometry(IG4Args& g, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x,
-                              int bm, int bn, int nsb, int wmc, std::string* why) {
+  // Host plan of one igemm4 launch: the kernel arguments, the LDS bytes and the per-step
+  // descriptor tables (ig4.h) the step loops read instead of walking the schedule themselves.
+  struct IG4Plan {
+    IG4Args g{};
+    size_t shm = 0;
+    int nwb = 1;
+    std::vector<IG4CDesc> cd;
+    std::vector<IG4LDesc> ld;
+  };
+  static bool igemm4_geometry(IG4Plan& plan, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x,
+                              int bm, int bn, int nsb, int wmc, bool bkn, std::string* why) {
+    IG4Args& g = plan.g;
     auto fail = [&](const char* m) { if (why) *why = m; return false; };
     if (mode != 0 && mode != 1) return fail("igemm4: conv (mode 0) or deconv (mode 1) only");
     if (Kc % 64) return fail("igemm4: Kc must be a multiple of 64");
@@ -424,30 +434,82 @@ class Program {
       }
       g.WXP = best_w;
     }
-    for (int p = 0; p < 4; ++p) { g.ntaps[p] = 0; g.oy_off[p] = 0; g.ox_off[p] = 0; }
+    int ntaps[4] = {0, 0, 0, 0}, tap[4][25];  // per phase: window pixel offset | weight tap << 16
+    for (int p = 0; p < 4; ++p) { g.oy_off[p] = 0; g.ox_off[p] = 0; g.send[p] = 0; }
     for (int p = 0; p < g.nphases; ++p) {
-      g.ntaps[p] = (int)ry[p].size();
-      if (g.ntaps[p] < nsb) return fail("igemm4: a phase has fewer taps than ring stages");
+      ntaps[p] = (int)ry[p].size();
+      if (ntaps[p] < nsb) return fail("igemm4: a phase has fewer taps than ring stages");
       g.oy_off[p] = oyo[p]; g.ox_off[p] = oxo[p];
-      for (int t = 0; t < g.ntaps[p]; ++t) {
+      for (int t = 0; t < ntaps[p]; ++t) {
         const int wy = ry[p][t] - miny, wx = rx[p][t] - minx;
         const int X = S == 2 ? (wx & 1) * g.HX + (wx >> 1) : wx;
-        g.tap[p][t] = (wy * g.WXP + X) | (wt[p][t] << 16);
+        tap[p][t] = (wy * g.WXP + X) | (wt[p][t] << 16);
       }
     }
     g.wpix = NI * g.WY * g.WXP;
     g.npw = (g.wpix * 10 + 63) / 64;  // 160-byte LDS pixels (igemm4.hip PIXS)
     g.win_bytes = g.npw * 1024;
-    g.nch = Kc / 64;
-    g.shared_win = g.nch == 1;
+    if (g.npw > 255) return fail("igemm4: window of more than 255 DMA pieces");
+    const int nch = Kc / 64;
+    const bool shared = nch == 1;
     g.ring_bytes = nsb * bn * 128;
     const int scratch = wmc * bn * 8 + 64;
-    g.nwb = (g.nch > 1 && g.ring_bytes + 2 * g.win_bytes + scratch <= 160 * 1024) ? 2 : 1;
-    if (g.ring_bytes + g.nwb * g.win_bytes + scratch > 160 * 1024) return fail("igemm4: window + ring exceed 160 KiB of LDS");
-    int steps = 0, w = 0;
-    for (int p = 0; p < g.nphases; ++p)
-      for (int c = 0; c < g.nch; ++c, ++w) steps += g.ntaps[p] + ((w > 0 && !g.shared_win && g.nwb == 1) ? nsb - 1 : 0);
+    int steps = 0;
+    const int nwb = (nch > 1 && g.ring_bytes + 2 * g.win_bytes + scratch <= 160 * 1024) ? 2 : 1;
+    for (int p = 0, w = 0; p < g.nphases; ++p)
+      for (int c = 0; c < nch; ++c, ++w) steps += ntaps[p] + ((w > 0 && !shared && nwb == 1) ? nsb - 1 : 0);
     g.steps = steps;
+    g.part_off = g.ring_bytes + nwb * g.win_bytes;
+    g.desc_off = g.part_off + scratch;
+    plan.nwb = nwb;
+    plan.shm = (size_t)g.desc_off + (size_t)8 * (steps + 1);
+    if (plan.shm > 160 * 1024) return fail("igemm4: window + ring exceed 160 KiB of LDS");
+    // the step schedule, unrolled (the order igemm4.hip's loaders and compute waves follow):
+    // phases, 64-channel chunks, taps; ahead of a chunk whose window reuses the only window
+    // buffer, NSB-1 empty steps (the loaders may overwrite it only once nobody reads it)
+    struct K { int p, c, t, nt, wl, sw, wlen; };
+    K k{0, 0, 0, ntaps[0], 0, 0, ntaps[0]};
+    const uint32_t bstage = (uint32_t)bn * 128;
+    plan.cd.assign(steps + 1, IG4CDesc{});
+    plan.ld.assign(steps, IG4LDesc{});
+    for (int x = 0; x < steps; ++x) {
+      const bool real = k.t >= 0;
+      const int tp = tap[k.p][std::max(k.t, 0)];
+      IG4CDesc& c = plan.cd[x];
+      c.uoff = (uint32_t)(g.ring_bytes + (nwb == 2 ? (k.wl & 1) : 0) * g.win_bytes + (tp & 0xffff) * 160);
+      c.soff = (uint32_t)(x % nsb) * bstage | (real ? 0u : IG4_EMPTY);
+      IG4LDesc& l = plan.ld[x];
+      const int wtap = tp >> 16, k0 = k.c * 64;
+      const size_t boff = bkn ? ((size_t)wtap * Kc + k0) * N * 2 : ((size_t)wtap * N * Kc + k0) * 2;
+      if (boff >= IG4_EMPTY) return fail("igemm4: weight tensor beyond 2 GiB");
+      l.boff = real ? (uint32_t)boff : IG4_EMPTY;
+      l.soff = (uint32_t)(x % nsb) * bstage;
+      l.win = 0;
+      if (!shared) {
+        if (nwb == 2) {  // the NEXT window streams in slices over this window's steps NSB-1 .. wlen-1
+          const bool last_win = (k.c + 1 == nch) && (k.p + 1 == g.nphases);
+          if (!last_win && k.sw >= nsb - 1) {
+            const int ns = k.wlen - (nsb - 1), i = k.sw - (nsb - 1);
+            const int ch = k.c + 1 == nch ? 0 : k.c + 1;
+            l.win = (uint32_t)(i * g.npw / ns) | (uint32_t)((i + 1) * g.npw / ns) << 8 | (uint32_t)((k.wl + 1) & 1) << 16 |
+                    (uint32_t)ch << 17;
+          }
+        } else if (k.wl > 0 && k.t == 0) {  // behind NSB-1 empty steps: the old window is dead
+          l.win = (uint32_t)g.npw << 8 | (uint32_t)k.c << 17;
+        }
+      }
+      g.send[k.p] = x + 1;
+      // next step
+      ++k.t; ++k.sw;
+      if (k.t < k.nt) continue;
+      if (++k.c == nch) { k.c = 0; ++k.p; }
+      if (k.p >= g.nphases) { k.p = g.nphases - 1; k.t = 0; k.nt = 1 << 20; continue; }
+      if (!shared) ++k.wl;
+      const int pre = (!shared && nwb == 1) ? nsb - 1 : 0;
+      k.nt = ntaps[k.p]; k.t = -pre; k.sw = 0; k.wlen = pre + k.nt;
+    }
+    plan.cd[steps] = plan.cd[steps - 1];  // the last step's (unused) prefetch
+    plan.cd[steps].soff |= IG4_EMPTY;
     g.fd_hw = fastdiv_make(HW); g.fd_tw = fastdiv_make(TR * Wq); g.fd_wq = fastdiv_make(Wq);
     g.fd_wimg = fastdiv_make(g.WY * g.WXP); g.fd_wxp = fastdiv_make(g.WXP);
     g.mtiles = (int)(((size_t)Bn * HW) / bm);
@@ -459,11 +521,11 @@ class Program {
   py::tuple igemm4_plan(int cfg, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x) {
     int bm, bn, nsb, wmc, wnc;
     if (dt_ == 2 || KF(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wmc, &wnc)) return py::make_tuple(-1, std::string("bad cfg"));
-    IG4Args g{};
+    IG4Plan plan;
     std::string why;
-    if (!igemm4_geometry(g, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, &why))
+    if (!igemm4_geometry(plan, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, false, &why))
       return py::make_tuple(-1, why);
-    return py::make_tuple(g.ring_bytes + g.nwb * g.win_bytes + wmc * bn * 8 + 64, std::string("nwb=") + std::to_string(g.nwb));
+    return py::make_tuple((int)plan.shm, std::string("nwb=") + std::to_string(plan.nwb));
   }
 
   int igemm4_ex(const std::string& name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win,
@@ -473,10 +535,13 @@ class Program {
     int bm, bn, nsb, wmc, wnc;
     if (dt_ == 2 || KF(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wmc, &wnc))
       throw std::runtime_error("bad igemm4 cfg " + std::to_string(cfg) + " for this element type");
-    IG4Args a{};
+    IG4Plan plan;
     std::string why;
-    if (!igemm4_geometry(a, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, &why))
+    if (!igemm4_geometry(plan, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, bkn != 0, &why))
       throw std::runtime_error(why);
+    IG4Args& a = plan.g;
+    a.cdesc = reinterpret_cast<const IG4CDesc*>(dev_alloc(plan.cd.size() * sizeof(IG4CDesc), plan.cd.data()));
+    a.ldesc = reinterpret_cast<const IG4LDesc*>(dev_alloc(plan.ld.size() * sizeof(IG4LDesc), plan.ld.data()));
     if ((mode == 0 && (Hout != (Hin + 1) / 2 || Wout != (Win + 1) / 2)) || (mode == 1 && (Hout != 2 * Hin || Wout != 2 * Win)))
       throw std::runtime_error("igemm4: stride-2 SAME shapes only");
     if (ldc % 4 || cofs % 4 || ldc < cofs + N) throw std::runtime_error("igemm4: 8-byte output rows");
@@ -514,7 +579,7 @@ class Program {
     if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
     last_mtiles_ = a.mtiles;
     last_nphases_ = a.nphases;
-    const size_t shm = (size_t)a.ring_bytes + (size_t)a.nwb * a.win_bytes + (size_t)wmc * bn * 8 + 64;
+    const size_t shm = plan.shm;
     const unsigned blocks = (unsigned)(a.mtiles * a.ntiles);
     return add(name, stream, [this, a, cfg, bkn, blocks, shm](hipStream_t s) {
       return KF(dcg_igemm4_launch)(&a, cfg, bkn, blocks, shm, s);

@@ -93,61 +93,26 @@ __device__ __forceinline__ int kn_swz(int r) {  // as igemm3.hip (k-major B rows
   else return 4 * ((r >> 3) & 1);
 }
 
-// The schedule constants in SGPRs: read once from the kernel arguments (indexing the kernarg arrays
-// with a runtime value inside the K loop would be an s_load per step, and its s_waitcnt lgkmcnt(0)
-// also waits for every outstanding ds_read -- it serialised fragment reads and MFMAs).
-struct Sched {
-  int nt0, nt1, nt2, nt3, nch, nph, shared, nwb;
-  __device__ __forceinline__ int ntaps(int p) const { return p == 0 ? nt0 : p == 1 ? nt1 : p == 2 ? nt2 : nt3; }
-};
-
-__device__ __forceinline__ Sched sched_of(const IG4Args& a) {
-  Sched q;
-  q.nt0 = a.ntaps[0]; q.nt1 = a.ntaps[1]; q.nt2 = a.ntaps[2]; q.nt3 = a.ntaps[3];
-  q.nch = a.nch; q.nph = a.nphases; q.shared = a.shared_win; q.nwb = a.nwb;
-  return q;
+// descriptor loads through the constant address space: uniform, so scalar loads (s_load), which
+// the compiler may use only when the kernel's own stores cannot alias the table -- through a
+// generic pointer it emitted a vector load and waited for it (vmcnt) on every step
+__device__ __forceinline__ IG4CDesc ld_desc(const IG4CDesc* p, int i) {
+  typedef __attribute__((address_space(4))) const uint32_t cu32;
+  cu32* q = (cu32*)p + 2 * i;
+  IG4CDesc d;
+  d.uoff = q[0];
+  d.soff = q[1];
+  return d;
 }
-
-// Step cursor (wave-uniform): phase p, channel chunk c, tap t (t < 0: empty step ahead of a
-// reloaded window when only one window buffer fits), taps in this phase nt, window load ordinal
-// wl, steps taken in the current window sw, steps in it wlen.
-struct Cur {
-  int p, c, t, nt, wl, sw, wlen;
-};
-
-template <int NSB>
-__device__ __forceinline__ void cur_init(Cur& k, const Sched& q) {
-  k.p = 0; k.c = 0; k.t = 0; k.nt = q.nt0; k.wl = 0; k.sw = 0; k.wlen = q.nt0;
-}
-
-// one step: the common case is a compare and a (rarely taken) branch -- with the phase's tap
-// count re-derived on every step (a switch) the loop's scalar work was ~400 cycles per step.
-// (Kept one function: split into an inlined helper with an early return, the cursor lost its
-// uniformity -- the whole step loop went to VGPRs and exec-mask branches.)
-template <int NSB>
-__device__ __forceinline__ void cur_next(Cur& k, const Sched& q) {
-  ++k.t;
-  ++k.sw;
-  if (__builtin_expect(k.t < k.nt, 1)) return;
-  if (++k.c == q.nch) { k.c = 0; ++k.p; }
-  if (k.p >= q.nph) { k.p = q.nph - 1; k.t = 0; k.nt = 1 << 20; return; }  // past the end: a valid tap, never consumed
-  const bool load = !q.shared;
-  if (load) ++k.wl;
-  const int pre = (load && q.nwb == 1) ? NSB - 1 : 0;
-  k.nt = q.ntaps(k.p);
-  k.t = -pre;
-  k.sw = 0;
-  k.wlen = pre + k.nt;
-}
-
-// tap table entry (phase p, tap t) from a lane-distributed copy: lane i of v0 / v1 holds entry i /
-// 64 + i of the flat [4][25] table (v_readlane: no memory access in the K loop)
-__device__ __forceinline__ int tap_of(int v0, int v1, int p, int t) {
-  const int i = p * 25 + t;
-  // both lanes read, then a scalar select: no branch splits the K-loop body's basic block
-  const int x0 = __builtin_amdgcn_readlane(v0, i & 63);
-  const int x1 = __builtin_amdgcn_readlane(v1, max(i - 64, 0));
-  return i < 64 ? x0 : x1;
+__device__ __forceinline__ IG4LDesc ld_desc(const IG4LDesc* p, int i) {
+  typedef __attribute__((address_space(4))) const uint32_t cu32;
+  cu32* q = (cu32*)p + 4 * i;
+  IG4LDesc d;
+  d.boff = q[0];
+  d.soff = q[1];
+  d.win = q[2];
+  d.pad = 0;
+  return d;
 }
 
 // scheduling recipe of an MFMA cluster (NM MFMAs) and NR fragment reads for the next one:
@@ -375,12 +340,12 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
   lds_char* const l3 = (lds_char*)lds;
   const uint32_t lbase = (uint32_t)(uintptr_t)l3;
   const uint32_t win0 = (uint32_t)a.ring_bytes;  // window buffers after the ring
-  lds_f32* part = reinterpret_cast<lds_f32*>(l3 + a.ring_bytes + a.nwb * a.win_bytes);
+  lds_f32* part = reinterpret_cast<lds_f32*>(l3 + a.part_off);
   lds_i32* ctr = reinterpret_cast<lds_i32*>(part + WMC * BN * 2);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // diagnostics: 12 s_memtime stamps per workgroup (8 kernel entry, 9 tap table loaded,
+  // diagnostics: 12 s_memtime stamps per workgroup (8 kernel entry, 9 tile decoded,
   // 0-3 compute wave 0, 4-7 loader wave 0)
   unsigned long long* const stw = a.stamps ? a.stamps + (size_t)blockIdx.x * 12 : nullptr;
   if (stw && wave == 0 && lane == 0) stw[8] = __builtin_amdgcn_s_memtime();
@@ -397,11 +362,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
   const int b0 = (int)fdiv((uint32_t)m0, a.fd_hw);
   const int y0 = (int)fdiv((uint32_t)(m0 - b0 * a.Hq * a.Wq), a.fd_wq);
   const int S_ = a.steps;
-  const Sched q = sched_of(a);
-  const int* tflat = &a.tap[0][0];
-  int vt0 = tflat[lane], vt1 = lane < 36 ? tflat[64 + lane] : 0;
-  asm volatile("" : "+v"(vt0), "+v"(vt1));  // loaded (and waited for) here, not re-loaded in the K loop
-  if (stw && wave == 0 && lane == 0) stw[9] = __builtin_amdgcn_s_memtime() + (unsigned)(vt0 & 0);
+  if (stw && wave == 0 && lane == 0) stw[9] = __builtin_amdgcn_s_memtime();
 
   if (tid < 64 && lane < WNC) ctr[lane] = 0;
 
@@ -435,61 +396,45 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     const int lid = wave - NC;
     const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.Bw, a.b_bytes);
     const int Kc = a.Kc, N = a.N;
-    auto issue_win = [&](int q0, int q1, int buf, int ch) -> int { return issue_win_w(q0, q1, buf, ch, lid, NL); };
-    // B pieces of step k (one 64-deep k slice of weight tap wt) into ring slot `slot`
-    auto issue_b = [&](const Cur& k, int slot) {
-      const int wt = tap_of(vt0, vt1, k.p, k.t) >> 16;
-      const int k0 = k.c * 64;
-      const uint32_t dst0 = lbase + (uint32_t)slot * BSTAGE;
+    // per-lane part of each B piece's global byte offset (the step's (tap, k0) part is uniform:
+    // IG4LDesc::boff)
+    uint32_t boff_l[PBL];
 #pragma unroll
-      for (int i = 0; i < PBL; ++i) {
-        const int q = lid * PBL + i;
-        uint32_t off;
-        if constexpr (BKN) {
-          const int rr = q * (1024 / SB) + lane / (SB / 16);
-          const int n = n0 + ((lane % (SB / 16)) ^ (kn_swz<SB>(rr) >> 1)) * 8;
-          off = (uint32_t)(((wt * Kc + k0 + rr) * N + n) * 2);
-        } else {
-          const int r = q * 8 + (lane >> 3);
-          const int j = (lane & 7) ^ sw8(r);
-          // stage row r holds channel n0 + ig4::pair_perm(r) (the epilogue's 16-byte stores)
-          off = (uint32_t)(((wt * N + n0 + ig4::pair_perm(r)) * Kc + k0 + j * 8) * 2);
-        }
-        dma16_asm_la(rb, dst0 + q * 1024, off);
+    for (int i = 0; i < PBL; ++i) {
+      const int q = lid * PBL + i;
+      if constexpr (BKN) {
+        const int rr = q * (1024 / SB) + lane / (SB / 16);
+        const int n = n0 + ((lane % (SB / 16)) ^ (kn_swz<SB>(rr) >> 1)) * 8;
+        boff_l[i] = (uint32_t)((rr * N + n) * 2);
+      } else {
+        const int r = q * 8 + (lane >> 3);
+        const int j = (lane & 7) ^ sw8(r);
+        // stage row r holds channel n0 + ig4::pair_perm(r) (the epilogue's 16-byte stores)
+        boff_l[i] = (uint32_t)(((n0 + ig4::pair_perm(r)) * Kc + j * 8) * 2);
       }
-    };
-    // everything stage x (= step of cursor k) carries for this loader; returns its DMA count
-    auto issue_stage = [&](const Cur& k, int slot) -> int {
-      int n = 0;
+    }
+    // everything stage x carries for this loader; returns its DMA count
+    auto issue_stage = [&](int x) -> int {
       if (a.ablate & 2) return 0;  // timing study: no DMA at all
-      if (k.t >= 0) { issue_b(k, slot); n += PBL; }
-      if (!a.shared_win) {
-        if (a.nwb == 2) {
-          // the NEXT window streams in slices over this window's steps NSB-1 .. wlen-1
-          const bool last_win = (k.c + 1 == q.nch) && (k.p + 1 == q.nph);
-          if (!last_win && k.sw >= NSB - 1) {
-            const int ns = k.wlen - (NSB - 1), i = k.sw - (NSB - 1);
-            const int ch = k.c + 1 == q.nch ? 0 : k.c + 1;
-            n += issue_win(i * a.npw / ns, (i + 1) * a.npw / ns, (k.wl + 1) & 1, ch);
-          }
-        } else if (k.wl > 0 && k.t == 0) {
-          n += issue_win(0, a.npw, 0, k.c);  // behind NSB-1 empty steps: the old window is dead
-        }
+      const IG4LDesc d = ig4::ld_desc(a.ldesc, x);
+      int n = 0;
+      if (!(d.boff & IG4_EMPTY)) {
+        const uint32_t dst0 = lbase + d.soff;
+#pragma unroll
+        for (int i = 0; i < PBL; ++i) dma16_asm_la(rb, dst0 + (lid * PBL + i) * 1024, d.boff + boff_l[i]);
+        n = PBL;
       }
+      const int q0 = d.win & 255, q1 = (d.win >> 8) & 255;
+      if (q0 < q1) n += issue_win_w(q0, q1, (d.win >> 16) & 1, d.win >> 17, lid, NL);
       return n;
     };
 
     unsigned long long* st = (lid == 0 && lane == 0) ? stw : nullptr;
     if (st) st[4] = __builtin_amdgcn_s_memtime();
-    Cur ki;
-    cur_init<NSB>(ki, q);
     int cnt[NSB];
     if (!(a.ablate & 2)) issue_win_w(0, a.npw, 0, 0, wave, NC + NL);  // window 0: every wave issues a share
 #pragma unroll
-    for (int x = 0; x < NSB - 1; ++x) {
-      cnt[x] = 0;
-      if (x < S_) { cnt[x] = issue_stage(ki, x % NSB); cur_next<NSB>(ki, q); }
-    }
+    for (int x = 0; x < NSB - 1; ++x) cnt[x] = x < S_ ? issue_stage(x) : 0;
     // stages 0 and 1 (and window 0) landed at barrier 0
     if constexpr (NSB == 4) wvm_dyn(cnt[2]);
     else wvm<0>();
@@ -498,8 +443,7 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
     if (st) st[6] = __builtin_amdgcn_s_memtime();
     for (int s = 0; s + 1 < S_; ++s) {
       const int x = s + NSB - 1;
-      int cx = 0;
-      if (x < S_) { cx = issue_stage(ki, x % NSB); cur_next<NSB>(ki, q); }
+      const int cx = x < S_ ? issue_stage(x) : 0;
       // stage s+2 landed at barrier s+1 (stage s+3 = x may stay in flight when NSB = 4)
       if constexpr (NSB == 4) wvm_dyn(cx);
       else wvm<0>();
@@ -540,20 +484,12 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
 #pragma unroll
     for (int im = 0; im < FM; ++im) acc[jn][im] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // fragments of k-half h (32 of the 64 k rows) of the step at cursor k
-  const int win_bytes = __builtin_amdgcn_readfirstlane(a.win_bytes);
-  const int wl_mask = __builtin_amdgcn_readfirstlane(a.nwb == 2 ? 1 : 0);
-  auto read_frags = [&](int h, const Cur& k, int slot, elem8 (&af)[FM], elem8 (&wf)[FN]) {
-    // wave-uniform part (window buffer + tap offset + k half) computed in SGPRs (the cursor
-    // fields are pinned scalar: a select of them in VGPRs cost a v_mul_lo_u32 per read block)
-    const int kp_ = __builtin_amdgcn_readfirstlane(k.p), kt_ = __builtin_amdgcn_readfirstlane(k.t);
-    const int kwl = __builtin_amdgcn_readfirstlane(k.wl);
-    const int toff = tap_of(vt0, vt1, kp_, max(kt_, 0)) & 0xffff;
-    const int uoff = (int)win0 + (kwl & wl_mask) * win_bytes + toff * PIXB + h * 64;
-    const lds_char* wb = l3 + uoff;
+  // fragments of k-half h (32 of the 64 k rows) of the step with descriptor d (uoff, soff in SGPRs)
+  auto read_frags = [&](int h, uint32_t uoff, uint32_t soff, elem8 (&af)[FM], elem8 (&wf)[FN]) {
+    const lds_char* wb = l3 + (uoff + h * 64);
 #pragma unroll
     for (int im = 0; im < FM; ++im) af[im] = *LDS_PTR(const elem8, wb + pb[im]);
-    const lds_char* sb = l3 + slot * BSTAGE;
+    const lds_char* sb = l3 + (soff & ~IG4_EMPTY);
     if constexpr (BKN) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
@@ -610,50 +546,75 @@ __global__ __launch_bounds__(64 * (WMC * WNC + ig4::NL)) void igemm4_kernel(IG4A
 
   unsigned long long* stc = (wave == 0 && lane == 0) ? stw : nullptr;
   if (stc) stc[0] = __builtin_amdgcn_s_memtime();
-  // the compute waves' share of window 0 (they are idle until barrier 0 anyway)
-  if (!(a.ablate & 2)) {
-    issue_win_w(0, a.npw, 0, 0, wave, NC + NL);
-    ig4::wvm<0>();
+  // the compute waves' share of window 0 (they are idle until barrier 0 anyway) and the copy of
+  // the step descriptors into LDS (landed before barrier 0)
+  if (!(a.ablate & 2)) issue_win_w(0, a.npw, 0, 0, wave, NC + NL);
+  for (int i = tid; i < S_ + 1; i += 64 * NC) {
+    const IG4CDesc d = ig4::ld_desc(a.cdesc, i);
+    *LDS_PTR(unsigned long long, l3 + a.desc_off + i * 8) = (unsigned long long)d.uoff | ((unsigned long long)d.soff << 32);
   }
-  Cur k, k1;
-  cur_init<NSB>(k, q);
-  k1 = k;
-  cur_next<NSB>(k1, q);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // The step descriptors: copied into LDS in the prologue, and 64 at a time from there into two
+  // VGPRs (lane i = step base + i); a step takes its successor's with two v_readlane -- no memory
+  // access, so no wait, in the step loop (a scalar load there turned every LDS wait in its
+  // shadow into lgkmcnt(0): SMEM returns out of order; an LDS read of it forced a drain at the
+  // register hand-over). The 64-step window is refilled once every 64 steps.
+  const lds_char* cdl = l3 + a.desc_off;
+  uint32_t vdu = 0, vds = 0;
+  auto fill_cd = [&](int base) {
+    const unsigned long long v = *LDS_PTR(const unsigned long long, cdl + min(base + lane, S_) * 8);
+    vdu = (uint32_t)v;
+    vds = (uint32_t)(v >> 32);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto cd_at = [&](int i) -> IG4CDesc {  // i - (the window base) in [0, 64)
+    IG4CDesc d;
+    d.uoff = __builtin_amdgcn_readlane(vdu, i);
+    d.soff = __builtin_amdgcn_readlane(vds, i);
+    return d;
+  };
   elem8 a0[FM], w0[FN], a1[FM], w1[FN];
   barrier_study(a.ablate);  // B_0: stages 0, 1 and window 0 landed
   if (stc) stc[1] = __builtin_amdgcn_s_memtime();
+  fill_cd(0);
+  IG4CDesc d0 = cd_at(0);
   const bool study_nomfma = (a.ablate & 1) != 0;
-  // every step ends by reading the first k-half of the NEXT step (stage s+1 landed at B_s); for
-  // the last step, or ahead of empty steps, the read is clamped to the current step (unused).
-  // Empty steps do the same, so the first real step after them finds its fragments ready.
-  if (!study_nomfma) read_frags(0, k, 0, a0, w0);
+  // every step ends by reading the first k-half of the NEXT step (stage s+1 landed at B_s); an
+  // empty step's descriptor points at valid LDS, so its reads need no clamping (data unused), and
+  // the last empty step's prefetch is the first real step's first half.
+  if (!study_nomfma) read_frags(0, d0.uoff, d0.soff, a0, w0);
   // phases outer, steps inner: the epilogue code sits between the loops, so the hot loop body
   // stays a few hundred bytes of code (inlined into the step loop, the epilogue variants spread
   // every iteration over tens of KiB: instruction-cache misses cost more than the MFMAs)
   int s = 0;
-  for (int p = 0; p < q.nph; ++p) {
-    for (; s < S_ && k.p == p; ++s) {
+  for (int p = 0; p < a.nphases; ++p) {
+    const int send = a.send[p];
+    for (; s < send; ++s) {
       if (s > 0) barrier_study(a.ablate);  // B_s: stage s+1 landed, every compute wave done with step s-1
-      const bool nxt = s + 1 < S_ && k1.t >= 0;
-      const Cur kp = nxt ? k1 : k;
-      const int slotp = (nxt ? s + 1 : s) % NSB;
+      if (__builtin_expect(((s + 1) & 63) == 0, 0)) fill_cd(s + 1);
+      const IG4CDesc d1 = cd_at((s + 1) & 63);
       if (!study_nomfma) {
         // the k-half-1 fragment reads are interleaved with the first MFMA cluster (they land
         // long before the second needs them): one compute wave per SIMD, so an un-interleaved
         // read / address block would leave the matrix core idle. The next step's k-half-0 reads
-        // run on every path (an empty step's are what the first real step after it consumes):
-        // one definition of a0 / w0, so no register copies at the join.
-        const bool real = k.t >= 0;
+        // run on every path: one definition of a0 / w0, so no register copies at the join.
+        const bool real = !(d0.soff & IG4_EMPTY);
         if (real) {
-          read_frags(1, k, s % NSB, a1, w1);
+          read_frags(1, d0.uoff, d0.soff, a1, w1);
           mfmas(a0, w0);
           ig4::interleave<FM * FN, FM + FN>();
+        } else {
+          // an empty step consumes its (unused) first-half fragments too: both paths reach the
+          // next reads with nothing in flight into a0 / w0, so no waits for them there
+#pragma unroll
+          for (int im = 0; im < FM; ++im) asm volatile("" ::"v"(a0[im]));
+#pragma unroll
+          for (int jn = 0; jn < FN; ++jn) asm volatile("" ::"v"(w0[jn]));
         }
-        read_frags(0, kp, slotp, a0, w0);
+        read_frags(0, d1.uoff, d1.soff, a0, w0);
         if (real) mfmas(a1, w1);
       }
-      k = k1;
-      cur_next<NSB>(k1, q);
+      d0 = d1;
     }
     if (stc) stc[2] = __builtin_amdgcn_s_memtime();
     epilogue(p);
