@@ -126,6 +126,8 @@ def main():
                        "global_batch": args.batch_size * args.gpus, "per_gpu_batch": args.batch_size,
                        "seq_len": None, "parallelism": "dp%d" % args.gpus, "engine": eng.name,
                        "hip_graph": bool(getattr(eng, "graph_enabled", False)),
+                       "schedule": eng._schedule() if hasattr(eng, "_schedule") else None,
+                       "graphs_per_step": len(getattr(eng, "_graphs", [])) or None,
                        "backend": backend, "world_size": world_seen, "devices": devices,
                        "kernels_per_step": eng.kernel_count() if hasattr(eng, "kernel_count") else None,
                        "gflop_per_image": round(cfg.flops_per_image() / 1e9, 4),

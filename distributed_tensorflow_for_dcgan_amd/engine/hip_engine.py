@@ -19,15 +19,20 @@ graph launches:
   progC          TF-Adam(G), TF-Adam(D), beta powers, global step (device-resident); each
                  Adam also writes the 16-bit weight mirror the next step's GEMMs read
 
-Schedules (``_schedule``), all three covered by the stream-hazard checker
+Schedules (``_schedule``), all covered by the stream-hazard checker
 (``engine/schedule_check.py``) and by GPU bit-exactness tests:
   "fused"       single process: ONE hipGraph; the two backward chains on two streams; ONE
                 Adam launch for both models after the join (16-bit dtypes)
-  "concurrent"  DDP (and the per-phase timed step): the same two chains cut into 6 graph
-                segments so the collectives are issued between them from the host -- D's top
-                layer + head (76 % of D's gradient bytes at 64x64) as soon as the D chain has
-                produced it, G's gradients when the G chain ends, the rest of D's when the D
-                chain ends; Adam(G) waits for G's collective only, Adam(D) for all
+  "ddp"         DDP over RCCL (default): the fused schedule with the gradient all-reduces on a
+                comm stream INSIDE the same single hipGraph (RCCL collectives are captured) --
+                D's top layer + head as soon as the D chain has produced it, the rest of D's when
+                that chain ends, then G's gradients in per-layer buckets as G's weight gradients
+                land (``_g_cuts``); Adam(D) runs under G's last collective, Adam(G) after it
+  "concurrent"  DDP over gloo (host-synchronous collectives cannot be captured) and the
+                per-phase timed step: the two chains cut into 6 graph segments, the collectives
+                issued between them from the host -- D's top layer + head (76 % of D's gradient
+                bytes at 64x64) as soon as the D chain has produced it, G's gradients when the G
+                chain ends, the rest of D's when the D chain ends
   "serial"      ``schedule="serial"`` / DCGAN_SERIAL_DBWD=1: fwd + G chain, then the D chain, as
                 5 segments (the G all-reduce overlaps D's backward)
 
@@ -56,7 +61,7 @@ from ..parallel import dist as D
 
 RELU, LRELU, TANH, NONE = 1, 2, 3, 0
 DTYPES = {"bf16": (0, torch.bfloat16), "fp16": (1, torch.float16), "fp32": (2, torch.float32)}
-SCHEDULES = ("fused", "concurrent", "serial")
+SCHEDULES = ("fused", "ddp", "concurrent", "serial")
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
@@ -268,6 +273,7 @@ class HipEngine:
         self.progB = self._prog()
         self.progW = self._prog()  # G's weight gradients (see _build_gloss_and_g_backward)
         self._g_w: List[Tuple[int, int]] = []
+        self._g_w_layer: List[str] = []
         self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
         self._a_fwd = self.progA.size()  # forward done: D's d_loss backward may start from here
         self._build_gloss_and_g_backward(self.progA, self.progW)
@@ -276,6 +282,7 @@ class HipEngine:
         # D-gradient slice final after the D chain's first segment: the top conv layer (+ its BN)
         # and the head, which the ParamSet lays out last
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
+        self._g_cuts = self._g_bucket_cuts()
         self.progCast = self._prog()  # fp32 masters -> 16-bit mirrors (init / checkpoint load)
         if not self.f32:
             for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
@@ -290,13 +297,14 @@ class HipEngine:
         the join of the two backward chains). "serial" runs Adam(G) first (progC[:_c_split],
         overlapping D's all-reduces), then Adam(D) + the step counter; "concurrent" -- whose D
         chain ends first -- runs Adam(D) first (overlapping G's all-reduce), then Adam(G) + the
-        step counter. fp16: one overflow check gates both, everything in the second part."""
+        step counter ("ddp" likewise). fp16: one overflow check gates both, everything in the
+        second part."""
         self.progC = self._prog()
         sch = self._schedule()
         if sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
             self._c_split = self.progC.size()
-        elif sch == "concurrent" and not self.f16:
+        elif sch in ("concurrent", "ddp") and not self.f16:
             self._build_update_d_first(self.progC)
         else:
             self._build_update(self.progC, first=True)
@@ -639,10 +647,31 @@ class HipEngine:
             emit_wgrad()
             fused_next = emit_dgrad()
 
-    def _w_mark(self, prog, progw, begin: int) -> None:
-        """progW[begin:] (one layer's weight gradient) needs progA up to its current end."""
+    def _g_bucket_cuts(self) -> List[Tuple[int, int, int]]:
+        """G's gradient buckets for the "ddp" schedule: (progW piece index, lo, hi) -- after G's
+        weight-gradient piece k the flat slice [lo, hi) is final (that layer's weights, biases and
+        BN parameters, whose BN backward precedes the piece's mark, plus every later layer's);
+        a last bucket [0, lo) (projection + g_bn0, written at the end of progA) follows the join.
+        Default: cut after the two lowest G deconvs (the largest weight tensors; at 64x64: 4.1 MB
+        after g_h2, 13.1 MB after g_h1, 3.3 MB last). DCGAN_G_CUTS=g_h2,g_h1 names them."""
+        env = os.environ.get("DCGAN_G_CUTS")
+        names = ([s for s in env.split(",") if s] if env is not None else
+                 [L.name for L in self.gl[:-1][:2]])
+        offs = self.model.g.offsets
+        cuts, hi = [], self.model.g.flat.numel()
+        for k, layer in enumerate(self._g_w_layer):
+            if layer in names:
+                lo = offs[layer + "/w"][0]
+                cuts.append((k, lo, hi))
+                hi = lo
+        cuts.append((len(self._g_w_layer), 0, hi))
+        return cuts
+
+    def _w_mark(self, prog, progw, begin: int, layer: str) -> None:
+        """progW[begin:] (`layer`'s weight gradient) needs progA up to its current end."""
         if progw.size() > begin:
             self._g_w.append((prog.size(), progw.size()))
+            self._g_w_layer.append(layer)
 
     def _act_bwd_dbias(self, prog, name, dy, y, dx, rows, C, act, db, chain):
         """dx = dy * act'(y) and the bias gradient db = column sums of dx: one fused launch
@@ -813,7 +842,7 @@ class HipEngine:
             w0 = progw.size()
             progw.nwgrad(Lg.name + ".nwgrad", _p(self.img_g), B, Lg.out_hw, Lg.out_hw, Lg.cout, _p(a_prev), Lg.in_hw,
                          Lg.in_hw, padL, _p(gG[Lg.name + "/w"]), 0)
-            self._w_mark(prog, progw, w0)
+            self._w_mark(prog, progw, w0, Lg.name)
             prog.nconv(Lg.name + ".dgrad", _p(self.img_g), _p(wL), 0, _p(da_prev), B, Lg.out_hw, Lg.out_hw, Lg.cout,
                        Lg.in_hw, Lg.in_hw, padL, padL, NONE, 0.0, grid, _p(x_prev), _p(a_prev), _p(st["mean"]),
                        _p(st["rstd"]), RELU, cfg.lrelu_leak, _p(part), 0)
@@ -824,7 +853,7 @@ class HipEngine:
             w0 = progw.size()
             self._wgrad(progw, Lg.name, 2, self.g_last_col, 1, 1, self.kp_g, a_prev, B * Lg.in_hw ** 2, 1, 1, Lg.cin,
                         0, gG[Lg.name + "/w"])
-            self._w_mark(prog, progw, w0)
+            self._w_mark(prog, progw, w0, Lg.name)
             r = self._dgrad_bnb(prog, 2, B, 1, 1, self.kp_g, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev, x_prev,
                                 a_prev, 1, RELU)
             fused_next = None
@@ -837,7 +866,7 @@ class HipEngine:
             w0 = progw.size()
             self._wgrad(progw, Lg.name, 0, self.img_g, Lg.out_hw, Lg.out_hw, Lg.cout, a_prev, B, Lg.in_hw, Lg.in_hw,
                         Lg.cin, padL, gG[Lg.name + "/w"])
-            self._w_mark(prog, progw, w0)
+            self._w_mark(prog, progw, w0, Lg.name)
             r = self._dgrad_bnb(prog, 0, B, Lg.out_hw, Lg.out_hw, Lg.cout, Lg.in_hw, Lg.in_hw, Lg.cin, True, bn_prev,
                                 x_prev, a_prev, 1, RELU)
             fused_next = None
@@ -860,7 +889,7 @@ class HipEngine:
             w0 = progw.size()
             self._wgrad(progw, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
                         gG[L.name + "/w"])
-            self._w_mark(prog, progw, w0)
+            self._w_mark(prog, progw, w0, L.name)
             r = self._dgrad_bnb(prog, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc,
                                 src, 1, RELU)
             fused_next = None
@@ -936,16 +965,23 @@ class HipEngine:
 
     def _schedule(self) -> str:
         req = self._sched_req
-        if self.ddp or self._timing:  # collectives / phase timers need the segmented step
+        if self._timing:  # phase timers need the segmented step
             return req if req in ("concurrent", "serial") else "concurrent"
+        if self.ddp:
+            if req in ("ddp", "concurrent", "serial"):
+                return req
+            return os.environ.get("DCGAN_DDP_SCHEDULE") or ("concurrent" if D.backend() == "gloo" else "ddp")
         return req or "fused"
+
+    def _one_graph(self) -> bool:
+        return self._schedule() in ("fused", "ddp")
 
     def _segments(self):
         """The step as a list of (name, [(program, begin, end)], stream) segments."""
         sch = self._schedule()
         A, B, C, W = self.progA, self.progB, self.progC, self.progW
         M = self.MAIN
-        if sch == "fused":
+        if sch in ("fused", "ddp"):
             return [("step", [(A, 0, -1), (B, 0, -1), (W, 0, -1), (C, 0, -1)], M)]
         if sch == "serial":
             return [("fwd+G_bwd", [(A, 0, -1), (W, 0, -1)], M), ("D_bwd_top", [(B, 0, self._b_split)], M),
@@ -1016,6 +1052,48 @@ class HipEngine:
         ex.wait(cs, ex.alt[0])
         ex.run(self.progC, [cs, ex.side])
 
+    def _run_ddp(self, ex, cs):
+        """The "ddp" schedule: the fused step with the gradient all-reduces on the comm stream,
+        issued from inside the step (and captured with it into ONE hipGraph under RCCL).
+        Comm-stream order = issue order: D's top layer + head (final after progB[:_b_split]),
+        the rest of D's (the D chain ends first), G's buckets as G's weight gradients land
+        (``_g_cuts``), G's last bucket once both chains have joined. Adam(D) waits for D's
+        collectives only and runs under G's last one; Adam(G) + the step counter follow it."""
+        alt = ex.alt[0]
+        ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
+        ex.wait(alt, cs)
+        ex.run(self.progB, ex.alt, 0, self._b_split)
+        self._ar_launch(ex, "dtop", alt)
+        ex.run(self.progB, ex.alt, self._b_split, -1)
+        self._ar_launch(ex, "drest", alt)
+        d_done = ex.mark(ex.comm) if self.ddp else None
+        cuts = {k: r for (k, _, _), r in zip(self._g_cuts[:-1], self._ar_gparts[:-1])}
+        gw = self._g_wgrad_on_d_stream()
+        pos, marks = self._a_fwd, []
+        for a_end, _ in self._g_w:
+            ex.run(self.progA, [cs, ex.side], pos, a_end)
+            marks.append(ex.mark(cs))
+            pos = a_end
+        ex.run(self.progA, [cs, ex.side], pos, -1)
+        wst = alt if gw else cs  # G weight gradients behind the D chain (64x64) or on cs
+        w = 0
+        for k, (m, (_, w_end)) in enumerate(zip(marks, self._g_w)):
+            if gw:
+                ex.wait_mark(alt, m)
+            ex.run(self.progW, ex.alt if gw else [cs, ex.side], w, w_end)
+            w = w_end
+            if k in cuts and self.ddp:
+                ex.wait(ex.comm, wst)
+                ex.collective(cuts[k], ex.comm)
+        ex.wait(cs, alt)
+        if self.ddp:
+            ex.wait(ex.comm, cs)
+            ex.collective(self._ar_gparts[-1], ex.comm)
+            ex.wait_mark(cs, d_done)
+        ex.run(self.progC, [cs, ex.side], 0, self._c_split)   # Adam(D) under G's last bucket
+        self._ar_join(ex, cs)
+        ex.run(self.progC, [cs, ex.side], self._c_split, -1)  # Adam(G), beta powers, step
+
     def _seg(self, ex, i, stream):
         """Run segment i on `stream` (graph replay, or eager replay of its program ranges)."""
         if self.graph_enabled:
@@ -1043,11 +1121,13 @@ class HipEngine:
     def _run_step(self, ex):
         cs = ex.main()
         sch = self._schedule()
-        if sch == "fused":
+        if sch in ("fused", "ddp"):
             if self.graph_enabled:
                 self._seg(ex, 0, cs)
-            else:
+            elif sch == "fused":
                 self._run_fused(ex, cs)
+            else:
+                self._run_ddp(ex, cs)
             return
         if sch == "concurrent":
             alt = ex.alt[0]
@@ -1102,17 +1182,24 @@ class HipEngine:
             self._ar_g = D.GradAllReducer(self.grad_g.flat, mb, wd, stream=cs, force=True)
             self._ar_dtop = D.GradAllReducer(self.grad_d.flat[o:], mb, wd, stream=cs, force=True)
             self._ar_drest = D.GradAllReducer(self.grad_d.flat[:o], mb, wd, stream=cs, force=True)
+            # "ddp": G's gradient in per-layer buckets (see _g_bucket_cuts)
+            self._ar_gparts = [D.GradAllReducer(self.grad_g.flat[lo:hi], mb, wd, stream=cs, force=True)
+                               for _, lo, hi in self._g_cuts]
 
     def _capture(self):
-        """Capture each step segment into its own hipGraph (collectives stay outside, issued
-        between replays on the comm stream). Capturing does not execute anything; it is
+        """Capture the step: "fused" and "ddp" as ONE hipGraph ("ddp" with its RCCL collectives
+        inside), the segmented schedules one graph per segment (their collectives stay outside,
+        issued between replays on the comm stream). Capturing does not execute anything; it is
         attempted only after one eager step has loaded every code object, and any failure
         falls back to eager replay of the recorded programs."""
         ex = self._get_exec()
+        sch = self._schedule()
+        if sch == "ddp" and self.ddp and D.is_initialized() and D.backend() != "nccl":
+            return False  # host-synchronous collectives (gloo) cannot be captured
         try:
             torch.cuda.synchronize(self.device)
             graphs = []
-            fused = self._schedule() == "fused"
+            one = self._one_graph()
             for name, parts, which in self._segments():
                 if all((p.size() if e < 0 else e) <= b for p, b, e in parts):
                     graphs.append(None)  # empty segment (fp16: no separate G update)
@@ -1120,8 +1207,12 @@ class HipEngine:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     cs = torch.cuda.current_stream(self.device)
-                    if fused:
+                    if one and self.ddp:
+                        ex.wait(ex.comm, cs)  # the comm stream joins the capture from its start
+                    if sch == "fused":
                         self._run_fused(ex, cs)
+                    elif sch == "ddp":
+                        self._run_ddp(ex, cs)
                     else:
                         sec = ex.side if which == self.MAIN else ex.alt[1]
                         for prog, b, e in parts:

@@ -40,6 +40,11 @@ def rank() -> int:
     return dist.get_rank() if is_initialized() else 0
 
 
+def backend() -> Optional[str]:
+    """The default process group's backend ("nccl" = RCCL, "gloo"), None without one."""
+    return dist.get_backend() if is_initialized() else None
+
+
 def ddp_forced() -> bool:
     """DCGAN_FORCE_DDP=1: run the data-parallel path (process group, collectives on the comm
     stream, segmented step) even for a single process -- a one-rank RCCL group exercises the

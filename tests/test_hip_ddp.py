@@ -47,6 +47,8 @@ def _run(eng):
 def _worker(rank, world, port, graph, out_dir, schedule="concurrent"):
     if schedule == "serial":
         os.environ["DCGAN_SERIAL_DBWD"] = "1"
+    if schedule == "ddp":
+        os.environ["DCGAN_DDP_SCHEDULE"] = "ddp"  # eager under gloo (its collectives cannot be captured)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["DCGAN_DIST_BACKEND"] = "gloo"
@@ -61,10 +63,12 @@ def _worker(rank, world, port, graph, out_dir, schedule="concurrent"):
     D.shutdown()
 
 
-@pytest.mark.parametrize("graph,schedule", [(False, "concurrent"), (True, "concurrent"), (True, "serial")])
+@pytest.mark.parametrize("graph,schedule", [(False, "concurrent"), (True, "concurrent"), (True, "serial"),
+                                            (False, "ddp")])
 def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
-    """Both DDP schedules: "concurrent" (D chain and G chain on separate streams, 6 graph
-    segments, collectives issued from both chains) and "serial" (DCGAN_SERIAL_DBWD=1)."""
+    """The DDP schedules over two ranks: "concurrent" (D chain and G chain on separate streams,
+    6 graph segments, collectives issued from both chains), "serial" (DCGAN_SERIAL_DBWD=1) and
+    "ddp" (the one-graph RCCL schedule with per-layer G buckets, run eagerly under gloo)."""
     ctx = mp.get_context("spawn")
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, str(tmp_path), schedule)) for r in range(2)]
@@ -75,7 +79,7 @@ def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
         assert p.exitcode == 0, "rank exited with %s" % p.exitcode
     r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
-    assert r0["graph"] == graph
+    assert r0["graph"] == (graph and schedule != "ddp")
     assert torch.equal(r0["d"], r1["d"]) and torch.equal(r0["g"], r1["g"])
     assert r0["step"] == STEPS
     eng = _make(1, 0, graph)
@@ -121,36 +125,40 @@ def test_bench_two_ranks_json_contract(tmp_path):
     assert res["value"] > 0 and res["higher_is_better"] is True and res["scaling"] == "weak"
 
 
-def _rccl_worker(out_dir, graph, port):
+def _rccl_worker(out_dir, graph, port, schedule):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["DCGAN_FORCE_DDP"] = "1"
+    os.environ["DCGAN_DDP_SCHEDULE"] = schedule
     os.environ.pop("DCGAN_DIST_BACKEND", None)
     torch.cuda.set_device(0)
     from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
     import torch.distributed as tdist
     D.init_distributed(1, 0, torch.device("cuda", 0))
     eng = _make(1, 0, graph)
-    assert eng.ddp and eng._schedule() == "concurrent"
+    assert eng.ddp and eng._schedule() == schedule
     d, g, step = _run(eng)
     torch.save({"d": d, "g": g, "step": step, "backend": tdist.get_backend(), "world": tdist.get_world_size(),
-                "graph": eng.graph_enabled}, os.path.join(out_dir, "rccl.pt"))
+                "graph": eng.graph_enabled, "graphs": len(eng._graphs)}, os.path.join(out_dir, "rccl.pt"))
     D.barrier()
     D.shutdown()
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph):
+@pytest.mark.parametrize("graph,schedule", [(False, "ddp"), (True, "ddp"), (True, "concurrent")])
+def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule):
     """The REAL collective path on a one-GPU box: a one-rank RCCL (backend "nccl") process group
-    (DCGAN_FORCE_DDP=1), the segmented concurrent schedule with the gradient all-reduces issued
-    on the comm stream between graph segments -- bit-identical to the fused single-graph step."""
+    (DCGAN_FORCE_DDP=1). "ddp": the RCCL all-reduces captured INSIDE the step's single hipGraph
+    (per-layer G buckets); "concurrent": issued on the comm stream between 6 graph segments.
+    Both bit-identical to the fused single-graph step."""
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port()))
+    p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port(), schedule))
     p.start()
     p.join(timeout=600)
     assert p.exitcode == 0, "RCCL rank exited with %s" % p.exitcode
     r = torch.load(tmp_path / "rccl.pt", weights_only=True)
     assert r["backend"] == "nccl" and r["world"] == 1 and r["step"] == STEPS and r["graph"] == graph
+    if graph:
+        assert r["graphs"] == (1 if schedule == "ddp" else 6)
     eng = _make(1, 0, True)
     assert not eng.ddp and eng._schedule() == "fused"
     d, g, _ = _run(eng)
@@ -172,4 +180,5 @@ def test_bench_force_ddp_reports_rccl():
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
+    assert res["config"]["schedule"] == "ddp" and res["config"]["graphs_per_step"] == 1
     assert res["n_gpus"] == 1 and res["value"] > 0

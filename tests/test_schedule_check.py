@@ -7,14 +7,15 @@ import torch
 from distributed_tensorflow_for_dcgan_amd.engine import schedule_check as SC
 from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
 
-CASES = [(1, None, False), (1, None, True), (1, "serial", False), (2, None, False), (2, "serial", False)]
+CASES = [(1, None, False), (1, None, True), (1, "serial", False), (2, None, False), (2, "concurrent", False),
+         (2, "serial", False)]
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("world,schedule,timing", CASES)
 def test_schedule_has_no_stream_hazards(dtype, world, schedule, timing):
     sched, hz, n = SC.check(DCGANConfig(), 4, dtype, world, schedule, timing)
-    expect = schedule or ("fused" if world == 1 and not timing else "concurrent")
+    expect = schedule or ("concurrent" if timing else "fused" if world == 1 else "ddp")
     assert sched == expect
     assert n > 100
     assert hz == [], "\n".join(map(str, hz[:10]))
@@ -96,3 +97,26 @@ def test_op_accesses_are_recorded():
     launches = sum(p.op_info(i)[2] == eng.ext.OP_LAUNCH for p in (eng.progA, eng.progB, eng.progW, eng.progC)
                    for i in range(p.size()))
     assert eng.kernel_count() == launches
+
+
+def test_checker_finds_an_early_g_bucket():
+    """One-graph DDP: issuing G's first bucket one weight-gradient piece too early (before the
+    piece that finalises it) is a race between the collective and that wgrad."""
+    eng = _dry(world=2)
+    assert eng._schedule() == "ddp"
+    hz, _ = SC.check_engine(eng)
+    assert hz == []
+    k, lo, hi = eng._g_cuts[0]
+    assert k >= 1
+    eng._g_cuts[0] = (k - 1, lo, hi)
+    hz, _ = SC.check_engine(eng)
+    assert any("allreduce" in h.a or "allreduce" in h.b for h in hz), hz
+
+
+def test_ddp_g_buckets_tile_the_gradient():
+    eng = _dry(world=2)
+    cuts = eng._g_cuts
+    assert len(cuts) == 3 and cuts[-1][1] == 0
+    assert cuts[0][2] == eng.grad_g.flat.numel()
+    for (_, lo, _), (_, _, hi) in zip(cuts, cuts[1:]):
+        assert lo == hi
