@@ -23,16 +23,17 @@ Schedules (``_schedule``), all covered by the stream-hazard checker
 (``engine/schedule_check.py``) and by GPU bit-exactness tests:
   "fused"       single process: ONE hipGraph; the two backward chains on two streams; ONE
                 Adam launch for both models after the join (16-bit dtypes)
-  "ddp"         DDP over RCCL (default): the fused schedule with the gradient all-reduces on a
-                comm stream INSIDE the same single hipGraph (RCCL collectives are captured) --
-                D's top layer + head as soon as the D chain has produced it, the rest of D's when
-                that chain ends, then G's gradients in per-layer buckets as G's weight gradients
-                land (``_g_cuts``); Adam(D) runs under G's last collective, Adam(G) after it
-  "concurrent"  DDP over gloo (host-synchronous collectives cannot be captured) and the
-                per-phase timed step: the two chains cut into 6 graph segments, the collectives
-                issued between them from the host -- D's top layer + head (76 % of D's gradient
-                bytes at 64x64) as soon as the D chain has produced it, G's gradients when the G
-                chain ends, the rest of D's when the D chain ends
+  "concurrent"  DDP (default) and the per-phase timed step: the two chains cut into 6 graph
+                segments, the collectives issued between them from the host on a comm stream --
+                D's top layer + head (76 % of D's gradient bytes at 64x64) as soon as the D chain
+                has produced it, the rest of D's when the D chain ends, G's gradients when the G
+                chain ends; Adam(D) runs under G's all-reduce
+  "ddp"         DCGAN_DDP_SCHEDULE=ddp (RCCL): the fused schedule with the gradient all-reduces on
+                the comm stream INSIDE the same single hipGraph (RCCL collectives are captured);
+                G's gradients go out in per-layer buckets as G's weight gradients land
+                (``_g_cuts``). W=1 overhead vs "fused" is ~1.5 % (vs ~7 % segmented), but ROCm's
+                graph executor does not overlap the collectives with the compute branches, so
+                with real communication the segmented step is faster (ab_ddp_one_graph_r3.txt)
   "serial"      ``schedule="serial"`` / DCGAN_SERIAL_DBWD=1: fwd + G chain, then the D chain, as
                 5 segments (the G all-reduce overlaps D's backward)
 
@@ -961,6 +962,9 @@ class HipEngine:
     def _g_wgrad_on_d_stream(self) -> bool:
         if self.G_WGRAD_ON_D_STREAM is not None:
             return bool(self.G_WGRAD_ON_D_STREAM)
+        env = os.environ.get("DCGAN_G_WGRAD_ON_D")
+        if env in ("0", "1"):
+            return env == "1"
         return self.cfg.output_size <= 64
 
     def _schedule(self) -> str:
@@ -970,7 +974,10 @@ class HipEngine:
         if self.ddp:
             if req in ("ddp", "concurrent", "serial"):
                 return req
-            return os.environ.get("DCGAN_DDP_SCHEDULE") or ("concurrent" if D.backend() == "gloo" else "ddp")
+            # "concurrent" by default: inside ONE hipGraph the collectives do not overlap the
+            # compute branches on ROCm (emulated ring collectives, 64x64: 1.39 ms vs 1.33 for
+            # the segmented step; profiles/r3/ab_ddp_one_graph_r3.txt)
+            return os.environ.get("DCGAN_DDP_SCHEDULE") or "concurrent"
         return req or "fused"
 
     def _one_graph(self) -> bool:

@@ -192,7 +192,7 @@ def main(argv=None) -> int:
     bad = 0
     for dtype in ("bf16", "fp16", "fp32"):
         for world, sched, timing in ((1, None, False), (1, None, True), (1, "serial", False), (2, None, False),
-                                     (2, "concurrent", False), (2, "serial", False)):
+                                     (2, "ddp", False), (2, "serial", False)):
             s, hz, n = check(cfg, args.batch_size, dtype, world, sched, timing)
             print("%-5s W=%d %-10s timing=%d ops=%4d hazards=%d" % (dtype, world, s, timing, n, len(hz)))
             for h in hz[:10]:

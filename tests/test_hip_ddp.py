@@ -48,7 +48,7 @@ def _worker(rank, world, port, graph, out_dir, schedule="concurrent"):
     if schedule == "serial":
         os.environ["DCGAN_SERIAL_DBWD"] = "1"
     if schedule == "ddp":
-        os.environ["DCGAN_DDP_SCHEDULE"] = "ddp"  # eager under gloo (its collectives cannot be captured)
+        os.environ["DCGAN_DDP_SCHEDULE"] = "ddp"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["DCGAN_DIST_BACKEND"] = "gloo"
@@ -180,5 +180,5 @@ def test_bench_force_ddp_reports_rccl():
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
-    assert res["config"]["schedule"] == "ddp" and res["config"]["graphs_per_step"] == 1
+    assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 6
     assert res["n_gpus"] == 1 and res["value"] > 0

@@ -7,7 +7,7 @@ import torch
 from distributed_tensorflow_for_dcgan_amd.engine import schedule_check as SC
 from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
 
-CASES = [(1, None, False), (1, None, True), (1, "serial", False), (2, None, False), (2, "concurrent", False),
+CASES = [(1, None, False), (1, None, True), (1, "serial", False), (2, None, False), (2, "ddp", False),
          (2, "serial", False)]
 
 
@@ -15,7 +15,7 @@ CASES = [(1, None, False), (1, None, True), (1, "serial", False), (2, None, Fals
 @pytest.mark.parametrize("world,schedule,timing", CASES)
 def test_schedule_has_no_stream_hazards(dtype, world, schedule, timing):
     sched, hz, n = SC.check(DCGANConfig(), 4, dtype, world, schedule, timing)
-    expect = schedule or ("concurrent" if timing else "fused" if world == 1 else "ddp")
+    expect = schedule or ("fused" if world == 1 and not timing else "concurrent")
     assert sched == expect
     assert n > 100
     assert hz == [], "\n".join(map(str, hz[:10]))
@@ -24,14 +24,14 @@ def test_schedule_has_no_stream_hazards(dtype, world, schedule, timing):
 @pytest.mark.parametrize("size", [28, 128])
 def test_other_resolutions_have_no_stream_hazards(size):
     c = 1 if size == 28 else 3
-    for world, schedule, timing in ((1, None, False), (2, None, False)):
+    for world, schedule, timing in ((1, None, False), (2, None, False), (2, "ddp", False)):
         _, hz, _ = SC.check(DCGANConfig(output_size=size, c_dim=c), 2, "bf16", world, schedule, timing)
         assert hz == [], "\n".join(map(str, hz[:10]))
 
 
-def _dry(world=1, timing=False):
+def _dry(world=1, timing=False, schedule=None):
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
-    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=world, dry_run=True, graph=False)
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=world, dry_run=True, graph=False, schedule=schedule)
     if timing:
         eng._timing = True
         eng._build_updates()
@@ -102,7 +102,7 @@ def test_op_accesses_are_recorded():
 def test_checker_finds_an_early_g_bucket():
     """One-graph DDP: issuing G's first bucket one weight-gradient piece too early (before the
     piece that finalises it) is a race between the collective and that wgrad."""
-    eng = _dry(world=2)
+    eng = _dry(world=2, schedule="ddp")
     assert eng._schedule() == "ddp"
     hz, _ = SC.check_engine(eng)
     assert hz == []
@@ -114,7 +114,7 @@ def test_checker_finds_an_early_g_bucket():
 
 
 def test_ddp_g_buckets_tile_the_gradient():
-    eng = _dry(world=2)
+    eng = _dry(world=2, schedule="ddp")
     cuts = eng._g_cuts
     assert len(cuts) == 3 and cuts[-1][1] == 0
     assert cuts[0][2] == eng.grad_g.flat.numel()
