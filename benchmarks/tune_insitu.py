@@ -9,7 +9,10 @@ rebuild the engine, time ``--steps`` graph-replayed steps, keep a change only if
 incumbent by more than ``--min_gain``. One process, every candidate on the same GPU.
 
 ``python -m benchmarks.tune_insitu [--steps 150] [--passes 1] [--write]`` -- ``--write`` stores the
-result in ops/igemm_tuned.json (the table the engine reads).
+result in ops/igemm_tuned.json (the table the engine reads). Other image sizes / dtypes
+(``--output_size 128``, ``--output_size 256 --batch 512 --dtype fp16``): the layers with no table
+entry yet start from the heuristic's choice (``--seed``), so every GEMM of that step is tuned.
+``--ig4`` also tries the igemm4.hip tiles (halo window + loader waves) on conv / deconv layers.
 """
 import argparse
 import gc
@@ -24,9 +27,9 @@ from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
 from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
 
 
-def step_ms(cfg, B, steps, warmup):
+def step_ms(cfg, B, steps, warmup, dtype="bf16"):
     dev = torch.device("cuda", 0)
-    eng = HipEngine(cfg, B, dev, seed=0)
+    eng = HipEngine(cfg, B, dev, seed=0, dtype=dtype)
     real = torch.rand(B, cfg.output_size, cfg.output_size, cfg.c_dim, device=dev) * 2 - 1
     eng.set_synthetic_batch(real)
     for _ in range(warmup):
@@ -43,38 +46,51 @@ def step_ms(cfg, B, steps, warmup):
     return ms
 
 
-def used_keys(cfg, B):
-    """Tuned-table keys the engine consults while building the step."""
+def used_keys(cfg, B, dtype="bf16", seed=False):
+    """Tuned-table keys the engine consults while building the step. seed=True: keys with no
+    entry get the heuristic's (cfg, splits) as their entry (igemm3 / wgrad3 choices only)."""
     seen = []
+    picked = {}
     orig_i, orig_w = H.igemm_cfg_for, H.wgrad3_cfg_for
 
     def log_i(mode, Bn, Hin, Win, Kc, Hout, Wout, N, *a, **k):
         key = "%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N)
+        r = orig_i(mode, Bn, Hin, Win, Kc, Hout, Wout, N, *a, **k)
         if key not in seen:
             seen.append(key)
-        return orig_i(mode, Bn, Hin, Win, Kc, Hout, Wout, N, *a, **k)
+            picked[key] = r
+        return r
 
     def log_w(Mc, Nc, Bn, Hd, Wd, Hg):
         key = H.wgrad3_key(Mc, Nc, Bn, Hd, Wd, Hg)
+        r = orig_w(Mc, Nc, Bn, Hd, Wd, Hg)
         if key not in seen:
             seen.append(key)
-        return orig_w(Mc, Nc, Bn, Hd, Wd, Hg)
+            picked[key] = r
+        return r
 
     H.igemm_cfg_for, H.wgrad3_cfg_for = log_i, log_w
     import distributed_tensorflow_for_dcgan_amd.engine.hip_engine as E
     E.H.igemm_cfg_for, E.H.wgrad3_cfg_for = log_i, log_w
     try:
-        eng = HipEngine(cfg, B, torch.device("cuda", 0), seed=0, graph=False)
+        eng = HipEngine(cfg, B, torch.device("cuda", 0), seed=0, graph=False, dtype=dtype)
         del eng
     finally:
         H.igemm_cfg_for, H.wgrad3_cfg_for = orig_i, orig_w
         E.H.igemm_cfg_for, E.H.wgrad3_cfg_for = orig_i, orig_w
     gc.collect()
     torch.cuda.empty_cache()
-    return [k for k in seen if k in H.tuned_table()]
+    table = H.tuned_table()
+    if seed:
+        for k in seen:
+            r = picked.get(k)
+            if k not in table and r is not None and r[0] >= 200:
+                table[k] = (int(r[0]), int(r[1]))
+                print("  seed %-28s %d:%d (heuristic)" % (k, r[0], r[1]), flush=True)
+    return [k for k in seen if k in table]
 
 
-def neighbours(key, cur, tiles=False):
+def neighbours(key, cur, tiles=False, ig4=False):
     cfg, sp = cur
     out = []
     for s2 in (sp // 2, sp * 2, sp + 1, sp - 1):
@@ -95,6 +111,8 @@ def neighbours(key, cur, tiles=False):
         for t2 in (range(9) if tiles else ()):
             if t2 != tile:
                 out.append((200 + 10 * ns + t2, sp))
+        if ig4 and not key.startswith("2,"):  # igemm4: no split-K, conv / deconv layers only
+            out += [(c, 1) for c in (500, 501, 503, 506, 507, 510, 511, 515, 516, 517)]
     seen, res = set(), []
     for c in out:
         if c not in seen and c != cur:
@@ -112,25 +130,30 @@ def main():
     ap.add_argument("--min_gain", type=float, default=0.003, help="relative step-time gain to accept a change")
     ap.add_argument("--only", default="", help="comma-separated key prefixes")
     ap.add_argument("--tiles", action="store_true", help="also try sibling tiles (slower)")
+    ap.add_argument("--ig4", action="store_true", help="also try igemm4 tiles")
+    ap.add_argument("--seed", action="store_true", help="tune layers with no table entry from the heuristic")
+    ap.add_argument("--output_size", type=int, default=64)
+    ap.add_argument("--c_dim", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--out", default="", help="also write the resulting table (JSON) here")
     a = ap.parse_args()
-    cfg = DCGANConfig()
+    cfg = DCGANConfig(output_size=a.output_size, c_dim=a.c_dim)
     table = H.tuned_table()
-    keys = used_keys(cfg, a.batch)
+    keys = used_keys(cfg, a.batch, a.dtype, a.seed)
     if a.only:
         keys = [k for k in keys if any(k.startswith(p) for p in a.only.split(","))]
     print("keys in the step: %d" % len(keys), flush=True)
-    best = step_ms(cfg, a.batch, a.steps, a.warmup)
+    best = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)
     print("incumbent %.4f ms" % best, flush=True)
     log = []
     for ps in range(a.passes):
         for key in keys:
             cur = table[key]
-            for cand in neighbours(key, cur, a.tiles):
+            for cand in neighbours(key, cur, a.tiles, a.ig4):
                 table[key] = cand
                 try:
-                    ms = step_ms(cfg, a.batch, a.steps, a.warmup)
+                    ms = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)
                 except Exception as e:  # illegal combination for this layer: skip
                     print("  %s %d:%d failed: %s" % (key, cand[0], cand[1], str(e)[:80]), flush=True)
                     table[key] = cur
@@ -146,7 +169,7 @@ def main():
                     table[key] = cur
             table[key] = cur
         # re-measure the incumbent (noise guard for the next pass)
-        best = step_ms(cfg, a.batch, a.steps, a.warmup)
+        best = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)
         print("pass %d done: %.4f ms" % (ps + 1, best), flush=True)
     out = {k: "%d:%d" % v for k, v in sorted(table.items())}
     if a.out:

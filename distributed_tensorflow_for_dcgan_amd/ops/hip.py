@@ -179,11 +179,13 @@ def pick_igemm_cfg(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
 def pick_igemm3(M: int, N: int, Kc: int, taps: int, phases: int = 1, rows_per_group: Optional[int] = None,
                 target_blocks: int = 2 * CU_COUNT) -> Optional[Tuple[int, int]]:
     """(cfg, splits) heuristic for igemm3: the largest 64x64-per-wave tile that fits N, then
-    split-K until ~target_blocks workgroups (each split keeps >= 4 K tiles)."""
+    split-K until ~target_blocks workgroups (each split keeps >= 4 K tiles). Two LDS stages
+    (21x): every layer of the in-situ tuned 128x128 step moved from 3 stages to 2
+    (profiles/r3/tune_insitu_128_r3.txt), as most 64x64 entries had."""
     if N >= 128:
-        order = [200, 201, 203, 205]
+        order = [210, 211, 213, 215]
     elif N >= 64:
-        order = [201, 203, 205]
+        order = [211, 213, 215]
     else:
         return None
     kt = taps * -(-Kc // 64)
