@@ -101,6 +101,8 @@ def neighbours(key, cur, tiles=False, ig4=False):
         fam = [300, 301, 302, 303, 310, 311, 312, 313] + ([320, 322, 330, 332] if Mc == 64 else [])
         if not tiles:
             fam = {310: (311, 313), 311: (310, 313), 313: (311, 312), 312: (313, 311)}.get(cfg, ())
+            if 300 <= cfg < 320:  # the same tile with the other LDS stage count (NS 3 <-> 2)
+                fam = tuple(fam) + (cfg + 10 if cfg < 310 else cfg - 10,)
         out += [(c, sp) for c in fam]
     elif cfg >= 200:
         ns = (cfg - 200) // 10

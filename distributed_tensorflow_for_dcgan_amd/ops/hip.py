@@ -307,7 +307,7 @@ def pick_wgrad3(Mc: int, Nc: int, K: int, target_blocks: int = 2 * CU_COUNT) -> 
         sp = 1
         while tiles * sp < target_blocks and kt // (2 * sp) >= 8 and sp < 16:
             sp *= 2
-        return 300 + tid, sp
+        return 310 + tid, sp  # two LDS stages (31x), as every tuned 64x64 entry
     return None
 
 
