@@ -302,11 +302,9 @@ class HipEngine:
         second part."""
         self.progC = self._prog()
         sch = self._schedule()
-        if sch == "fused" and self.dt == 0 and not self._adam_d_early():
+        if sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
             self._c_split = self.progC.size()
-        elif sch == "fused" and self.dt == 0:  # Adam(D) beside G's weight gradients, then Adam(G)
-            self._build_update_d_first(self.progC)
         elif sch in ("concurrent", "ddp") and not self.f16:
             self._build_update_d_first(self.progC)
         else:
@@ -969,17 +967,6 @@ class HipEngine:
             return env == "1"
         return self.cfg.output_size <= 64
 
-    def _adam_d_early(self) -> bool:
-        """Fused bf16 step, G weight gradients behind the D chain: Adam(D) on the main stream as
-        soon as the G data-gradient chain and the D chain are done, beside G's weight gradients;
-        Adam(G) + the step counter after the join. DCGAN_ADAM_D_EARLY=0/1 overrides."""
-        if self.ddp or self.dt != 0 or not self._g_wgrad_on_d_stream():
-            return False
-        env = os.environ.get("DCGAN_ADAM_D_EARLY")
-        if env in ("0", "1"):
-            return env == "1"
-        return False
-
     def _schedule(self) -> str:
         req = self._sched_req
         if self._timing:  # phase timers need the segmented step
@@ -1058,7 +1045,6 @@ class HipEngine:
             ex.wait(cs, ex.alt[0])
             ex.run(self.progC, [cs, ex.side])
             return
-        d_end = ex.mark(ex.alt[0])  # the D chain's end (before the G weight gradients queue there)
         pos, marks = self._a_fwd, []
         for a_end, _ in self._g_w:
             ex.run(self.progA, [cs, ex.side], pos, a_end)
@@ -1070,12 +1056,6 @@ class HipEngine:
             ex.wait_mark(ex.alt[0], m)
             ex.run(self.progW, ex.alt, w, w_end)
             w = w_end
-        if self._adam_d_early():
-            ex.wait_mark(cs, d_end)
-            ex.run(self.progC, [cs, ex.side], 0, self._c_split)   # Adam(D) beside G's wgrads
-            ex.wait(cs, ex.alt[0])
-            ex.run(self.progC, [cs, ex.side], self._c_split, -1)  # Adam(G), powers, step
-            return
         ex.wait(cs, ex.alt[0])
         ex.run(self.progC, [cs, ex.side])
 
