@@ -131,6 +131,7 @@ def main():
     ap.add_argument("--passes", type=int, default=1)
     ap.add_argument("--min_gain", type=float, default=0.003, help="relative step-time gain to accept a change")
     ap.add_argument("--only", default="", help="comma-separated key prefixes")
+    ap.add_argument("--keys", default="", help="'|'-separated full table keys")
     ap.add_argument("--tiles", action="store_true", help="also try sibling tiles (slower)")
     ap.add_argument("--ig4", action="store_true", help="also try igemm4 tiles")
     ap.add_argument("--seed", action="store_true", help="tune layers with no table entry from the heuristic")
@@ -145,6 +146,8 @@ def main():
     keys = used_keys(cfg, a.batch, a.dtype, a.seed)
     if a.only:
         keys = [k for k in keys if any(k.startswith(p) for p in a.only.split(","))]
+    if a.keys:
+        keys = [k for k in keys if k in a.keys.split("|")]
     print("keys in the step: %d" % len(keys), flush=True)
     best = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)
     print("incumbent %.4f ms" % best, flush=True)
