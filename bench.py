@@ -127,7 +127,7 @@ def main():
                        "seq_len": None, "parallelism": "dp%d" % args.gpus, "engine": eng.name,
                        "hip_graph": bool(getattr(eng, "graph_enabled", False)),
                        "schedule": eng._schedule() if hasattr(eng, "_schedule") else None,
-                       "graphs_per_step": len(getattr(eng, "_graphs", [])) or None,
+                       "graphs_per_step": sum(g is not None for g in getattr(eng, "_graphs", [])) or None,
                        "backend": backend, "world_size": world_seen, "devices": devices,
                        "kernels_per_step": eng.kernel_count() if hasattr(eng, "kernel_count") else None,
                        "gflop_per_image": round(cfg.flops_per_image() / 1e9, 4),
