@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--batch_size", type=int, default=128)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--schedule", default="concurrent", choices=["concurrent", "ddp"])
+    ap.add_argument("--schedule", default="concurrent", choices=["concurrent", "serial", "ddp"])
     ap.add_argument("--fake_comm_us", default="", help="concurrent: G,Dtop,Drest all-reduce latencies (us)")
     ap.add_argument("--fake_busbw_gbs", type=float, default=0.0,
                     help="emulate every bucket with the ring model at this bus bandwidth (GB/s)")
@@ -61,10 +61,10 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig()
-    ddp = a.schedule == "ddp" or bool(a.fake_comm_us) or a.fake_busbw_gbs > 0
+    ddp = a.schedule != "concurrent" or bool(a.fake_comm_us) or a.fake_busbw_gbs > 0
     eng = HipEngine(cfg, a.batch_size, dev, ddp=ddp, schedule=a.schedule if ddp else None)
-    if a.schedule == "concurrent":
-        eng.enable_timing()  # the segmented "concurrent" schedule, Adam(G) / Adam(D) apart
+    if a.schedule in ("concurrent", "serial"):
+        eng.enable_timing()  # the segmented schedules, Adam(G) / Adam(D) apart
     cpu = _cycles_per_us() if ddp else 0.0
     comm = {}
     if ddp:
