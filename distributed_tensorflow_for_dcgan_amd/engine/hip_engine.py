@@ -1190,8 +1190,8 @@ class HipEngine:
             self._ar_dtop = D.GradAllReducer(self.grad_d.flat[o:], mb, wd, stream=cs, force=True)
             self._ar_drest = D.GradAllReducer(self.grad_d.flat[:o], mb, wd, stream=cs, force=True)
             # "ddp": G's gradient in per-layer buckets (see _g_bucket_cuts)
-            self._ar_gparts = [D.GradAllReducer(self.grad_g.flat[lo:hi], mb, wd, stream=cs, force=True)
-                               for _, lo, hi in self._g_cuts]
+            self._ar_gparts = ([D.GradAllReducer(self.grad_g.flat[lo:hi], mb, wd, stream=cs, force=True)
+                                for _, lo, hi in self._g_cuts] if self._schedule() == "ddp" else [])
 
     def _capture(self):
         """Capture the step: "fused" and "ddp" as ONE hipGraph ("ddp" with its RCCL collectives
