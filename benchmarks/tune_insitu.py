@@ -90,7 +90,7 @@ def used_keys(cfg, B, dtype="bf16", seed=False):
     return [k for k in seen if k in table]
 
 
-def neighbours(key, cur, tiles=False, ig4=False):
+def neighbours(key, cur, tiles=False, ig4=False, extra_tiles=()):
     cfg, sp = cur
     out = []
     for s2 in (sp // 2, sp * 2, sp + 1, sp - 1):
@@ -111,6 +111,9 @@ def neighbours(key, cur, tiles=False, ig4=False):
             if ns2 != ns:
                 out.append((200 + 10 * ns2 + tile, sp))
         for t2 in (range(9) if tiles else ()):
+            if t2 != tile:
+                out.append((200 + 10 * ns + t2, sp))
+        for t2 in extra_tiles:  # e.g. --extra_tiles 9: the 8-wave 128x128 tile, same stages / split
             if t2 != tile:
                 out.append((200 + 10 * ns + t2, sp))
         if ig4 and not key.startswith("2,"):  # igemm4: no split-K, conv / deconv layers only
@@ -134,6 +137,7 @@ def main():
     ap.add_argument("--keys", default="", help="'|'-separated full table keys")
     ap.add_argument("--tiles", action="store_true", help="also try sibling tiles (slower)")
     ap.add_argument("--ig4", action="store_true", help="also try igemm4 tiles")
+    ap.add_argument("--extra_tiles", default="", help="comma-separated igemm3 tile ids to try on every GEMM entry")
     ap.add_argument("--seed", action="store_true", help="tune layers with no table entry from the heuristic")
     ap.add_argument("--output_size", type=int, default=64)
     ap.add_argument("--c_dim", type=int, default=3)
@@ -155,7 +159,8 @@ def main():
     for ps in range(a.passes):
         for key in keys:
             cur = table[key]
-            for cand in neighbours(key, cur, a.tiles, a.ig4):
+            extra = tuple(int(x) for x in a.extra_tiles.split(",") if x)
+            for cand in neighbours(key, cur, a.tiles, a.ig4, extra):
                 table[key] = cand
                 try:
                     ms = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)
