@@ -3,8 +3,7 @@
 
 For every conv-shaped GEMM of the DCGAN training step (D forward on 2B, D dgrads, G forward,
 G dgrads, at per-GPU batch B) time every tile configuration -- igemm.hip (both staging
-variants), igemm3.hip (every tile, 2..5 LDS stages, split-K 1..8) and igemm4.hip (halo window,
-every tile that fits) with the weight layout
+variants) and igemm3.hip (every tile, 2..5 LDS stages, split-K 1..8) with the weight layout
 the engine reads for that GEMM -- in ONE process, interleaved (guide §5.4 rule 24), and
 report TF/s. ``--write`` stores the fastest "cfg:splits" per shape in ops/igemm_tuned.json,
 which the engine's tile policy consults first.
@@ -51,7 +50,6 @@ def shapes(cfg: DCGANConfig, B: int):
 
 
 V1 = False  # --v1: also time the first-generation igemm.hip tiles
-IG4 = True  # --no-ig4: leave out igemm4.hip
 
 
 def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
@@ -69,12 +67,6 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     phases = 4 if mode == 1 else 1
     M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
     kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
-    if mode in (0, 1) and IG4:  # igemm4: halo window + loader waves (geometry checked per shape)
-        pad = same_pads(Hout)[0] if mode == 1 else same_pads(2 * Hout)[0]
-        for c in range(500, 520):
-            if c % 10 in H.IGEMM4_TILES and H.IGEMM4_TILES[c % 10][1] <= N and \
-                    H.igemm4_lds(c, mode, Bn, Kc, Hout, Wout, N, pad, pad) is not None:
-                out.append((c, 1))
     for c in range(200, 240):
         if c % 10 not in H.IGEMM3_TILES or H.igemm3_lds(c) > 160 * 1024:
             continue
@@ -108,14 +100,12 @@ def main():
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--only", default="")
     ap.add_argument("--v1", action="store_true", help="also time igemm.hip (v1) tiles")
-    ap.add_argument("--no-ig4", action="store_true", help="leave out igemm4.hip tiles")
     ap.add_argument("--out", default="", help="also write this run's table (JSON) here")
     ap.add_argument("--top", type=int, default=6, help="candidates listed per shape")
     ap.add_argument("--cfgs", default="", help="comma-separated cfg prefix filter, e.g. 4,21")
     a = ap.parse_args()
-    global V1, IG4
+    global V1
     V1 = a.v1
-    IG4 = not a.no_ig4
     cfg = DCGANConfig(output_size=a.size)
     ext = H.ext()
     dev = torch.device("cuda", 0)

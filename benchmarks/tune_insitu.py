@@ -12,7 +12,6 @@ incumbent by more than ``--min_gain``. One process, every candidate on the same 
 result in ops/igemm_tuned.json (the table the engine reads). Other image sizes / dtypes
 (``--output_size 128``, ``--output_size 256 --batch 512 --dtype fp16``): the layers with no table
 entry yet start from the heuristic's choice (``--seed``), so every GEMM of that step is tuned.
-``--ig4`` also tries the igemm4.hip tiles (halo window + loader waves) on conv / deconv layers.
 """
 import argparse
 import gc
@@ -90,7 +89,7 @@ def used_keys(cfg, B, dtype="bf16", seed=False):
     return [k for k in seen if k in table]
 
 
-def neighbours(key, cur, tiles=False, ig4=False, extra_tiles=()):
+def neighbours(key, cur, tiles=False, extra_tiles=()):
     cfg, sp = cur
     out = []
     for s2 in (sp // 2, sp * 2, sp + 1, sp - 1):
@@ -116,8 +115,6 @@ def neighbours(key, cur, tiles=False, ig4=False, extra_tiles=()):
         for t2 in extra_tiles:  # e.g. --extra_tiles 9: the 8-wave 128x128 tile, same stages / split
             if t2 != tile:
                 out.append((200 + 10 * ns + t2, sp))
-        if ig4 and not key.startswith("2,"):  # igemm4: no split-K, conv / deconv layers only
-            out += [(c, 1) for c in (500, 501, 503, 506, 507, 510, 511, 515, 516, 517)]
     seen, res = set(), []
     for c in out:
         if c not in seen and c != cur:
@@ -136,7 +133,6 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated key prefixes")
     ap.add_argument("--keys", default="", help="'|'-separated full table keys")
     ap.add_argument("--tiles", action="store_true", help="also try sibling tiles (slower)")
-    ap.add_argument("--ig4", action="store_true", help="also try igemm4 tiles")
     ap.add_argument("--extra_tiles", default="", help="comma-separated igemm3 tile ids to try on every GEMM entry")
     ap.add_argument("--seed", action="store_true", help="tune layers with no table entry from the heuristic")
     ap.add_argument("--output_size", type=int, default=64)
@@ -160,7 +156,7 @@ def main():
         for key in keys:
             cur = table[key]
             extra = tuple(int(x) for x in a.extra_tiles.split(",") if x)
-            for cand in neighbours(key, cur, a.tiles, a.ig4, extra):
+            for cand in neighbours(key, cur, a.tiles, extra):
                 table[key] = cand
                 try:
                     ms = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)

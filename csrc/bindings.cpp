@@ -32,7 +32,6 @@
 #include <vector>
 
 #include "hip/kernels.h"
-#include "hip/ig4.h"
 extern "C" {
 #include "hip/narrow2.inc"
 }
@@ -179,13 +178,6 @@ class Program {
                uintptr_t bias, int act, float leak, uintptr_t stats, int stream, int bkn, int kb_valid, int splits,
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
                int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
-    if (cfg >= 500) {
-      if (out_f32 || splits != 1 || (kb_valid >= 0 && kb_valid != Kc))
-        throw std::runtime_error("igemm4: elem_t output, no split-K");
-      return igemm4_ex(name, mode, A, Bw, C, Bn, Hin, Win, Kc, Hout, Wout, N, pad_y, pad_x, cfg, ldc, cofs, bias,
-                       act, leak, stats, stream, bkn, bnb_x, bnb_y, bnb_mean, bnb_rstd, bnb_rpg, bnb_act, bnb_leak,
-                       bnb_store_g);
-    }
     int bm = 0, bn = 0, ns = 0;
     const bool v3 = cfg >= 200;
     if (cfg >= 400) throw std::runtime_error("bad igemm cfg " + std::to_string(cfg));
@@ -325,267 +317,6 @@ class Program {
     return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); },
                acc.v);
   }
-
-  // ------------------------------------------------------------------ igemm4 (halo window, loader waves)
-  // Geometry of csrc/hip/igemm4.hip: a tile is NI whole images or TR whole rows of one image of
-  // the (phase) output grid; every tap of every phase reads its activation fragments from the
-  // tile's input window at a constant pixel offset (tap table), stride-2 windows stored
-  // column-split by parity. Returns the LDS bytes of the launch through *shm_out when non-null
-  // (igemm4_plan, for the tile policy) without recording anything.
-  // Host plan of one igemm4 launch: the kernel arguments, the LDS bytes and the per-step
-  // descriptor tables (ig4.h) the step loops read instead of walking the schedule themselves.
-  struct IG4Plan {
-    IG4Args g{};
-    size_t shm = 0;
-    int nwb = 1;
-    std::vector<IG4CDesc> cd;
-    std::vector<IG4LDesc> ld;
-  };
-  static bool igemm4_geometry(IG4Plan& plan, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x,
-                              int bm, int bn, int nsb, int wmc, bool bkn, std::string* why) {
-    IG4Args& g = plan.g;
-    auto fail = [&](const char* m) { if (why) *why = m; return false; };
-    if (mode != 0 && mode != 1) return fail("igemm4: conv (mode 0) or deconv (mode 1) only");
-    if (Kc % 64) return fail("igemm4: Kc must be a multiple of 64");
-    if (N % bn) return fail("igemm4: N must be a multiple of the tile width");
-    int Hq, Wq;
-    std::vector<int> ntap, toff, wtap, oyo, oxo;  // per phase
-    std::vector<std::vector<int>> ry, rx, wt;    // per phase per tap: input row / col relative to the grid pixel
-    if (mode == 0) {
-      Hq = Hout; Wq = Wout;
-      ry.assign(1, {}); rx.assign(1, {}); wt.assign(1, {});
-      for (int t = 0; t < 25; ++t) { ry[0].push_back(t / 5 - pad_y); rx[0].push_back(t % 5 - pad_x); wt[0].push_back(t); }
-      oyo = {0}; oxo = {0};
-    } else {
-      if (Hout % 2 || Wout % 2) return fail("igemm4: deconv needs an even output size");
-      Hq = Hout / 2; Wq = Wout / 2;
-      for (int py = 0; py < 2; ++py)
-        for (int px = 0; px < 2; ++px) {
-          const int kys = (py + pad_y) & 1, kxs = (px + pad_x) & 1;
-          const int iy0 = (py + pad_y - kys) / 2, ix0 = (px + pad_x - kxs) / 2;
-          std::vector<int> a, b, c;
-          for (int ty = 0; kys + 2 * ty < 5; ++ty)
-            for (int tx = 0; kxs + 2 * tx < 5; ++tx) {
-              a.push_back(iy0 - ty); b.push_back(ix0 - tx); c.push_back((kys + 2 * ty) * 5 + kxs + 2 * tx);
-            }
-          ry.push_back(a); rx.push_back(b); wt.push_back(c);
-          oyo.push_back(py); oxo.push_back(px);
-        }
-    }
-    const int S = mode == 0 ? 2 : 1;
-    const int HW = Hq * Wq;
-    int TR, NI;
-    if (bm <= HW) {
-      if (HW % bm || bm % Wq) return fail("igemm4: tile rows must be whole grid rows dividing the image");
-      TR = bm / Wq; NI = 1;
-    } else {
-      if (bm % HW) return fail("igemm4: tile rows must be whole images");
-      TR = Hq; NI = bm / HW;
-    }
-    if (((size_t)Bn * HW) % bm) return fail("igemm4: the tile rows must divide the batch rows");
-    int miny = 1 << 20, maxy = -(1 << 20), minx = 1 << 20, maxx = -(1 << 20);
-    for (size_t p = 0; p < ry.size(); ++p)
-      for (size_t t = 0; t < ry[p].size(); ++t) {
-        miny = std::min(miny, ry[p][t]); maxy = std::max(maxy, ry[p][t]);
-        minx = std::min(minx, rx[p][t]); maxx = std::max(maxx, rx[p][t]);
-      }
-    g.S = S; g.Hq = Hq; g.Wq = Wq; g.TR = TR; g.NI = NI;
-    g.WY = S * (TR - 1) + maxy - miny + 1;
-    g.WX = S * (Wq - 1) + maxx - minx + 1;
-    if (S == 2) { g.HX = (g.WX + 1) / 2; g.WXP = 2 * g.HX; } else { g.HX = 0; g.WXP = g.WX; }
-    g.win_oy = miny; g.win_ox = minx;
-    g.nphases = (int)ry.size();
-    // window row pitch (LDS pixels): the smallest >= the row width for which every activation
-    // fragment read (16 output pixels x one 16-byte chunk per lane, 160-byte LDS pixels, every
-    // tap) is free of ds_read_b128 bank conflicts (MI355X_MICROARCH.md LDS lane groups)
-    {
-      static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
-                                     {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
-                                     {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
-                                     {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
-      const int base_w = g.WXP;
-      int best_w = base_w, best_c = 1 << 30;
-      for (int wxp = base_w; wxp < base_w + 16; ++wxp) {
-        int worst = 0;
-        for (int m0 = 0; m0 < std::min(bm, 64 * 8); m0 += 16) {  // fragment row blocks (one per 16 rows)
-          int pix[16];
-          for (int fr = 0; fr < 16; ++fr) {
-            const int ml = m0 + fr, bl = ml / (TR * Wq), rem = ml % (TR * Wq), ty = rem / Wq, x = rem % Wq;
-            pix[fr] = (bl * g.WY + S * ty) * wxp + x;
-          }
-          for (size_t p = 0; p < ry.size(); ++p)
-            for (size_t t = 0; t < ry[p].size(); ++t) {
-              const int wy = ry[p][t] - miny, wx = rx[p][t] - minx;
-              const int toff = wy * wxp + (S == 2 ? (wx & 1) * g.HX + (wx >> 1) : wx);
-              for (int gi = 0; gi < 4; ++gi) {
-                int cnt[16] = {0};
-                int c = 0;
-                for (int i = 0; i < 16; ++i) {
-                  const int l = grp[gi][i];
-                  const int slot = ((pix[l & 15] + toff) * 10 + (l >> 4)) % 16;
-                  c = std::max(c, ++cnt[slot]);
-                }
-                worst = std::max(worst, c);
-              }
-            }
-        }
-        if (worst < best_c) { best_c = worst; best_w = wxp; }
-        if (best_c == 1) break;
-      }
-      g.WXP = best_w;
-    }
-    int ntaps[4] = {0, 0, 0, 0}, tap[4][25];  // per phase: window pixel offset | weight tap << 16
-    for (int p = 0; p < 4; ++p) { g.oy_off[p] = 0; g.ox_off[p] = 0; g.send[p] = 0; }
-    for (int p = 0; p < g.nphases; ++p) {
-      ntaps[p] = (int)ry[p].size();
-      if (ntaps[p] < nsb) return fail("igemm4: a phase has fewer taps than ring stages");
-      g.oy_off[p] = oyo[p]; g.ox_off[p] = oxo[p];
-      for (int t = 0; t < ntaps[p]; ++t) {
-        const int wy = ry[p][t] - miny, wx = rx[p][t] - minx;
-        const int X = S == 2 ? (wx & 1) * g.HX + (wx >> 1) : wx;
-        tap[p][t] = (wy * g.WXP + X) | (wt[p][t] << 16);
-      }
-    }
-    g.wpix = NI * g.WY * g.WXP;
-    g.npw = (g.wpix * 10 + 63) / 64;  // 160-byte LDS pixels (igemm4.hip PIXS)
-    g.win_bytes = g.npw * 1024;
-    if (g.npw > 255) return fail("igemm4: window of more than 255 DMA pieces");
-    const int nch = Kc / 64;
-    const bool shared = nch == 1;
-    g.ring_bytes = nsb * bn * 128;
-    const int scratch = wmc * bn * 8 + 64;
-    int steps = 0;
-    const int nwb = (nch > 1 && g.ring_bytes + 2 * g.win_bytes + scratch <= 160 * 1024) ? 2 : 1;
-    for (int p = 0, w = 0; p < g.nphases; ++p)
-      for (int c = 0; c < nch; ++c, ++w) steps += ntaps[p] + ((w > 0 && !shared && nwb == 1) ? nsb - 1 : 0);
-    g.steps = steps;
-    g.part_off = g.ring_bytes + nwb * g.win_bytes;
-    g.desc_off = g.part_off + scratch;
-    plan.nwb = nwb;
-    plan.shm = (size_t)g.desc_off + (size_t)8 * (steps + 1);
-    if (plan.shm > 160 * 1024) return fail("igemm4: window + ring exceed 160 KiB of LDS");
-    // the step schedule, unrolled (the order igemm4.hip's loaders and compute waves follow):
-    // phases, 64-channel chunks, taps; ahead of a chunk whose window reuses the only window
-    // buffer, NSB-1 empty steps (the loaders may overwrite it only once nobody reads it)
-    struct K { int p, c, t, nt, wl, sw, wlen; };
-    K k{0, 0, 0, ntaps[0], 0, 0, ntaps[0]};
-    const uint32_t bstage = (uint32_t)bn * 128;
-    plan.cd.assign(steps + 1, IG4CDesc{});
-    plan.ld.assign(steps, IG4LDesc{});
-    for (int x = 0; x < steps; ++x) {
-      const bool real = k.t >= 0;
-      const int tp = tap[k.p][std::max(k.t, 0)];
-      IG4CDesc& c = plan.cd[x];
-      c.uoff = (uint32_t)(g.ring_bytes + (nwb == 2 ? (k.wl & 1) : 0) * g.win_bytes + (tp & 0xffff) * 160);
-      c.soff = (uint32_t)(x % nsb) * bstage | (real ? 0u : IG4_EMPTY);
-      IG4LDesc& l = plan.ld[x];
-      const int wtap = tp >> 16, k0 = k.c * 64;
-      const size_t boff = bkn ? ((size_t)wtap * Kc + k0) * N * 2 : ((size_t)wtap * N * Kc + k0) * 2;
-      if (boff >= IG4_EMPTY) return fail("igemm4: weight tensor beyond 2 GiB");
-      l.boff = real ? (uint32_t)boff : IG4_EMPTY;
-      l.soff = (uint32_t)(x % nsb) * bstage;
-      l.win = 0;
-      if (!shared) {
-        if (nwb == 2) {  // the NEXT window streams in slices over this window's steps NSB-1 .. wlen-1
-          const bool last_win = (k.c + 1 == nch) && (k.p + 1 == g.nphases);
-          if (!last_win && k.sw >= nsb - 1) {
-            const int ns = k.wlen - (nsb - 1), i = k.sw - (nsb - 1);
-            const int ch = k.c + 1 == nch ? 0 : k.c + 1;
-            l.win = (uint32_t)(i * g.npw / ns) | (uint32_t)((i + 1) * g.npw / ns) << 8 | (uint32_t)((k.wl + 1) & 1) << 16 |
-                    (uint32_t)ch << 17;
-          }
-        } else if (k.wl > 0 && k.t == 0) {  // behind NSB-1 empty steps: the old window is dead
-          l.win = (uint32_t)g.npw << 8 | (uint32_t)k.c << 17;
-        }
-      }
-      g.send[k.p] = x + 1;
-      // next step
-      ++k.t; ++k.sw;
-      if (k.t < k.nt) continue;
-      if (++k.c == nch) { k.c = 0; ++k.p; }
-      if (k.p >= g.nphases) { k.p = g.nphases - 1; k.t = 0; k.nt = 1 << 20; continue; }
-      if (!shared) ++k.wl;
-      const int pre = (!shared && nwb == 1) ? nsb - 1 : 0;
-      k.nt = ntaps[k.p]; k.t = -pre; k.sw = 0; k.wlen = pre + k.nt;
-    }
-    plan.cd[steps] = plan.cd[steps - 1];  // the last step's (unused) prefetch
-    plan.cd[steps].soff |= IG4_EMPTY;
-    g.fd_hw = fastdiv_make(HW); g.fd_tw = fastdiv_make(TR * Wq); g.fd_wq = fastdiv_make(Wq);
-    g.fd_wimg = fastdiv_make(g.WY * g.WXP); g.fd_wxp = fastdiv_make(g.WXP);
-    g.mtiles = (int)(((size_t)Bn * HW) / bm);
-    g.ntiles = N / bn;
-    return true;
-  }
-
-  // LDS bytes of an igemm4 launch, or -1 (with the reason) when the shape does not fit the tile
-  py::tuple igemm4_plan(int cfg, int mode, int Bn, int Kc, int Hout, int Wout, int N, int pad_y, int pad_x) {
-    int bm, bn, nsb, wmc, wnc;
-    if (dt_ == 2 || KF(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wmc, &wnc)) return py::make_tuple(-1, std::string("bad cfg"));
-    IG4Plan plan;
-    std::string why;
-    if (!igemm4_geometry(plan, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, false, &why))
-      return py::make_tuple(-1, why);
-    return py::make_tuple((int)plan.shm, std::string("nwb=") + std::to_string(plan.nwb));
-  }
-
-  int igemm4_ex(const std::string& name, int mode, uintptr_t A, uintptr_t Bw, uintptr_t C, int Bn, int Hin, int Win,
-                int Kc, int Hout, int Wout, int N, int pad_y, int pad_x, int cfg, int ldc, int cofs, uintptr_t bias,
-                int act, float leak, uintptr_t stats, int stream, int bkn, uintptr_t bnb_x, uintptr_t bnb_y,
-                uintptr_t bnb_mean, uintptr_t bnb_rstd, int bnb_rpg, int bnb_act, float bnb_leak, int bnb_store_g) {
-    int bm, bn, nsb, wmc, wnc;
-    if (dt_ == 2 || KF(dcg_igemm4_tile)(cfg, &bm, &bn, &nsb, &wmc, &wnc))
-      throw std::runtime_error("bad igemm4 cfg " + std::to_string(cfg) + " for this element type");
-    IG4Plan plan;
-    std::string why;
-    if (!igemm4_geometry(plan, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x, bm, bn, nsb, wmc, bkn != 0, &why))
-      throw std::runtime_error(why);
-    IG4Args& a = plan.g;
-    a.cdesc = reinterpret_cast<const IG4CDesc*>(dev_alloc(plan.cd.size() * sizeof(IG4CDesc), plan.cd.data()));
-    a.ldesc = reinterpret_cast<const IG4LDesc*>(dev_alloc(plan.ld.size() * sizeof(IG4LDesc), plan.ld.data()));
-    if ((mode == 0 && (Hout != (Hin + 1) / 2 || Wout != (Win + 1) / 2)) || (mode == 1 && (Hout != 2 * Hin || Wout != 2 * Win)))
-      throw std::runtime_error("igemm4: stride-2 SAME shapes only");
-    if (ldc % 4 || cofs % 4 || ldc < cofs + N) throw std::runtime_error("igemm4: 8-byte output rows");
-    a.A = P<const elem_t>(A); a.Bn = Bn; a.H = Hin; a.W = Win; a.Kc = Kc;
-    a.Bw = P<const elem_t>(Bw); a.N = N;
-    a.C = P<elem_t>(C); a.outH = Hout; a.outW = Wout; a.ldc = ldc; a.cofs = cofs; a.ostride = mode == 1 ? 2 : 1;
-    a.bias = P<const float>(bias); a.act = act; a.leak = leak; a.stats = P<float>(stats);
-    const size_t a_elems = (size_t)Bn * Hin * Win * Kc, b_elems = (size_t)25 * N * Kc;
-    if (a_elems * es_ >= OOB || b_elems * es_ >= OOB) throw std::runtime_error("igemm4 operand exceeds the buffer range");
-    a.a_bytes = (uint32_t)(a_elems * es_); a.b_bytes = (uint32_t)(b_elems * es_);
-    const size_t c_rows = (size_t)Bn * Hout * Wout;
-    AccList acc;
-    acc.r(A, a_elems * es_).r(Bw, b_elems * es_).r(bias, (size_t)N * 4)
-        .w(C, (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_)
-        .w(stats, (size_t)a.mtiles * a.nphases * 2 * N * 4);
-    if (bnb_x || bnb_store_g) {
-      const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
-      if (!stats || !bnb_y) throw std::runtime_error("igemm4 fused backward: needs stats and y");
-      if (bnb_store_g) {
-        a.bnb_x = P<const elem_t>(bnb_y); a.bnb_y = P<const elem_t>(bnb_y);
-        a.bnb_rpg = 1 << 30; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak; a.bnb_store_g = 1;
-        acc.r(bnb_y, xy_bytes);
-      } else {
-        if (bnb_rpg <= 0 || !bnb_mean || !bnb_rstd) throw std::runtime_error("igemm4 bnb: needs rows-per-group, mean, rstd");
-        if (bnb_rpg % bm || ((size_t)Bn * a.Hq * a.Wq) % bnb_rpg)
-          throw std::runtime_error("igemm4 bnb: tile rows must divide the group");
-        a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
-        a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
-        a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
-        const size_t groups = (size_t)Bn * a.Hq * a.Wq / bnb_rpg;
-        acc.r(bnb_x, xy_bytes).r(bnb_y, xy_bytes).r(bnb_mean, groups * N * 4).r(bnb_rstd, groups * N * 4);
-      }
-    }
-    if (const char* ab = getenv("DCGAN_IGEMM_ABLATE")) a.ablate = atoi(ab);  // kernel studies only
-    if (const char* st = getenv("DCGAN_IGEMM_STAMPS")) a.stamps = reinterpret_cast<unsigned long long*>(strtoull(st, nullptr, 0));
-    last_mtiles_ = a.mtiles;
-    last_nphases_ = a.nphases;
-    const size_t shm = plan.shm;
-    const unsigned blocks = (unsigned)(a.mtiles * a.ntiles);
-    return add(name, stream, [this, a, cfg, bkn, blocks, shm](hipStream_t s) {
-      return KF(dcg_igemm4_launch)(&a, cfg, bkn, blocks, shm, s);
-    }, acc.v);
-  }
-
 
   int last_mtiles() const { return last_mtiles_; }
   int last_nphases() const { return last_nphases_; }
@@ -1169,11 +900,7 @@ static py::tuple igemm_tile(int cfg, int dtype) {
   int bm = 0, bn = 0, ns = 0;
   int rc;
 #define DT(fn) (dtype == 2 ? fn##_f32 : dtype == 1 ? fn##_f16 : fn)
-  if (cfg >= 500) {
-    int wm = 0, wn = 0;
-    if (dtype == 2) throw std::runtime_error("igemm4: 16-bit builds only");
-    rc = (dtype == 1 ? dcg_igemm4_tile_f16 : dcg_igemm4_tile)(cfg, &bm, &bn, &ns, &wm, &wn);
-  } else if (cfg >= 400) rc = -1;
+  if (cfg >= 400) rc = -1;
   else if (cfg >= 200) rc = DT(dcg_igemm3_tile)(cfg, &bm, &bn, &ns);
   else rc = DT(dcg_igemm_tile)(cfg, &bm, &bn);
 #undef DT
@@ -1230,7 +957,6 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("kb_valid"), py::arg("splits"), py::arg("bnb_x") = 0, py::arg("bnb_y") = 0,
            py::arg("bnb_mean") = 0, py::arg("bnb_rstd") = 0, py::arg("bnb_rpg") = 0, py::arg("bnb_act") = 0,
            py::arg("bnb_leak") = 0.f, py::arg("bnb_store_g") = 0)
-      .def("igemm4_plan", &Program::igemm4_plan)
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)

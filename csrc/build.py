@@ -6,11 +6,14 @@
 * ``_dcgan_host``: host-side C++ runtime -- TFRecord reader/writer (CRC32C), tf.train.Example
   parsing, multi-threaded shuffling loader with a pinned ring buffer (csrc/host/*.cpp).
 
-Objects are cached in build/ keyed by source mtime; the .so files land next to the Python
-package so they travel with the repository snapshot to the GPU box.
+Objects are cached in build/ keyed by a content hash (sha256 of the compile command and of every
+source / header the object depends on, kept in ``<object>.sig``): a stale object survives neither
+an edit nor a copied tree with shifted mtimes. ``--force`` rebuilds everything. The .so files land
+next to the Python package so they travel with the repository snapshot to the GPU box.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import re
 import subprocess
@@ -35,11 +38,33 @@ def _py_includes():
     return [pybind11.get_include(), sysconfig.get_paths()["include"]]
 
 
-def _newer(src_list, dst) -> bool:
-    if not os.path.exists(dst):
-        return True
-    t = os.path.getmtime(dst)
-    return any(os.path.getmtime(s) > t for s in src_list)
+FORCE = False  # --force: rebuild every object and library
+
+
+def _signature(src_list, cmd) -> str:
+    h = hashlib.sha256()
+    h.update("\0".join(cmd).encode())
+    for s in sorted(src_list):
+        h.update(b"\0" + os.path.basename(s).encode() + b"\0")
+        with open(s, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stale(src_list, dst, cmd) -> bool:
+    """True when dst must be (re)built: missing, --force, or its recorded content hash differs."""
+    sig = _signature(src_list, cmd)
+    try:
+        with open(dst + ".sig") as f:
+            old = f.read().strip()
+    except OSError:
+        old = ""
+    return FORCE or not os.path.exists(dst) or old != sig
+
+
+def _mark(src_list, dst, cmd) -> None:
+    with open(dst + ".sig", "w") as f:
+        f.write(_signature(src_list, cmd) + "\n")
 
 
 def _run(cmd):
@@ -86,31 +111,42 @@ def build_hip(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(os.path.join(CSRC, "hip", f) for f in os.listdir(os.path.join(CSRC, "hip")) if f.endswith(".hip"))
     common = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC]
-    jobs_list = []
+    jobs_list = []  # (cmd, deps, obj)
     objs = []
     for s in srcs:  # every kernel file once per element type it declares (`// dcg-variants:`)
         deps = sorted(_deps(s))
         for tag, defs in _variants(s):
             o = os.path.join(BUILD, os.path.basename(s) + tag + ".o")
             objs.append(o)
-            if _newer(deps, o):
-                jobs_list.append([HIPCC] + common + defs + ["-c", s, "-o", o])
+            cmd = [HIPCC] + common + defs + ["-c", s, "-o", o]
+            if _stale(deps, o, cmd):
+                jobs_list.append((cmd, deps, o))
     binding = os.path.join(CSRC, "bindings.cpp")
     bo = os.path.join(BUILD, "bindings.o")
     objs.append(bo)
-    if _newer(sorted(_deps(binding)), bo):
-        inc = []
-        for i in _py_includes():
-            inc += ["-I", i]
-        jobs_list.append([HIPCC, "-O2", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC] + inc +
-                         ["-c", binding, "-o", bo])
+    inc = []
+    for i in _py_includes():
+        inc += ["-I", i]
+    bcmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", "--offload-arch=%s" % ARCH, "-I", CSRC] + inc + ["-c", binding, "-o", bo]
+    bdeps = sorted(_deps(binding))
+    if _stale(bdeps, bo, bcmd):
+        jobs_list.append((bcmd, bdeps, bo))
+
+    def job(j):
+        cmd, deps, o = j
+        out = _run(cmd)
+        _mark(deps, o, cmd)
+        return out
+
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        for out in ex.map(_run, jobs_list):
+        for out in ex.map(job, jobs_list):
             if verbose and out.strip():
                 print(out)
     so = os.path.join(PKG, "_dcgan_hip" + _ext_suffix())
-    if _newer(objs, so):
-        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", so])
+    lcmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH] + objs + ["-o", so]
+    if _stale(objs, so, lcmd):
+        _run(lcmd)
+        _mark(objs, so, lcmd)
     return so
 
 
@@ -122,21 +158,25 @@ def build_host(verbose: bool = False) -> str:
     so = os.path.join(PKG, "_dcgan_host" + _ext_suffix())
     if not srcs:
         return ""
-    if _newer(srcs + hdrs, so):
-        inc = []
-        for i in _py_includes():
-            inc += ["-I", i]
-        flags = ["-O3", "-fPIC", "-std=c++17", "-shared", "-pthread", "-I", hsrc]
-        if os.environ.get("DCGAN_HOST_SANITIZE"):
-            flags = ["-O1", "-g", "-fPIC", "-std=c++17", "-shared", "-pthread", "-I", hsrc,
-                     "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
-        _run(["g++"] + flags + inc + srcs + ["-o", so])
+    inc = []
+    for i in _py_includes():
+        inc += ["-I", i]
+    flags = ["-O3", "-fPIC", "-std=c++17", "-shared", "-pthread", "-I", hsrc]
+    if os.environ.get("DCGAN_HOST_SANITIZE"):
+        flags = ["-O1", "-g", "-fPIC", "-std=c++17", "-shared", "-pthread", "-I", hsrc,
+                 "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
+    cmd = ["g++"] + flags + inc + srcs + ["-o", so]
+    if _stale(srcs + hdrs, so, cmd):
+        _run(cmd)
+        _mark(srcs + hdrs, so, cmd)
     return so
 
 
 def main(argv=None) -> int:
+    global FORCE
     argv = sys.argv[1:] if argv is None else argv
     verbose = "-v" in argv
+    FORCE = "--force" in argv
     built = []
     if "--host-only" not in argv:
         built.append(build_hip(verbose))

@@ -434,8 +434,6 @@ extern "C" int DCG_API(dcg_wgrad_launch)(const dcg::WGradArgs* a, int cfg, int s
 // 16-bit-only kernels: no fp32 build (the engine does not select them for fp32)
 extern "C" int DCG_API(dcg_igemm_tile)(int, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_igemm_launch)(const dcg::IGemmArgs*, int, int, int, hipStream_t) { return -2; }
-extern "C" int DCG_API(dcg_igemm4_tile)(int, int*, int*, int*, int*, int*) { return -1; }
-extern "C" int DCG_API(dcg_igemm4_launch)(const dcg::IG4Args*, int, int, unsigned, size_t, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_igemm3_threads)(int) { return 256; }
 extern "C" int DCG_API(dcg_wgrad3_tile)(int, int*, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_wgrad3_launch)(const dcg::WGrad3Args*, int, hipStream_t) { return -2; }

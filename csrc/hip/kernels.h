@@ -56,7 +56,6 @@ struct IGemmArgs {
   int bnb_store_g;
 };
 
-struct IG4Args;  // igemm4.hip (csrc/hip/ig4.h)
 
 struct WGradArgs {
   const elem_t* G; int Hg, Wg, Mc;     // gathered operand [B][Hg][Wg][Mc] (plain: [K][Mc])

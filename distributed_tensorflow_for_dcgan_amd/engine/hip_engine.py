@@ -63,6 +63,7 @@ from ..parallel import dist as D
 RELU, LRELU, TANH, NONE = 1, 2, 3, 0
 DTYPES = {"bf16": (0, torch.bfloat16), "fp16": (1, torch.float16), "fp32": (2, torch.float32)}
 SCHEDULES = ("fused", "ddp", "concurrent", "serial")
+DDP_SCHEDULES = ("ddp", "concurrent", "serial")  # schedules that issue the gradient all-reduces
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
@@ -977,7 +978,10 @@ class HipEngine:
             # "concurrent" by default: inside ONE hipGraph the collectives do not overlap the
             # compute branches on ROCm (emulated ring collectives, 64x64: 1.39 ms vs 1.33 for
             # the segmented step; profiles/r3/ab_ddp_one_graph_r3.txt)
-            return os.environ.get("DCGAN_DDP_SCHEDULE") or "concurrent"
+            env = os.environ.get("DCGAN_DDP_SCHEDULE") or "concurrent"
+            if env not in DDP_SCHEDULES:  # "fused" here would issue no all-reduce at all
+                raise ValueError("DCGAN_DDP_SCHEDULE=%r: expected one of %s" % (env, ", ".join(DDP_SCHEDULES)))
+            return env
         return req or "fused"
 
     def _one_graph(self) -> bool:

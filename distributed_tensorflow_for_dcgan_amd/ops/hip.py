@@ -81,38 +81,15 @@ def igemm3_lds(cfg: int) -> int:
     return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
 
 
-# igemm4.hip (halo window + loader waves): cfg 500 + 10k + id, B ring stages NSB = (4, 3)[k]; the
-# compute waves are 64x64 each (+ 4 loader waves); the window geometry is checked per shape by
-# Program.igemm4_plan (csrc/bindings.cpp)
-IGEMM4_TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (512, 64), 5: (64, 256),
-                6: (128, 64), 7: (64, 128)}
-IGEMM4_STAGES = (4, 3)
-_IG4_PLAN = {}
-
-
-def igemm4_lds(cfg: int, mode: int, Bn: int, Kc: int, Hout: int, Wout: int, N: int, pad_y: int = 1,
-               pad_x: int = 1) -> Optional[int]:
-    """LDS bytes of an igemm4 launch, or None when the tile does not fit the shape."""
-    if cfg < 500 or cfg % 10 not in IGEMM4_TILES or (cfg - 500) // 10 >= len(IGEMM4_STAGES):
-        return None
-    key = (cfg, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x)
-    if key not in _IG4_PLAN:
-        shm, _ = ext().Program(0, True).igemm4_plan(cfg, mode, Bn, Kc, Hout, Wout, N, pad_y, pad_x)
-        _IG4_PLAN[key] = None if shm < 0 else shm
-    return _IG4_PLAN[key]
-
-
 # fp32 build (igemm_f32.hip): the only tile family of that element type, cfg 200..203
 IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)}
 
 
 def tile_of(cfg: int, dtype: int = 0) -> Tuple[int, int]:
-    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..239 igemm3.hip, 500..519
-    igemm4.hip; dtype 2 (fp32): igemm_f32.hip."""
+    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..239 igemm3.hip; dtype 2
+    (fp32): igemm_f32.hip."""
     if dtype == 2:
         return IGEMM_F32_TILES[cfg]
-    if cfg >= 500:
-        return IGEMM4_TILES[cfg % 10]
     if cfg >= 200:
         return IGEMM3_TILES[cfg % 10]
     return IGEMM_CFGS[cfg % 100]
@@ -136,8 +113,6 @@ def pick_igemm_f32(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
 
 def bnb_fits(cfg: int) -> bool:
     """True when the tile's LDS can hold the fused BN-backward statistics scratch (epilogue.h)."""
-    if cfg >= 500:  # igemm4 sizes its LDS per launch; its epilogue needs no C tile in LDS
-        return True
     bm, bn = tile_of(cfg)
     if cfg < 200:
         return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= 2 * (bm + bn) * 128
@@ -209,7 +184,7 @@ TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "igemm_tun
 def tuned_table() -> dict:
     """Per-layer tile choices measured on MI355X by ``benchmarks/bench_kernels.py --write``
     (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> "cfg:splits" (or a bare cfg): cfg < 200 is
-    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip, 500..519 igemm4.hip)."""
+    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip)."""
     global _TUNED
     if _TUNED is None:
         _TUNED = {}
@@ -242,9 +217,6 @@ def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wo
     if ent is not None:
         cfg, sp = ent
         ok = cfg >= 200 or (not bkn and sp == 1 and cfg % 100 in IGEMM_CFGS)
-        if cfg >= 500:
-            pads = same_pads(Hout)[0] if mode == 1 else same_pads(Hin)[0]
-            ok = sp == 1 and igemm4_lds(cfg, mode, Bn, Kc, Hout, Wout, N, pads, pads) is not None
         if ok and (rows_per_group is None or rows_per_group % tile_of(cfg)[0] == 0):
             return cfg, sp
     if N % 8 == 0 and N >= 64:

@@ -122,6 +122,12 @@ def run(flags: Flags, out=None) -> int:
     if preset:
         print("--dataset=%s preset: %s" % (flags.dataset, ", ".join("%s=%s" % kv for kv in sorted(preset.items()))),
               file=out)
+        if "output_size" in preset or "c_dim" in preset:
+            # the reference ignores --dataset and always builds 64x64x3 (distriubted_model.py:7-11)
+            print("WARNING: --dataset=%s changed the model shape to %dx%dx%d; the reference always trains "
+                  "64x64x3. Records of another shape fail to decode (image_raw size check); pass "
+                  "--output_size/--c_dim to override." % (flags.dataset, flags.output_size, flags.output_size,
+                                                         flags.c_dim), file=out)
     if flags.job_name == "ps":
         print("--job_name=ps: this framework trains with synchronous data parallelism over RCCL; "
               "there is no parameter server to run. Launch one worker per GPU instead "

@@ -832,114 +832,3 @@ def test_head_bwd_row_splits(R, groups, RS):
         pg = part[gi * ppg:(gi + 1) * ppg].reshape(RS, S, 2, C).sum(0)
         close(pg[:, 0], gg.sum(0), 1e-4, "sum g")
         close(pg[:, 1], (gg * xh).sum(0), 1e-4, "sum g xhat")
-
-
-
-IG4 = [500, 501, 502, 503, 504, 505, 506, 507, 510, 511, 516, 517]  # 51x: 3-stage B ring
-
-
-def _ig4_cfgs(mode, B, Kc, Ho, Co, pad):
-    h = H()
-    out = []
-    for cfg in IG4:
-        if h.IGEMM4_TILES[cfg % 10][1] > Co:
-            continue
-        if h.igemm4_lds(cfg, mode, B, Kc, Ho, Ho, Co, pad, pad) is not None:
-            out.append(cfg)
-    return out
-
-
-@pytest.mark.parametrize("B,Hs,Ci,Co", [(2, 32, 64, 128), (4, 16, 128, 256), (8, 8, 256, 512), (4, 16, 64, 64)])
-@pytest.mark.parametrize("bkn", [0, 1])
-def test_igemm4_conv(B, Hs, Ci, Co, bkn):
-    """igemm4.hip (input window in LDS, loader waves, transposed epilogue): stride-2 SAME conv with
-    bias + lrelu + BN statistics, every tile that fits the shape (one and two window buffers),
-    both weight layouts, vs the fp32 reference."""
-    h = H()
-    x = bf(rnd(B, Hs, Hs, Ci, seed=80))
-    w = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=81))
-    bias = rnd(Co, scale=0.1, seed=82)
-    ref_pre = R.conv2d_same(x.float(), w.float(), bias)
-    wp = w.reshape(25, Ci, Co).contiguous() if bkn else h.pack_conv_weight(w.float(), "conv", "fwd")
-    Ho = -(-Hs // 2)
-    pad = h.same_pads(Hs)[0]
-    cfgs = _ig4_cfgs(0, B, Ci, Ho, Co, pad)
-    assert cfgs, "no igemm4 tile fits"
-    for cfg in cfgs:
-        y, st = h.conv2d_same(x, wp, Co, bias=bias, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn))
-        tag = "igemm4 cfg%d bkn%d" % (cfg, bkn)
-        close(y, R.lrelu(ref_pre), 1.5e-2, tag)
-        s = st.sum(0)
-        close(s[0], ref_pre.reshape(-1, Co).sum(0), 2e-3, "sum " + tag)
-        close(s[1], ref_pre.reshape(-1, Co).pow(2).sum(0), 2e-3, "sumsq " + tag)
-        y2, st2 = h.conv2d_same(x, wp, Co, bias=bias, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn))
-        assert torch.equal(y, y2) and torch.equal(st, st2), "nondeterministic " + tag
-
-
-@pytest.mark.parametrize("B,Hi,Ci,Co", [(4, 4, 512, 256), (2, 8, 256, 128), (2, 16, 128, 64), (4, 16, 64, 128)])
-def test_igemm4_deconv_and_g_dgrad(B, Hi, Ci, Co):
-    """igemm4 conv_transpose (the 4 sub-pixel phases one after the other in each workgroup) with
-    bias + statistics, and the G data gradient (conv with the k-major deconv weight)."""
-    h = H()
-    Ho = 2 * Hi
-    pad = h.same_pads(Ho)[0]
-    x = bf(rnd(B, Hi, Hi, Ci, seed=83))
-    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=84))  # [5,5,out,in] = [25][N][Kc]
-    bias = rnd(Co, scale=0.1, seed=85)
-    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
-    cfgs = _ig4_cfgs(1, B, Ci, Ho, Co, pad)
-    assert cfgs, "no igemm4 tile fits"
-    for cfg in cfgs:
-        y, st = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, stats=True, cfg=cfg)
-        close(y, ref, 1e-2, "igemm4 deconv cfg%d" % cfg)
-        close(st.sum(0)[0], ref.reshape(-1, Co).sum(0), 3e-3, "igemm4 deconv stats cfg%d" % cfg)
-    xd = rnd(B, Hi, Hi, Ci, seed=86).requires_grad_(True)
-    yd = R.conv2d_transpose_same(xd, w.float(), (Ho, Ho))
-    dy = bf(rnd(B, Ho, Ho, Co, seed=87))
-    (gx,) = torch.autograd.grad(yd, xd, dy.float())
-    for cfg in _ig4_cfgs(0, B, Co, Hi, Ci, h.same_pads(Ho)[0]):
-        out = h.conv2d_same(dy, w.reshape(25, Co, Ci), Ci, cfg=cfg, bkn=True)
-        close(out, gx, 1e-2, "igemm4 G dgrad cfg%d" % cfg)
-
-
-@pytest.mark.parametrize("store_g", [0, 1])
-def test_igemm4_fused_bn_backward_stats(store_g):
-    """igemm4 data-gradient GEMM with the BN-backward (or activation-backward) statistics in its
-    register epilogue: stored tensor and partial sums vs the fp32 reference."""
-    h = H()
-    B, Hi, Ci, Co = 4, 16, 128, 64
-    Ho = 2 * Hi
-    dy = bf(rnd(B, Hi, Hi, Ci, seed=60))
-    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=61)).reshape(25, Co, Ci).contiguous()
-    x = bf(rnd(B, Ho, Ho, Co, seed=62))
-    y = bf(rnd(B, Ho, Ho, Co, seed=63) - 0.3)
-    mean = rnd(1, Co, scale=0.2, seed=64)
-    rstd = rnd(1, Co, seed=65).abs() + 0.5
-    da_ref = R.conv2d_transpose_same(dy.float(), w.reshape(5, 5, Co, Ci).float(), (Ho, Ho))
-    mph = B * Hi * Hi
-    for cfg in _ig4_cfgs(1, B, Ci, Ho, Co, 1):
-        bm = h.tile_of(cfg)[0]
-        if mph % bm:
-            continue
-        da = torch.empty(B, Ho, Ho, Co, device=dev, dtype=torch.bfloat16)
-        st = torch.empty(mph // bm * 4, 2, Co, device=dev)
-        prog = h.ext().Program()
-        if store_g:
-            prog.igemm_ex("actb", 1, h._p(dy), h._p(w), h._p(da), B, Hi, Hi, Ci, Ho, Ho, Co, 1, 1, cfg, 0, Co, 0, 0, 0,
-                          0.2, h._p(st), 0, 0, -1, 1, h._p(y), h._p(y), 0, 0, 0, 2, 0.2, 1)
-        else:
-            prog.igemm_ex("bnb", 1, h._p(dy), h._p(w), h._p(da), B, Hi, Hi, Ci, Ho, Ho, Co, 1, 1, cfg, 0, Co, 0, 0, 0,
-                          0.2, h._p(st), 0, 0, -1, 1, h._p(x), h._p(y), h._p(mean), h._p(rstd), mph, 2, 0.2, 0)
-        h.run(prog)
-        torch.cuda.synchronize()
-        g = da_ref * torch.where(y.float() > 0, 1.0, 0.2)
-        s = st.sum(0)
-        tag = "cfg%d store_g%d" % (cfg, store_g)
-        if store_g:
-            close(da, g, 1e-2, "g " + tag)
-            close(s[0], g.reshape(-1, Co).sum(0), 3e-3, "sum g " + tag)
-        else:
-            close(da, da_ref, 1e-2, "da " + tag)
-            xh = (x.float() - mean.reshape(Co)) * rstd.reshape(Co)
-            close(s[0], g.reshape(-1, Co).sum(0), 3e-3, "sum g " + tag)
-            close(s[1], (g * xh).reshape(-1, Co).sum(0), 3e-3, "sum g xhat " + tag)

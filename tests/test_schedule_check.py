@@ -120,3 +120,21 @@ def test_ddp_g_buckets_tile_the_gradient():
     assert cuts[0][2] == eng.grad_g.flat.numel()
     for (_, lo, _), (_, _, hi) in zip(cuts, cuts[1:]):
         assert lo == hi
+
+
+@pytest.mark.parametrize("bad", ["fused", "concurent", "graph"])
+def test_bad_ddp_schedule_env_is_rejected(monkeypatch, bad):
+    """DCGAN_DDP_SCHEDULE must name a schedule that issues the all-reduces: 'fused' would train
+    the ranks independently, a typo would run the serial code over the concurrent segments."""
+    monkeypatch.setenv("DCGAN_DDP_SCHEDULE", bad)
+    with pytest.raises(ValueError, match="DCGAN_DDP_SCHEDULE"):
+        _dry(world=2)
+
+
+@pytest.mark.parametrize("good", ["ddp", "concurrent", "serial"])
+def test_ddp_schedule_env_selects_the_schedule(monkeypatch, good):
+    monkeypatch.setenv("DCGAN_DDP_SCHEDULE", good)
+    eng = _dry(world=2)
+    assert eng._schedule() == good
+    hz, _ = SC.check_engine(eng)
+    assert hz == []
