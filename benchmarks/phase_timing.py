@@ -14,22 +14,49 @@ import torch
 
 from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
 from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
 
 
 class FakeReducer:
-    """Stand-in for parallel.dist.GradAllReducer on ONE GPU: occupies the comm stream for a
-    given time (a spinning kernel), at the same points of the schedule as the real
-    all-reduce, to see which schedule hides which collective latency (no bandwidth
-    contention is modelled). Capturable: the "ddp" schedule records it inside its graph."""
+    """Stand-in for parallel.dist.GradAllReducer on ONE GPU, at the same points of the schedule
+    as the real all-reduce. ``kind="rccl"`` (default): the RCCL-like copy kernel of
+    csrc/hip/comm_emu.hip -- ``nwg`` workgroups (RCCL's channels, one CU each) stream
+    2 (W-1)/W x the bucket's bytes through HBM (read the gradient, write a scratch buffer) paced
+    to the modelled ring time, so the collective takes CUs and HBM bandwidth from the compute it
+    overlaps, as the real one does. ``kind="sleep"``: round 3's single-thread timer
+    (``torch.cuda._sleep``: no CU or HBM footprint). Capturable: the "ddp" schedule records it
+    inside its graph."""
 
-    def __init__(self, us, cycles_per_us, numel=0):
+    def __init__(self, us, flat=None, world=8, esize=4, nwg=32, kind="rccl", cycles_per_us=0.0):
         self.us = float(us)
+        self.flat = flat
+        self.numel = 0 if flat is None else flat.numel()
+        self.kind = kind
         self.cycles = int(us * cycles_per_us)
-        self.numel = numel
+        self.nwg = int(nwg)
+        self.bytes = (int(2.0 * (world - 1) / world * self.numel * esize) // 16) * 16
+        self.prog = None
+        if kind == "rccl" and self.bytes > 0 and flat is not None:
+            from distributed_tensorflow_for_dcgan_amd.ops import hip as H
+            src_bytes = self.numel * flat.element_size()
+            # the wire moves up to 2x the payload: read it twice over when the slice is shorter
+            self.src = flat if src_bytes >= self.bytes else flat.repeat(-(-self.bytes // src_bytes))
+            self.dst = torch.empty(self.bytes // 4, device=flat.device, dtype=torch.float32)
+            self.prog = H.ext().Program()
+            self.prog.comm_emulate("comm_emu", self.src.data_ptr(), self.dst.data_ptr(), self.bytes, self.us,
+                                   self.nwg, 0)
 
     def issue(self):  # on the comm stream (the engine's executor orders it after the producers)
-        if self.cycles > 0:
+        if self.kind == "rccl" and self.prog is not None:
+            from distributed_tensorflow_for_dcgan_amd.ops import hip as H
+            H.run(self.prog)
+        elif self.cycles > 0:
             torch.cuda._sleep(self.cycles)
+
+    def accesses(self):  # as the real reducer: the gradient slice is read and written
+        if self.flat is None:
+            return []
+        return [(self.flat.data_ptr(), self.numel * self.flat.element_size(), True)]
 
 
 def _cycles_per_us():
@@ -58,14 +85,20 @@ def main():
                     help="emulate every bucket with the ring model at this bus bandwidth (GB/s)")
     ap.add_argument("--fake_lat_us", type=float, default=10.0)
     ap.add_argument("--fake_world", type=int, default=8)
+    ap.add_argument("--fake_kind", default="rccl", choices=["rccl", "sleep"],
+                    help="rccl: CU + HBM-consuming copy kernel (comm_emu.hip); sleep: round-3 timer")
+    ap.add_argument("--fake_nwg", type=int, default=32, help="workgroups (RCCL channels) of the rccl stand-in")
+    ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig()
     ddp = a.schedule != "concurrent" or bool(a.fake_comm_us) or a.fake_busbw_gbs > 0
-    eng = HipEngine(cfg, a.batch_size, dev, ddp=ddp, schedule=a.schedule if ddp else None)
+    eng = HipEngine(cfg, a.batch_size, dev, ddp=ddp, schedule=a.schedule if ddp else None,
+                    allreduce_dtype=a.allreduce_dtype)
     if a.schedule in ("concurrent", "serial"):
         eng.enable_timing()  # the segmented schedules, Adam(G) / Adam(D) apart
-    cpu = _cycles_per_us() if ddp else 0.0
+    cpu = _cycles_per_us() if ddp and a.fake_kind == "sleep" else 0.0
+    esize = 2 if a.allreduce_dtype == "bf16" else 4
     comm = {}
     if ddp:
         # collective call points of DDP on a comm stream; the update program is rebuilt for W=2
@@ -74,20 +107,24 @@ def main():
         eng._build_updates()
         eng._ensure_comm()
 
-        def fake(name, numel, us=None):
+        def fake(name, flat, us=None):
             if us is None:
-                us = ring_us(numel, a.fake_busbw_gbs, a.fake_lat_us, a.fake_world) if a.fake_busbw_gbs > 0 else 0.0
+                us = (ring_us(flat.numel(), a.fake_busbw_gbs, a.fake_lat_us, a.fake_world, esize)
+                      if a.fake_busbw_gbs > 0 else 0.0)
             comm[name] = round(us, 1)
-            return FakeReducer(us, cpu, numel)
+            return FakeReducer(us, flat, a.fake_world, esize, a.fake_nwg, a.fake_kind, cpu)
 
         gd, gg = eng.grad_d.flat, eng.grad_g.flat
         o = eng._d_top_off
         us3 = [float(x) for x in a.fake_comm_us.split(",")] if a.fake_comm_us else [None] * 3
-        eng._ar_g = fake("g", gg.numel(), us3[0])
-        eng._ar_dtop = fake("dtop", gd.numel() - o, us3[1])
-        eng._ar_drest = fake("drest", o, us3[2])
+        eng._ar_g = fake("g", gg, us3[0])
+        eng._ar_dtop = fake("dtop", gd[o:], us3[1])
+        eng._ar_drest = fake("drest", gd[:o], us3[2])
         if a.schedule == "ddp":
-            eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), hi - lo) for _, lo, hi in eng._g_cuts]
+            eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), gg[lo:hi]) for _, lo, hi in eng._g_cuts]
+        for name, r in list(vars(eng).items()):  # split G buckets of the segmented schedules
+            if name.startswith("_ar_gsplit") and isinstance(r, D.GradAllReducer):
+                setattr(eng, name, fake(name[4:], r.flat))
     eng.set_synthetic_batch(torch.rand(a.batch_size, 64, 64, 3, device=dev) * 2 - 1)
     for _ in range(a.warmup):
         eng.train_step()
@@ -103,7 +140,9 @@ def main():
         eng.train_step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.steps
-    print(json.dumps({"schedule": eng._schedule(), "graph": eng.graph_enabled, "fake_comm_us": comm,
+    print(json.dumps({"schedule": eng._schedule(), "graph": eng.graph_enabled, "fake_kind": a.fake_kind,
+                      "fake_world": a.fake_world, "fake_busbw_gbs": a.fake_busbw_gbs, "wire": a.allreduce_dtype,
+                      "fake_comm_us": comm,
                       "ms_per_step_timed": round(ms, 4), "phases_ms": {k: round(v, 4) for k, v in acc.items()}}))
 
 

@@ -2,8 +2,8 @@
 
 The step (``image_train.py:151-158`` semantics) is recorded ONCE into
 native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buffers, then
-replayed every step -- captured into hipGraphs so a step is one (single process) or six (DDP)
-graph launches:
+replayed every step -- captured into hipGraphs so a step is one (single process) or seven
+(DDP) graph launches:
 
   progA[:a_fwd]  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
                  2B batch [real | fake] with per-half BN statistics (= the reference's two
@@ -23,11 +23,14 @@ Schedules (``_schedule``), all covered by the stream-hazard checker
 (``engine/schedule_check.py``) and by GPU bit-exactness tests:
   "fused"       single process: ONE hipGraph; the two backward chains on two streams; ONE
                 Adam launch for both models after the join (16-bit dtypes)
-  "concurrent"  DDP (default) and the per-phase timed step: the two chains cut into 6 graph
+  "concurrent"  DDP (default) and the per-phase timed step: the two chains cut into 7 graph
                 segments, the collectives issued between them from the host on a comm stream --
                 D's top layer + head (76 % of D's gradient bytes at 64x64) as soon as the D chain
-                has produced it, the rest of D's when the D chain ends, G's gradients when the G
-                chain ends; Adam(D) runs under G's all-reduce
+                has produced it; G's lowest deconv (64 % of G's bytes) as soon as its weight
+                gradient exists (``_g_split_plan``: the G chain computes it right after its input
+                gradient, the rest of G's backward follows as "G_tail"); the rest of D's when the
+                D chain ends, the rest of G's when the G tail ends; Adam(D) runs under G's last
+                all-reduce
   "ddp"         DCGAN_DDP_SCHEDULE=ddp (RCCL): the fused schedule with the gradient all-reduces on
                 the comm stream INSIDE the same single hipGraph (RCCL collectives are captured);
                 G's gradients go out in per-layer buckets as G's weight gradients land
@@ -285,6 +288,7 @@ class HipEngine:
         # and the head, which the ParamSet lays out last
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
         self._g_cuts = self._g_bucket_cuts()
+        self._g_split = self._g_split_plan()
         self.progCast = self._prog()  # fp32 masters -> 16-bit mirrors (init / checkpoint load)
         if not self.f32:
             for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
@@ -669,6 +673,25 @@ class HipEngine:
         cuts.append((len(self._g_w_layer), 0, hi))
         return cuts
 
+    def _g_split_plan(self):
+        """Where the segmented ("concurrent") DDP schedule splits G's gradient all-reduce: G's
+        lowest deconv (g_h1 at 64x64: 13.1 of G's 20.5 MB) has its weight gradient computed as
+        soon as its input gradient exists -- progA up to the position that piece needs, then the
+        piece itself -- and its slice [lo, hi) (weights, bias, BN parameters) goes on the wire
+        while the rest of G's backward (the g_h1 data gradient, g_bn0, the projection and the
+        other layers' weight gradients) runs. Returns (a_need, w_begin, w_end, lo, hi) or None
+        (one G all-reduce after the chain)."""
+        if len(self.gl) < 2 or self.gl[0].name not in self._g_w_layer:
+            return None
+        k = self._g_w_layer.index(self.gl[0].name)
+        a_need, w_end = self._g_w[k]
+        w_begin = self._g_w[k - 1][1] if k > 0 else 0
+        if w_end <= w_begin or a_need <= self._a_fwd:
+            return None
+        offs = self.model.g.offsets
+        lo, hi = offs[self.gl[0].name + "/w"][0], offs[self.gl[1].name + "/w"][0]
+        return a_need, w_begin, w_end, lo, hi
+
     def _w_mark(self, prog, progw, begin: int, layer: str) -> None:
         """progW[begin:] (`layer`'s weight gradient) needs progA up to its current end."""
         if progw.size() > begin:
@@ -998,9 +1021,16 @@ class HipEngine:
             return [("fwd+G_bwd", [(A, 0, -1), (W, 0, -1)], M), ("D_bwd_top", [(B, 0, self._b_split)], M),
                     ("D_bwd_rest", [(B, self._b_split, -1)], M), ("adam_G", [(C, 0, self._c_split)], M),
                     ("adam_D", [(C, self._c_split, -1)], M)]
+        sp = self._g_split
+        if sp is None:
+            g_chain, g_tail = [(A, self._a_fwd, -1), (W, 0, -1)], []
+        else:  # G's lowest deconv weight gradient ends the chain; the rest of G's backward follows
+            a_need, wb, we = sp[:3]
+            g_chain = [(A, self._a_fwd, a_need), (W, wb, we)]
+            g_tail = [(A, a_need, -1), (W, 0, wb), (W, we, -1)]
         return [("fwd", [(A, 0, self._a_fwd)], M), ("D_bwd_top", [(B, 0, self._b_split)], self.ALT),
-                ("G_chain", [(A, self._a_fwd, -1), (W, 0, -1)], M), ("D_bwd_rest", [(B, self._b_split, -1)], self.ALT),
-                ("adam_D", [(C, 0, self._c_split)], M), ("adam_G", [(C, self._c_split, -1)], M)]
+                ("G_chain", g_chain, M), ("D_bwd_rest", [(B, self._b_split, -1)], self.ALT),
+                ("G_tail", g_tail, M), ("adam_D", [(C, 0, self._c_split)], M), ("adam_G", [(C, self._c_split, -1)], M)]
 
     def enable_timing(self) -> None:
         """Per-phase GPU timers: the step runs as segments with events between
@@ -1149,23 +1179,30 @@ class HipEngine:
             self._seg(ex, 1, alt)              # D chain: head + top layer gradients
             self._tick(2, alt)
             self._ar_launch(ex, "dtop", alt)
-            self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward -> grad_g final
+            self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward to g_h1's wgrad
             self._tick(3, cs)
+            if self._g_split is not None:
+                self._ar_launch(ex, "gsplit_a", cs)  # g_h1's slice, under the rest of both chains
             self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
-            # the D chain ends first: D's last bucket goes on the wire before G's, and Adam(D)
-            # runs while G's all-reduce is in flight
+            self._seg(ex, 4, cs)               # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
+            self._tick(5, cs)
+            # D's last bucket, then the rest of G's; Adam(D) runs while G's is in flight
             self._ar_launch(ex, "drest", alt)
             d_done = ex.mark(ex.comm) if self.ddp else None
-            self._ar_launch(ex, "g", cs)
+            if self._g_split is not None:
+                self._ar_launch(ex, "gsplit_b", cs)
+                self._ar_launch(ex, "gsplit_c", cs)
+            else:
+                self._ar_launch(ex, "g", cs)
             if d_done is not None:
-                ex.wait_mark(cs, d_done)       # dtop + drest collectives
+                ex.wait_mark(cs, d_done)       # dtop + drest (and g_h1's) collectives
             ex.wait(cs, alt)                   # (W = 1, timed: the D chain itself)
-            self._seg(ex, 4, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
-            self._tick(5, cs)
-            self._ar_join(ex, cs)              # G's collective
-            self._seg(ex, 5, cs)               # Adam G, step counter, G mirror
+            self._seg(ex, 5, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
             self._tick(6, cs)
+            self._ar_join(ex, cs)              # G's collectives
+            self._seg(ex, 6, cs)               # Adam G, step counter, G mirror
+            self._tick(7, cs)
             return
         self._tick(0, cs)
         self._seg(ex, 0, cs)                   # fwd, g_loss chain through D(fake), G backward -> grad_g final
@@ -1191,6 +1228,12 @@ class HipEngine:
             o = self._d_top_off
             cs, mb, wd = self.comm_stream, self.bucket_mb, self.allreduce_dtype
             self._ar_g = D.GradAllReducer(self.grad_g.flat, mb, wd, stream=cs, force=True)
+            if self._g_split is not None:  # "concurrent": g_h1's slice first, then the two others
+                lo, hi = self._g_split[3:]
+                gf = self.grad_g.flat
+                self._ar_gsplit_a = D.GradAllReducer(gf[lo:hi], mb, wd, stream=cs, force=True)
+                self._ar_gsplit_b = D.GradAllReducer(gf[hi:], mb, wd, stream=cs, force=True)
+                self._ar_gsplit_c = D.GradAllReducer(gf[:lo], mb, wd, stream=cs, force=True)
             self._ar_dtop = D.GradAllReducer(self.grad_d.flat[o:], mb, wd, stream=cs, force=True)
             self._ar_drest = D.GradAllReducer(self.grad_d.flat[:o], mb, wd, stream=cs, force=True)
             # "ddp": G's gradient in per-layer buckets (see _g_bucket_cuts)

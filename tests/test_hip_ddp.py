@@ -67,7 +67,7 @@ def _worker(rank, world, port, graph, out_dir, schedule="concurrent"):
                                             (False, "ddp")])
 def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
     """The DDP schedules over two ranks: "concurrent" (D chain and G chain on separate streams,
-    6 graph segments, collectives issued from both chains), "serial" (DCGAN_SERIAL_DBWD=1) and
+    7 graph segments, collectives issued from both chains), "serial" (DCGAN_SERIAL_DBWD=1) and
     "ddp" (the one-graph RCCL schedule with per-layer G buckets, run eagerly under gloo)."""
     ctx = mp.get_context("spawn")
     port = _free_port()
@@ -88,6 +88,63 @@ def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
     assert torch.equal(r0["g"], g), (r0["g"] - g).abs().max()
 
 
+def _real(rank):
+    return torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(100 + rank)) * 2 - 1
+
+
+def _one_step_grads(world, rank, graph):
+    """One training step with rank-specific data and rank-seeded z; returns the gradient buffers
+    after the step (after the all-reduce at W > 1: the SUM over ranks, Adam applies the 1/W)."""
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+    dev = torch.device("cuda", 0)
+    eng = HipEngine(DCGANConfig(output_size=64, c_dim=3), B, dev, seed=3, rank=rank, world=world, graph=graph,
+                    rank_seeded_z=True)
+    eng.set_batch(_real(rank).to(dev))
+    eng.train_step()
+    torch.cuda.synchronize()
+    return eng.grad_d.flat.cpu().clone(), eng.grad_g.flat.cpu().clone(), eng.model.d.flat.cpu(), eng.model.g.flat.cpu()
+
+
+def _grad_worker(rank, world, port, graph, out_dir, schedule):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DCGAN_DIST_BACKEND"] = "gloo"
+    os.environ["DCGAN_DDP_SCHEDULE"] = schedule
+    torch.cuda.set_device(0)
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    D.init_distributed(world, rank, torch.device("cuda", 0))
+    gd, gg, d, g = _one_step_grads(world, rank, graph)
+    torch.save({"gd": gd, "gg": gg, "d": d, "g": g}, os.path.join(out_dir, "g%d.pt" % rank))
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.mark.parametrize("graph,schedule", [(True, "concurrent"), (False, "ddp")])
+def test_hip_ddp_different_rank_batches_sum_gradients(tmp_path, graph, schedule):
+    """Two ranks with DIFFERENT real batches and z: the all-reduced gradient in every slice (D's
+    top layer + head, the rest of D, every G layer) equals the sum of the two single-process
+    engines' gradients on the same per-rank inputs, bit for bit (a two-term fp32 sum is exact in
+    either order), and both ranks hold the same weights after the update."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, graph, str(tmp_path), schedule)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0, "rank exited with %s" % p.exitcode
+    r0 = torch.load(tmp_path / "g0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "g1.pt", weights_only=True)
+    assert torch.equal(r0["d"], r1["d"]) and torch.equal(r0["g"], r1["g"])
+    assert torch.equal(r0["gd"], r1["gd"]) and torch.equal(r0["gg"], r1["gg"])
+    a = _one_step_grads(1, 0, graph)
+    b = _one_step_grads(1, 1, graph)
+    assert not torch.equal(a[0], b[0]) and not torch.equal(a[1], b[1]), "per-rank inputs must differ"
+    assert torch.equal(r0["gd"], a[0] + b[0]), (r0["gd"] - (a[0] + b[0])).abs().max()
+    assert torch.equal(r0["gg"], a[1] + b[1]), (r0["gg"] - (a[1] + b[1])).abs().max()
+
+
 def test_timed_concurrent_schedule_matches_fused():
     """The per-phase timed step (6 concurrent graph segments, the DDP schedule at W=1) is the
     same computation as the single fused graph, bit for bit; phase ends are reported."""
@@ -99,7 +156,8 @@ def test_timed_concurrent_schedule_matches_fused():
     d1, g1, _ = _run(b)
     assert torch.equal(d0, d1) and torch.equal(g0, g1)
     pt = b.phase_times()
-    assert set(pt) == {"fwd@end", "D_bwd_top@end", "G_chain@end", "D_bwd_rest@end", "adam_G@end", "adam_D@end"}
+    assert set(pt) == {"fwd@end", "D_bwd_top@end", "G_chain@end", "D_bwd_rest@end", "G_tail@end", "adam_G@end",
+                       "adam_D@end"}
     assert all(v > 0 for v in pt.values())
 
 
@@ -148,7 +206,7 @@ def _rccl_worker(out_dir, graph, port, schedule):
 def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule):
     """The REAL collective path on a one-GPU box: a one-rank RCCL (backend "nccl") process group
     (DCGAN_FORCE_DDP=1). "ddp": the RCCL all-reduces captured INSIDE the step's single hipGraph
-    (per-layer G buckets); "concurrent": issued on the comm stream between 6 graph segments.
+    (per-layer G buckets); "concurrent": issued on the comm stream between 7 graph segments.
     Both bit-identical to the fused single-graph step."""
     ctx = mp.get_context("spawn")
     p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port(), schedule))
@@ -158,7 +216,7 @@ def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule):
     r = torch.load(tmp_path / "rccl.pt", weights_only=True)
     assert r["backend"] == "nccl" and r["world"] == 1 and r["step"] == STEPS and r["graph"] == graph
     if graph:
-        assert r["graphs"] == (1 if schedule == "ddp" else 6)
+        assert r["graphs"] == (1 if schedule == "ddp" else 7)
     eng = _make(1, 0, True)
     assert not eng.ddp and eng._schedule() == "fused"
     d, g, _ = _run(eng)
@@ -180,5 +238,5 @@ def test_bench_force_ddp_reports_rccl():
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
-    assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 6
+    assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 7
     assert res["n_gpus"] == 1 and res["value"] > 0

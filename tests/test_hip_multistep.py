@@ -183,7 +183,8 @@ def test_generator_learns_flat_colour_images(tmp_path):
     are much flatter (mean per-image spatial std under 0.5x the untrained sampler's; measured
     0.99 -> 0.36 after 600 steps, with D winning by then) and inside the data's intensity range
     (|mean| < 0.7; a GAN may favour one of the two modes, so the mean is not pinned to the data
-    mean). 600 steps."""
+    mean), and at least 80 % of the sampled images have a mean grey level near a data mode
+    (|per-image mean| >= 0.3), which a generator collapsed to constant grey fails. 600 steps."""
     from distributed_tensorflow_for_dcgan_amd.data import pipeline as PL
     from distributed_tensorflow_for_dcgan_amd.data import tfrecord as TR
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
@@ -207,7 +208,12 @@ def test_generator_learns_flat_colour_images(tmp_path):
         x = eng.sampler(z).float()
         return float(x.mean()), float(x.flatten(1).std(1).mean())
 
+    def near_mode():  # fraction of sampled images whose mean grey level sits near a data mode (+-0.6)
+        x = eng.sampler(z).float()
+        return float((x.flatten(1).mean(1).abs() >= 0.3).float().mean())
+
     m0, s0 = sample_stats()
+    f0 = near_mode()
     try:
         for _ in range(600):
             eng.set_batch(src.next())
@@ -216,8 +222,12 @@ def test_generator_learns_flat_colour_images(tmp_path):
     finally:
         src.close()
     m1, s1 = sample_stats()
-    print("\nsampler before: mean %.3f spatial std %.3f; after 600 steps: mean %.3f spatial std %.3f; losses %s"
-          % (m0, s0, m1, s1, eng.last_losses()))
+    f1 = near_mode()
+    print("\nsampler before: mean %.3f spatial std %.3f near-mode %.2f; after 600 steps: mean %.3f spatial std %.3f "
+          "near-mode %.2f; losses %s" % (m0, s0, f0, m1, s1, f1, eng.last_losses()))
     assert all(math.isfinite(v) for v in eng.last_losses().values())
     assert s1 < 0.5 * s0, (s0, s1)
     assert abs(m1) < 0.7, m1
+    # a generator collapsed to a constant grey (mean ~0) passes the two checks above; the data
+    # are two modes at +-0.6, so most samples must sit near one of them
+    assert f1 >= 0.8, (f0, f1)

@@ -57,8 +57,9 @@ def test_checker_finds_the_round1_adam_race():
         eng._seg(ex, 2, cs)
         eng._seg(ex, 3, alt)
         eng._seg(ex, 4, cs)
-        ex.wait(cs, alt)
         eng._seg(ex, 5, cs)
+        ex.wait(cs, alt)
+        eng._seg(ex, 6, cs)
 
     eng._run_step = round1_order
     hz, _ = SC.check_engine(eng)
