@@ -50,8 +50,6 @@ def shapes(cfg: DCGANConfig, B: int):
 
 
 V1 = False  # --v1: also time the first-generation igemm.hip tiles
-IG5 = True  # --no-ig5: leave out igemm5.hip
-IG3 = True  # --no-ig3: leave out igemm3.hip
 
 
 def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
@@ -69,20 +67,6 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     phases = 4 if mode == 1 else 1
     M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
     kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
-    if mode in (0, 1) and IG5:  # igemm5: ping-pong wave groups (conv / deconv, N % 4 == 0)
-        for c in range(400, 420):
-            if c % 10 not in H.IGEMM5_TILES or H.igemm5_lds(c) > 160 * 1024:
-                continue
-            bm, bn = H.IGEMM5_TILES[c % 10]
-            if bn > N:
-                continue
-            tiles = -(-M // bm) * -(-N // bn) * phases
-            for sp in (1, 2, 3, 4, 6, 8):
-                if sp > 1 and (kt // sp < 3 or tiles * sp > 2048 or tiles >= 512):
-                    continue
-                out.append((c, sp))
-    if not IG3:
-        return out
     for c in range(200, 240):
         if c % 10 not in H.IGEMM3_TILES or H.igemm3_lds(c) > 160 * 1024:
             continue
@@ -116,16 +100,12 @@ def main():
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--only", default="")
     ap.add_argument("--v1", action="store_true", help="also time igemm.hip (v1) tiles")
-    ap.add_argument("--no-ig5", action="store_true", help="leave out igemm5.hip tiles")
-    ap.add_argument("--no-ig3", action="store_true", help="leave out igemm3.hip tiles")
     ap.add_argument("--out", default="", help="also write this run's table (JSON) here")
     ap.add_argument("--top", type=int, default=6, help="candidates listed per shape")
     ap.add_argument("--cfgs", default="", help="comma-separated cfg prefix filter, e.g. 4,21")
     a = ap.parse_args()
-    global V1, IG5, IG3
+    global V1
     V1 = a.v1
-    IG5 = not a.no_ig5
-    IG3 = not a.no_ig3
     cfg = DCGANConfig(output_size=a.size)
     ext = H.ext()
     dev = torch.device("cuda", 0)

@@ -191,15 +191,11 @@ class Program {
                uintptr_t bnb_x = 0, uintptr_t bnb_y = 0, uintptr_t bnb_mean = 0, uintptr_t bnb_rstd = 0,
                int bnb_rpg = 0, int bnb_act = 0, float bnb_leak = 0.f, int bnb_store_g = 0) {
     int bm = 0, bn = 0, ns = 0;
-    const bool v5 = cfg >= 400;  // igemm5.hip: ping-pong wave groups, register epilogue
-    const bool v3 = cfg >= 200 && !v5;
-    if (cfg >= 420) throw std::runtime_error("bad igemm cfg " + std::to_string(cfg));
-    if (v5 ? KF(dcg_igemm5_tile)(cfg, &bm, &bn, &ns)
-           : v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
+    const bool v3 = cfg >= 200;
+    if (cfg >= 400) throw std::runtime_error("bad igemm cfg " + std::to_string(cfg));
+    if (v3 ? KF(dcg_igemm3_tile)(cfg, &bm, &bn, &ns) : KF(dcg_igemm_tile)(cfg, &bm, &bn))
       throw std::runtime_error("bad igemm cfg " + std::to_string(cfg) + " for this element type");
-    if (v5 && (mode == 2 || N % 4 || ldc % 4 || cofs % 4))
-      throw std::runtime_error("igemm5: conv / deconv with 4-channel output groups only");
-    if (!v3 && !v5 && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
+    if (!v3 && (bkn || splits != 1)) throw std::runtime_error("igemm cfg < 200 supports neither bkn nor split-K");
     if (splits < 1) throw std::runtime_error("splits must be >= 1");
     const int kal = (int)(16 / es_);  // 16-byte A rows
     if (Kc % kal) throw std::runtime_error("igemm needs 16-byte A rows (Kc % " + std::to_string(kal) + " == 0)");
@@ -286,26 +282,7 @@ class Program {
     acc.r(A, a_elems * es_).r(Bw, b_elems * es_).r(bias, (size_t)N * 4)
         .w(C, (c_rows - 1) * ldc * out_es + (size_t)(cofs + N) * out_es)
         .w(stats, (size_t)mtiles * a.nphases * 2 * N * 4);
-    if (bnb_x && v5) {  // register epilogue: no LDS C tile; only the BN-group alignment matters
-      if (out_f32) throw std::runtime_error("igemm5 bnb: elem_t output only");
-      const size_t xy_bytes = (c_rows - 1) * ldc * es_ + (size_t)(cofs + N) * es_;
-      if (bnb_store_g) {
-        if (!stats || !bnb_y) throw std::runtime_error("igemm act-backward store: needs stats and y");
-        a.bnb_x = P<const elem_t>(bnb_y); a.bnb_y = P<const elem_t>(bnb_y);
-        a.bnb_rpg = 1 << 30; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak; a.bnb_store_g = 1;
-        acc.r(bnb_y, xy_bytes);
-      } else {
-        if (!stats || bnb_rpg <= 0 || !bnb_y || !bnb_mean || !bnb_rstd)
-          throw std::runtime_error("igemm bnb: needs stats, rows-per-group, y, mean, rstd");
-        for (auto& q : ph)
-          if (bnb_rpg % bm || q.M % bnb_rpg) throw std::runtime_error("igemm bnb: tile rows must divide the group");
-        a.bnb_x = P<const elem_t>(bnb_x); a.bnb_y = P<const elem_t>(bnb_y);
-        a.bnb_mean = P<const float>(bnb_mean); a.bnb_rstd = P<const float>(bnb_rstd);
-        a.bnb_rpg = bnb_rpg; a.bnb_act = bnb_act; a.bnb_leak = bnb_leak;
-        const size_t groups = (size_t)(maxM / bnb_rpg);
-        acc.r(bnb_x, xy_bytes).r(bnb_y, xy_bytes).r(bnb_mean, groups * N * 4).r(bnb_rstd, groups * N * 4);
-      }
-    } else if (bnb_x) {
+    if (bnb_x) {
       const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
       const size_t nt = v3 ? (size_t)KF(dcg_igemm3_threads)(cfg) : 256;
@@ -349,9 +326,6 @@ class Program {
       acc.w((uintptr_t)a.ws, tiles * splits * (size_t)bm * bn * sizeof(float)).w((uintptr_t)a.counters, tiles * 4);
     }
     const unsigned blocks = (unsigned)(tiles * splits);
-    if (v5)
-      return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm5_launch)(&a, cfg, bkn, blocks, s); },
-                 acc.v);
     return add(name, stream, [this, a, cfg, bkn, blocks](hipStream_t s) { return KF(dcg_igemm3_launch)(&a, cfg, bkn, blocks, s); },
                acc.v);
   }
@@ -938,8 +912,7 @@ static py::tuple igemm_tile(int cfg, int dtype) {
   int bm = 0, bn = 0, ns = 0;
   int rc;
 #define DT(fn) (dtype == 2 ? fn##_f32 : dtype == 1 ? fn##_f16 : fn)
-  if (cfg >= 420) rc = -1;
-  else if (cfg >= 400) rc = DT(dcg_igemm5_tile)(cfg, &bm, &bn, &ns);
+  if (cfg >= 400) rc = -1;
   else if (cfg >= 200) rc = DT(dcg_igemm3_tile)(cfg, &bm, &bn, &ns);
   else rc = DT(dcg_igemm_tile)(cfg, &bm, &bn);
 #undef DT

@@ -435,8 +435,6 @@ extern "C" int DCG_API(dcg_wgrad_launch)(const dcg::WGradArgs* a, int cfg, int s
 extern "C" int DCG_API(dcg_igemm_tile)(int, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_igemm_launch)(const dcg::IGemmArgs*, int, int, int, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_igemm3_threads)(int) { return 256; }
-extern "C" int DCG_API(dcg_igemm5_tile)(int, int*, int*, int*) { return -1; }
-extern "C" int DCG_API(dcg_igemm5_launch)(const dcg::IGemmArgs*, int, int, unsigned, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_wgrad3_tile)(int, int*, int*, int*) { return -1; }
 extern "C" int DCG_API(dcg_wgrad3_launch)(const dcg::WGrad3Args*, int, hipStream_t) { return -2; }
 extern "C" int DCG_API(dcg_narrow_deconv)(const elem_t*, const elem_t*, const float*, elem_t*, int, int, int, int, int,

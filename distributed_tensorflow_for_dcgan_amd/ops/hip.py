@@ -81,28 +81,15 @@ def igemm3_lds(cfg: int) -> int:
     return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
 
 
-# igemm5.hip (two ping-pong wave groups, 3-4 stage ring, register epilogue): cfg 400 + 10k + id,
-# ring depth NS = (3, 4)[k]; tile id -> workgroup tile (2 GM) x BN on 8 waves
-IGEMM5_TILES = {0: (256, 128), 1: (256, 64), 2: (128, 128), 3: (128, 64)}
-IGEMM5_STAGES = (3, 4)
-
-
-def igemm5_lds(cfg: int) -> int:
-    bm, bn = IGEMM5_TILES[cfg % 10]
-    return IGEMM5_STAGES[(cfg - 400) // 10] * (bm + bn) * 128
-
-
 # fp32 build (igemm_f32.hip): the only tile family of that element type, cfg 200..203
 IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)}
 
 
 def tile_of(cfg: int, dtype: int = 0) -> Tuple[int, int]:
-    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..239 igemm3.hip, 400..419
-    igemm5.hip; dtype 2 (fp32): igemm_f32.hip."""
+    """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..239 igemm3.hip; dtype 2
+    (fp32): igemm_f32.hip."""
     if dtype == 2:
         return IGEMM_F32_TILES[cfg]
-    if cfg >= 400:
-        return IGEMM5_TILES[cfg % 10]
     if cfg >= 200:
         return IGEMM3_TILES[cfg % 10]
     return IGEMM_CFGS[cfg % 100]
@@ -126,8 +113,6 @@ def pick_igemm_f32(M: int, N: int, phases: int = 1, rows_per_group: Optional[int
 
 def bnb_fits(cfg: int) -> bool:
     """True when the tile's LDS can hold the fused BN-backward statistics scratch (epilogue.h)."""
-    if cfg >= 400:  # igemm5: register epilogue, no C tile in LDS
-        return True
     bm, bn = tile_of(cfg)
     if cfg < 200:
         return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= 2 * (bm + bn) * 128
@@ -199,7 +184,7 @@ TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "igemm_tun
 def tuned_table() -> dict:
     """Per-layer tile choices measured on MI355X by ``benchmarks/bench_kernels.py --write``
     (key ``mode,Bn,Hin,Win,Kc,Hout,Wout,N`` -> "cfg:splits" (or a bare cfg): cfg < 200 is
-    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip, 400..419 igemm5.hip)."""
+    igemm.hip (+100 = LDS-DMA staging), 200..239 igemm3.hip)."""
     global _TUNED
     if _TUNED is None:
         _TUNED = {}

@@ -218,112 +218,6 @@ def test_igemm_fused_bn_backward_stats(cfg):
     close(s[1], (g * xh).reshape(-1, Co).sum(0), 2e-3, "sum g xhat cfg%d" % cfg)
 
 
-IG5 = [400, 401, 402, 403, 411, 412, 413]  # 40x: 3-stage ring, 41x: 4 stages (tiles that fit 160 KiB)
-
-
-@pytest.mark.parametrize("B,Hs,Ci,Co", [(4, 16, 128, 256), (2, 32, 64, 128), (8, 8, 256, 512), (3, 7, 64, 64)])
-@pytest.mark.parametrize("bkn", [0, 1])
-def test_igemm5_conv_tiles_layouts_splits(B, Hs, Ci, Co, bkn):
-    """igemm5.hip (ping-pong wave groups, 3/4-stage ring, register epilogue): stride-2 SAME conv
-    with bias + lrelu + BN statistics for every tile, both weight layouts, split-K 1/3 (in-kernel
-    reduction, bitwise reproducible); odd sizes leave partial row tiles."""
-    h = H()
-    x = bf(rnd(B, Hs, Hs, Ci, seed=90))
-    w = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=91))          # HWIO = [25][Ci][Co] = bkn layout
-    bias = rnd(Co, scale=0.1, seed=92)
-    ref_pre = R.conv2d_same(x.float(), w.float(), bias)
-    wp = w.reshape(25, Ci, Co).contiguous() if bkn else h.pack_conv_weight(w.float(), "conv", "fwd")
-    for cfg in IG5:
-        if h.IGEMM5_TILES[cfg % 10][1] > Co:
-            continue
-        for splits in (1, 3):
-            y, st = h.conv2d_same(x, wp, Co, bias=bias, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn), splits=splits)
-            tag = "igemm5 cfg%d bkn%d s%d" % (cfg, bkn, splits)
-            close(y, R.lrelu(ref_pre), 1.5e-2, tag)
-            s = st.sum(0)
-            close(s[0], ref_pre.reshape(-1, Co).sum(0), 2e-3, "sum " + tag)
-            close(s[1], ref_pre.reshape(-1, Co).pow(2).sum(0), 2e-3, "sumsq " + tag)
-            y2, st2 = h.conv2d_same(x, wp, Co, bias=bias, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn),
-                                    splits=splits)
-            assert torch.equal(y, y2) and torch.equal(st, st2), "nondeterministic " + tag
-
-
-@pytest.mark.parametrize("B,Hi,Ho,Ci,Co", [(8, 4, 8, 512, 256), (2, 8, 16, 256, 128), (2, 16, 32, 128, 64),
-                                          (2, 4, 7, 64, 64)])
-def test_igemm5_deconv_and_g_dgrad(B, Hi, Ho, Ci, Co):
-    """igemm5 conv_transpose (4 sub-pixel phases; fp32 output and bias, split-K 1/2) and the G data
-    gradient (conv with the k-major deconv weight)."""
-    h = H()
-    x = bf(rnd(B, Hi, Hi, Ci, seed=93))
-    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=94))  # [5,5,out,in] = [25][N][Kc]
-    bias = rnd(Co, scale=0.1, seed=95)
-    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
-    for cfg in IG5:
-        if h.IGEMM5_TILES[cfg % 10][1] > Co:
-            continue
-        for splits in (1, 2):
-            y, st = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True,
-                                            stats=True, cfg=cfg, splits=splits)
-            close(y, ref, 2e-3, "igemm5 deconv cfg%d s%d" % (cfg, splits))
-            close(st.sum(0)[0], ref.reshape(-1, Co).sum(0), 3e-3, "igemm5 deconv stats cfg%d s%d" % (cfg, splits))
-    xd = rnd(B, Hi, Hi, Ci, seed=96).requires_grad_(True)
-    yd = R.conv2d_transpose_same(xd, w.float(), (Ho, Ho))
-    dy = bf(rnd(B, Ho, Ho, Co, seed=97))
-    (gx,) = torch.autograd.grad(yd, xd, dy.float())
-    for cfg in IG5:
-        if h.IGEMM5_TILES[cfg % 10][1] > Ci:
-            continue
-        out = h.conv2d_same(dy, w.reshape(25, Co, Ci), Ci, out_f32=True, cfg=cfg, bkn=True)
-        close(out, gx, 2e-3, "igemm5 G dgrad cfg%d" % cfg)
-
-
-@pytest.mark.parametrize("store_g", [0, 1])
-def test_igemm5_fused_bn_backward_stats(store_g):
-    """igemm5 data-gradient GEMM with the BN-backward (or activation-backward) statistics in its
-    register epilogue: the stored tensor and the partial sums vs the fp32 reference."""
-    h = H()
-    B, Hi, Ci, Co = 4, 16, 128, 64
-    Ho = 2 * Hi
-    dy = bf(rnd(B, Hi, Hi, Ci, seed=60))
-    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=61)).reshape(25, Co, Ci).contiguous()
-    x = bf(rnd(B, Ho, Ho, Co, seed=62))
-    y = bf(rnd(B, Ho, Ho, Co, seed=63) - 0.3)
-    mean = rnd(1, Co, scale=0.2, seed=64)
-    rstd = rnd(1, Co, seed=65).abs() + 0.5
-    da_ref = R.conv2d_transpose_same(dy.float(), w.reshape(5, 5, Co, Ci).float(), (Ho, Ho))
-    mph = B * Hi * Hi
-    ran = 0
-    for cfg in IG5:
-        bm, bn = h.tile_of(cfg)
-        if mph % bm or bn > Co:
-            continue
-        ran += 1
-        da = torch.empty(B, Ho, Ho, Co, device=dev, dtype=torch.bfloat16)
-        st = torch.empty(mph // bm * 4, 2, Co, device=dev)
-        prog = h.ext().Program()
-        if store_g:
-            prog.igemm_ex("actb", 1, h._p(dy), h._p(w), h._p(da), B, Hi, Hi, Ci, Ho, Ho, Co, 1, 1, cfg, 0, Co, 0, 0, 0,
-                          0.2, h._p(st), 0, 0, -1, 1, h._p(y), h._p(y), 0, 0, 0, 2, 0.2, 1)
-        else:
-            prog.igemm_ex("bnb", 1, h._p(dy), h._p(w), h._p(da), B, Hi, Hi, Ci, Ho, Ho, Co, 1, 1, cfg, 0, Co, 0, 0, 0,
-                          0.2, h._p(st), 0, 0, -1, 1, h._p(x), h._p(y), h._p(mean), h._p(rstd), mph, 2, 0.2, 0)
-        h.run(prog)
-        torch.cuda.synchronize()
-        g = da_ref * torch.where(y.float() > 0, 1.0, 0.2)
-        s = st.sum(0)
-        tag = "igemm5 cfg%d store_g%d" % (cfg, store_g)
-        if store_g:
-            close(da, g, 1e-2, "g " + tag)
-            close(s[0], g.reshape(-1, Co).sum(0), 3e-3, "sum g " + tag)
-        else:
-            close(da, da_ref, 1e-2, "da " + tag)
-            gs = da.float() * torch.where(y.float() > 0, 1.0, 0.2)
-            xh = (x.float() - mean.reshape(Co)) * rstd.reshape(Co)
-            close(s[0], gs.reshape(-1, Co).sum(0), 2e-3, "sum g " + tag)
-            close(s[1], (gs * xh).reshape(-1, Co).sum(0), 2e-3, "sum g xhat " + tag)
-    assert ran
-
-
 def test_igemm3_plain_im2col_bkn():
     """3-channel layers: im2col rows [M][80] x the natural weight [75][N] (rows 75..79 -> 0)."""
     h = H()
