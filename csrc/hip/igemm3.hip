@@ -63,6 +63,15 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
+// vmcnt(n * L) for a runtime n in [0, NMAX]
+template <int L, int NMAX>
+__device__ __forceinline__ void wait_vmcnt_n(int n) {
+  if constexpr (NMAX >= 3) { if (n >= 3) { wait_vmcnt<3 * L>(); return; } }
+  if constexpr (NMAX >= 2) { if (n >= 2) { wait_vmcnt<2 * L>(); return; } }
+  if constexpr (NMAX >= 1) { if (n >= 1) { wait_vmcnt<L>(); return; } }
+  wait_vmcnt<0>();
+}
+
 template <int BM, int BN, int WM, int WN, int BKN, int NS, int PL>
 __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   constexpr bool kStudy = DCG_IGEMM_STUDY != 0;
@@ -227,13 +236,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memtime();
   for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed for this wave; younger tiles (up to NS-2 of them) may stay in flight
-    if constexpr (NS >= 3) {
-      if (kt + 1 < nk) wait_vmcnt<LPT * (NS - 2)>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    // tile kt landed for this wave; the younger tiles issued so far (up to NS-2 of them) may stay
+    // in flight -- fewer near the end of the loop, where no new tile was issued (a fixed
+    // vmcnt(LPT * (NS-2)) would not cover tile nk-2 at NS >= 4)
+    wait_vmcnt_n<LPT, NS - 2>(min(NS - 2, nk - 1 - kt));
     // every wave's tile kt landed; every wave is done with slot (kt-1) % NS. A bare s_barrier:
     // __syncthreads() would add the workgroup release, i.e. a vmcnt(0) that also waits for the
     // younger DMA tiles and flattens the pipeline (LDS reads of the previous tile have all
