@@ -25,7 +25,9 @@ class FakeReducer:
     to the modelled ring time, so the collective takes CUs and HBM bandwidth from the compute it
     overlaps, as the real one does. ``kind="sleep"``: round 3's single-thread timer
     (``torch.cuda._sleep``: no CU or HBM footprint). Capturable: the "ddp" schedule records it
-    inside its graph."""
+    inside its graph. With a bf16 wire (esize 2) it also runs the real reducer's two cast copies
+    (fp32 gradient -> bf16 wire buffer before the collective, back after it:
+    parallel/dist.py GradAllReducer.issue), so the bf16 rows carry their full cost."""
 
     def __init__(self, us, flat=None, world=8, esize=4, nwg=32, kind="rccl", cycles_per_us=0.0):
         self.us = float(us)
@@ -36,27 +38,37 @@ class FakeReducer:
         self.nwg = int(nwg)
         self.bytes = (int(2.0 * (world - 1) / world * self.numel * esize) // 16) * 16
         self.prog = None
+        self.wire = (torch.empty(self.numel, device=flat.device, dtype=torch.bfloat16)
+                     if esize == 2 and flat is not None else None)
         if kind == "rccl" and self.bytes > 0 and flat is not None:
             from distributed_tensorflow_for_dcgan_amd.ops import hip as H
-            src_bytes = self.numel * flat.element_size()
+            payload = flat if self.wire is None else self.wire
+            src_bytes = self.numel * payload.element_size()
             # the wire moves up to 2x the payload: read it twice over when the slice is shorter
-            self.src = flat if src_bytes >= self.bytes else flat.repeat(-(-self.bytes // src_bytes))
+            self.src = payload if src_bytes >= self.bytes else payload.repeat(-(-self.bytes // src_bytes))
             self.dst = torch.empty(self.bytes // 4, device=flat.device, dtype=torch.float32)
             self.prog = H.ext().Program()
             self.prog.comm_emulate("comm_emu", self.src.data_ptr(), self.dst.data_ptr(), self.bytes, self.us,
                                    self.nwg, 0)
 
     def issue(self):  # on the comm stream (the engine's executor orders it after the producers)
+        if self.wire is not None:
+            self.wire.copy_(self.flat)
         if self.kind == "rccl" and self.prog is not None:
             from distributed_tensorflow_for_dcgan_amd.ops import hip as H
             H.run(self.prog)
         elif self.cycles > 0:
             torch.cuda._sleep(self.cycles)
+        if self.wire is not None:
+            self.flat.copy_(self.wire)
 
     def accesses(self):  # as the real reducer: the gradient slice is read and written
         if self.flat is None:
             return []
-        return [(self.flat.data_ptr(), self.numel * self.flat.element_size(), True)]
+        out = [(self.flat.data_ptr(), self.numel * self.flat.element_size(), True)]
+        if self.wire is not None:
+            out.append((self.wire.data_ptr(), self.numel * 2, True))
+        return out
 
 
 def _cycles_per_us():
