@@ -636,34 +636,6 @@ class Program {
                                 P<float>(stats), C, P<const unsigned long long>(gen_step), gen_seed, s);
     }, acc.v);
   }
-  // fused G head: z (Philox when gen_step) -> projection -> g_bn0 statistics + finalize (+EMA) ->
-  // apply + activation (misc.hip g_head_kernel). Throws when the shape does not fit the kernel.
-  int g_head(std::string name, uintptr_t z, uintptr_t W, uintptr_t b, uintptr_t x, uintptr_t y, int B, int K, int N,
-             int C, uintptr_t gen_step, uint64_t gen_seed, uintptr_t gamma, uintptr_t beta, float eps, uintptr_t mean,
-             uintptr_t rstd, uintptr_t scale, uintptr_t shift, uintptr_t ema_mean, uintptr_t ema_var, float decay,
-             int act, float leak, int stream) {
-    if (!g_head_fits(B, K, N, C)) throw std::runtime_error("g_head: shape does not fit the fused kernel");
-    AccList acc;
-    if (gen_step) acc.w(z, (size_t)B * K * 4).r(gen_step, 8);
-    else acc.r(z, (size_t)B * K * 4);
-    const size_t c4 = (size_t)C * 4;
-    acc.r(W, (size_t)K * N * 4).r(b, (size_t)N * 4).w(x, (size_t)B * N * es_).w(y, (size_t)B * N * es_)
-        .r(gamma, c4).r(beta, c4).w(mean, c4).w(rstd, c4).w(scale, c4).w(shift, c4).w(ema_mean, c4).w(ema_var, c4);
-    return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_g_head)(P<float>(z), P<const float>(W), P<const float>(b), P<elem_t>(x), P<elem_t>(y), B, K, N, C,
-                            P<const unsigned long long>(gen_step), gen_seed, P<const float>(gamma),
-                            P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
-                            P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, act, leak, s);
-    }, acc.v);
-  }
-  // the shape rule of dcg_g_head (CW = 2 channels per workgroup, z in <= 96 KiB of LDS)
-  static bool g_head_fits(int B, int K, int N, int C) {
-    if (C <= 0 || N % C || C % 2 || K <= 0) return false;
-    const int ncols = (N / C) * 2;
-    if (ncols > 256 || 256 % ncols) return false;
-    const int rpt = (B + 256 / ncols - 1) / (256 / ncols);
-    return rpt <= 32 && (size_t)B * K * 4 <= 96 * 1024;
-  }
   int linear_wgrad(std::string name, uintptr_t z, uintptr_t dh, uintptr_t dW, uintptr_t db, int B, int K, int N,
                    int stream) {
     return add(name, stream, [=](hipStream_t s) {
@@ -1022,8 +994,6 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("colsum_small", &Program::colsum_small)
       .def("gan_loss", &Program::gan_loss, py::arg("name"), py::arg("logits"), py::arg("B"), py::arg("out"),
            py::arg("dl_d"), py::arg("dl_g"), py::arg("prob"), py::arg("stream"), py::arg("ls") = 0)
-      .def("g_head", &Program::g_head)
-      .def_static("g_head_fits", &Program::g_head_fits)
       .def("linear_fwd", &Program::linear_fwd, py::arg("name"), py::arg("z"), py::arg("W"), py::arg("b"),
            py::arg("out"), py::arg("B"), py::arg("K"), py::arg("N"), py::arg("stream"), py::arg("stats") = 0,
            py::arg("C") = 0, py::arg("gen_step") = 0, py::arg("gen_seed") = 0)

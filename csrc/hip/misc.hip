@@ -171,151 +171,6 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(float* __restrict__ z, 
   }
 }
 
-// ---------------------------------------------------------------- fused G head
-// G's head stage in ONE launch (reference distriubted_model.py:88-95: z ->
-// linear -> reshape [B,4,4,C] -> batch norm -> relu): z (Philox, as linear_fwd), the projection,
-// the g_bn0 statistics, their finalize (+EMA), the BN apply and the activation. A workgroup owns
-// CW whole channels -- all S = N / C spatial positions of every batch row -- so its channels'
-// batch statistics never leave it: no partial rows, no finalize launch, no cross-workgroup
-// hand-off. Thread t: column q = t % (S * CW) (n = (q / CW) * C + c0 + q % CW), rows
-// (t / (S * CW)) * RPT + i. The pre-BN output x (bf16, what the BN backward reads), mean / rstd /
-// scale / shift and the EMA slots are written exactly as linear_fwd + bnfin_fwd + bn_apply_act
-// write them; the statistics are of the stored (rounded) x, summed in a fixed order (double).
-template <int CW, int RPT>
-__global__ __launch_bounds__(256) void g_head_kernel(float* __restrict__ z, const float* __restrict__ W,
-                                                     const float* __restrict__ bias, elem_t* __restrict__ xo,
-                                                     elem_t* __restrict__ yo, int B, int K, int N, int C,
-                                                     const unsigned long long* __restrict__ gen_step,
-                                                     uint64_t gen_seed, const float* __restrict__ gamma,
-                                                     const float* __restrict__ beta, float eps,
-                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     float* __restrict__ scale_out, float* __restrict__ shift_out,
-                                                     float* __restrict__ ema_mean, float* __restrict__ ema_var,
-                                                     float decay, int act, float leak) {
-  extern __shared__ __attribute__((aligned(16))) float zs[];  // [B][K]
-  __shared__ double red[2][256];
-  __shared__ float coef[2][CW];
-  const int tid = threadIdx.x;
-  const int S = N / C, ncols = S * CW;
-  const int c0 = blockIdx.x * CW;
-  // ---- z: 4 uniforms per Philox evaluation (bit-identical to philox_uniform_at / linear_fwd)
-  const int BK = B * K;
-  if (gen_step) {
-    const uint64_t st = gen_step[0];
-    for (int i4 = tid; 4 * i4 < BK; i4 += 256) {
-      uint32_t x0 = (uint32_t)i4, x1 = 0u, x2 = (uint32_t)st, x3 = (uint32_t)(st >> 32);
-      uint32_t k0 = (uint32_t)gen_seed, k1 = (uint32_t)(gen_seed >> 32);
-#pragma unroll
-      for (int r = 0; r < 10; ++r) {
-        philox_round(x0, x1, x2, x3, k0, k1);
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-      }
-      const uint32_t c4[4] = {x0, x1, x2, x3};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int idx = 4 * i4 + j;
-        if (idx < BK) {
-          const float v = -1.f + 2.f * ((float)(c4[j] >> 8) * (1.0f / 16777216.0f));
-          zs[idx] = v;
-          if (blockIdx.x == 0) z[idx] = v;
-        }
-      }
-    }
-  } else {
-    for (int i = tid; i < BK; i += 256) zs[i] = z[i];
-  }
-  __syncthreads();
-  // ---- projection: RPT rows x 1 column per thread (z rows broadcast from LDS)
-  const int q = tid % ncols, rg = tid / ncols;
-  const bool active = rg * RPT < B && q < ncols;
-  const int n = (q / CW) * C + c0 + q % CW;
-  const int r0 = rg * RPT;
-  float acc[RPT];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) acc[i] = 0.f;
-  if (active) {
-    constexpr int KU = 20;
-    int k = 0;
-    if ((K & 3) == 0) {
-      for (; k + KU <= K; k += KU) {
-        float w[KU];
-#pragma unroll
-        for (int u = 0; u < KU; ++u) w[u] = W[(size_t)(k + u) * N + n];
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-          const int r = min(r0 + i, B - 1);
-#pragma unroll
-          for (int u4 = 0; u4 < KU / 4; ++u4) {
-            const f32x4 zv = *reinterpret_cast<const f32x4*>(zs + r * K + k + 4 * u4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i] += zv[e] * w[4 * u4 + e];
-          }
-        }
-      }
-    }
-    for (; k < K; ++k) {
-      const float w = W[(size_t)k * N + n];
-#pragma unroll
-      for (int i = 0; i < RPT; ++i) acc[i] += zs[min(r0 + i, B - 1) * K + k] * w;
-    }
-  }
-  // ---- pre-BN output (rounded) and its per-thread sums
-  const float b = active ? (bias ? bias[n] : 0.f) : 0.f;
-  double s = 0.0, s2 = 0.0;
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const elem_t o = (elem_t)(acc[i] + b);
-    acc[i] = (float)o;
-    if (active && r0 + i < B) {
-      xo[(size_t)(r0 + i) * N + n] = o;
-      s += (double)acc[i];
-      s2 += (double)acc[i] * (double)acc[i];
-    }
-  }
-  red[0][tid] = s;
-  red[1][tid] = s2;
-  __syncthreads();
-  // fixed-order tree over the threads of one channel (t % CW); 256 / CW >= 2 entries each
-  for (int off = 128; off >= CW; off >>= 1) {
-    if (tid < off) {
-      red[0][tid] += red[0][tid + off];
-      red[1][tid] += red[1][tid + off];
-    }
-    __syncthreads();
-  }
-  if (tid < CW) {  // finalize (bnfin_fwd_kernel's arithmetic)
-    const int c = c0 + tid;
-    const double count = (double)B * S;
-    const double m = red[0][tid] / count;
-    double v = red[1][tid] / count - m * m;
-    if (v < 0.0) v = 0.0;
-    const float mf = (float)m, vf = (float)v;
-    const float r = rsqrtf(vf + eps);
-    mean_out[c] = mf;
-    rstd_out[c] = r;
-    const float sc = gamma[c] * r;
-    const float sh = beta[c] - mf * sc;
-    scale_out[c] = sc;
-    shift_out[c] = sh;
-    coef[0][tid] = sc;
-    coef[1][tid] = sh;
-    if (ema_mean) {
-      const float al = 1.f - decay;
-      ema_mean[c] -= al * (ema_mean[c] - mf);
-      ema_var[c] -= al * (ema_var[c] - vf);
-    }
-  }
-  __syncthreads();
-  // ---- BN apply + activation of the values still in registers
-  if (active) {
-    const float sc = coef[0][q % CW], sh = coef[1][q % CW];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i)
-      if (r0 + i < B) yo[(size_t)(r0 + i) * N + n] = (elem_t)apply_act(acc[i] * sc + sh, act, leak);
-  }
-}
-
 // dW[K][N] = z^T @ dh (fp32 out), db[N] = sum_b dh; block = 256 columns x KC k-rows
 template <int KC>  // KC % 4 == 0
 __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ z, const elem_t* __restrict__ dh,
@@ -967,40 +822,6 @@ extern "C" int DCG_API(dcg_linear_fwd)(float* z, const float* W, const float* b,
   dim3 grid((N + 255) / 256, (B + RB - 1) / RB);
   hipLaunchKernelGGL((linear_fwd_kernel<RB>), grid, dim3(256), RB * K * sizeof(float), s, z, W, b, out, B, K, N,
                      stats, C, gen_step, gen_seed);
-  return (int)hipGetLastError();
-}
-
-// fused G head (g_head_kernel): grid C / CW; 0 on success, -2 when the shape does not fit
-// (the engine then records linear_fwd + bn_finalize + bn_apply_act)
-extern "C" int DCG_API(dcg_g_head)(float* z, const float* W, const float* b, elem_t* x, elem_t* y, int B, int K, int N,
-                                   int C, const unsigned long long* gen_step, uint64_t gen_seed, const float* gamma,
-                                   const float* beta, float eps, float* mean, float* rstd, float* scale, float* shift,
-                                   float* ema_mean, float* ema_var, float decay, int act, float leak, hipStream_t s) {
-  constexpr int CW = 2;
-  if (C <= 0 || N % C || C % CW || K <= 0) return -2;
-  const int ncols = (N / C) * CW;
-  if (ncols > 256 || 256 % ncols) return -2;
-  const int rgroups = 256 / ncols;
-  const int rpt = (B + rgroups - 1) / rgroups;
-  const size_t shm = (size_t)B * K * sizeof(float);
-  if (shm > 96 * 1024) return -2;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {(const void*)g_head_kernel<CW, 8>, (const void*)g_head_kernel<CW, 16>,
-                          (const void*)g_head_kernel<CW, 32>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-      if (e != hipSuccess) return (int)e;
-    }
-    attr = true;
-  }
-#define GH_LAUNCH(R) \
-  hipLaunchKernelGGL((g_head_kernel<CW, R>), dim3(C / CW), dim3(256), shm, s, z, W, b, x, y, B, K, N, C, gen_step, \
-                     gen_seed, gamma, beta, eps, mean, rstd, scale, shift, ema_mean, ema_var, decay, act, leak)
-  if (rpt <= 8) GH_LAUNCH(8);
-  else if (rpt <= 16) GH_LAUNCH(16);
-  else if (rpt <= 32) GH_LAUNCH(32);
-  else return -2;
-#undef GH_LAUNCH
   return (int)hipGetLastError();
 }
 

@@ -85,7 +85,6 @@ class _TorchExec:
         self.dev = dev
         self.side = torch.cuda.Stream(device=dev)                        # slot 1 of main-stream segments
         self.alt = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]  # D chain (+ its slot 1)
-        self.extra = torch.cuda.Stream(device=dev)  # the last G weight gradient (fused schedule)
         self.comm = eng.comm_stream
 
     def main(self):
@@ -280,7 +279,7 @@ class HipEngine:
         self.progW = self._prog()  # G's weight gradients (see _build_gloss_and_g_backward)
         self._g_w: List[Tuple[int, int]] = []
         self._g_w_layer: List[str] = []
-        self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True, split_d=True)
+        self._build_forward(self.progA, update_ema=True, z=self.z, train_z=True)
         self._a_fwd = self.progA.size()  # forward done: D's d_loss backward may start from here
         self._build_gloss_and_g_backward(self.progA, self.progW)
         self._build_d_backward_dloss(self.progB)  # sets self._b_split (top layer done)
@@ -452,15 +451,6 @@ class HipEngine:
                 return rpb
         return 1
 
-    def _fused_g_head(self) -> bool:
-        """G's head stage (projection + g_bn0 + relu) as the one-launch g_head kernel: when its
-        shape fits (z in LDS, whole channels per workgroup); DCGAN_G_HEAD=0 records the
-        three-launch form (linear_fwd, bn_finalize, bn_apply_act) instead."""
-        cfg = self.cfg
-        if os.environ.get("DCGAN_G_HEAD", "1") == "0":
-            return False
-        return bool(self.progA.g_head_fits(self.B, cfg.z_dim, cfg.g_lin_out, cfg.g_base_ch))
-
     def _gout_applies_bn(self) -> bool:
         """G's RGB layer (narrow MFMA kernel) applies the BN + ReLU of the layer below itself."""
         L = self.gl[-1]
@@ -491,43 +481,22 @@ class HipEngine:
         return not self.f32 and L.cin <= 4 and L.cout == 64
 
     # ---- forward
-    def _build_forward(self, prog, update_ema: bool, z, train_z: bool, split_d: bool = False):
+    def _build_forward(self, prog, update_ema: bool, z, train_z: bool):
         cfg, B = self.cfg, self.B
         B2 = 2 * B
         Pg, Pd = self.model.g, self.model.d
         zseed = self.seed * 1000003 + 17 + 7919 * self.rank * int(self.rank_seeded_z)
-        split_d = split_d and self._split_d_ok()
-        if split_d:
-            # D on the real half needs only the input batch: it runs on stream slot 1 beside G's
-            # forward (forked here, joined before the head); D on the fake half follows G on slot 0
-            ev_fork = prog.new_event()
-            prog.record(ev_fork, 0)
-            prog.wait(ev_fork, 1)
-            self._build_d_forward_half(prog, 0, 1, update_ema)
         # G projection + g_bn0 + relu; train_z: z ~ U(-1,1) generated inside the projection kernel
         # (Philox keyed by the device step counter); g_bn0 partial statistics straight from it:
         # one partial row per (8-row block of z, spatial position) -- see linear_fwd_kernel
         C0 = cfg.g_base_ch
         rows0 = B * cfg.g_base_hw ** 2
-        if self._fused_g_head():
-            # one launch: projection + g_bn0 statistics, finalize (+EMA), apply + relu (misc.hip
-            # g_head_kernel: a workgroup owns whole channels, so no partial rows are exchanged)
-            st = self.bn["g_bn0"]
-            prog.g_head("g_head", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
-                        _p(self.g_h0), B, cfg.z_dim, cfg.g_lin_out, C0,
-                        _p(self.step_counter) if train_z else 0, zseed if train_z else 0,
-                        _p(Pg["g_bn0/gamma"]), _p(Pg["g_bn0/beta"]), cfg.bn_eps, _p(st["mean"]), _p(st["rstd"]),
-                        _p(st["scale"]), _p(st["shift"]),
-                        _p(self.model.g_bn.mean["g_bn0"]) if update_ema else 0,
-                        _p(self.model.g_bn.var["g_bn0"]) if update_ema else 0, cfg.bn_momentum, RELU,
-                        cfg.lrelu_leak, 0)
-        else:
-            P0 = -(-B // 8) * (cfg.g_lin_out // C0)
-            part0 = self._stats_buf("g_bn0", P0, C0)
-            prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
-                            B, cfg.z_dim, cfg.g_lin_out, 0, _p(part0), C0,
-                            _p(self.step_counter) if train_z else 0, zseed if train_z else 0)
-            self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, P0, update_ema)
+        P0 = -(-B // 8) * (cfg.g_lin_out // C0)
+        part0 = self._stats_buf("g_bn0", P0, C0)
+        prog.linear_fwd("g_h0_lin", _p(z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(self.g_h0_pre),
+                        B, cfg.z_dim, cfg.g_lin_out, 0, _p(part0), C0,
+                        _p(self.step_counter) if train_z else 0, zseed if train_z else 0)
+        self._bn_fwd(prog, "g_bn0", self.g_h0_pre, self.g_h0, rows0, C0, 1, RELU, part0, P0, update_ema)
         a_prev = self.g_h0
         Wg, Wd = self.wbf_g, self.wbf_d
         for L in self.gl:
@@ -554,13 +523,6 @@ class HipEngine:
                                         _p(self.g_a[Lp.name]), 0)
             else:  # last: + bias, tanh, written into the fake half of D's input
                 self._deconv_out(prog, L.name, a_prev, nat, self.fake, B, L, pad, Pg[L.name + "/biases"], TANH)
-        if split_d:
-            self._build_d_forward_half(prog, 1, 0, update_ema)
-            ev_join = prog.new_event()
-            prog.record(ev_join, 1)
-            prog.wait(ev_join, 0)
-            self._build_d_head(prog)
-            return
         # D forward on [real | fake]
         prev = self.d_in
         for i, L in enumerate(self.dl):
@@ -602,75 +564,6 @@ class HipEngine:
                 self._bn_fwd(prog, L.bn, self.d_x[L.name], self.d_a[L.name], rows, L.cout, 2, LRELU, part, P // 2,
                              update_ema, apply=not head_bn)
             prev = self.d_a[L.name]
-        self._build_d_head(prog)
-
-    def _split_d_ok(self) -> bool:
-        """D's forward as two half-batch chains (real beside G's forward, fake after it): 16-bit
-        builds with the direct layer-0 conv and epilogue BN statistics on every D BN layer;
-        DCGAN_SPLIT_D=0 keeps the stacked [real | fake] forward."""
-        if os.environ.get("DCGAN_SPLIT_D", "1") == "0" or self.f32 or not self._d0_direct():
-            return False
-        B = self.B
-        for L in self.dl[1:]:
-            if L.bn and self._stats_tiles(0, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout,
-                                          B * L.out_hw ** 2, True) is None:
-                return False
-        return True
-
-    def _build_d_forward_half(self, prog, g: int, stream: int, update_ema: bool):
-        """D's forward on half g of the stacked batch (0 = real, 1 = fake) on stream slot
-        `stream`: the same kernels as the stacked forward on B images, BN statistics / finalize /
-        EMA slot of group g (the stacked forward's per-group semantics)."""
-        cfg, B = self.cfg, self.B
-        Pd, Wd = self.model.d, self.wbf_d
-        sl = lambda t: t[g * B:(g + 1) * B]  # noqa: E731
-        tag = (".real", ".fake")[g]
-        prev = sl(self.d_in)
-        for i, L in enumerate(self.dl):
-            w = Wd[L.name + "/w"]
-            pad = same_pads(L.in_hw)[0]
-            rows = B * L.out_hw ** 2
-            if i == 0:
-                prog.nconv("d0.nconv" + tag, _p(prev), _p(w), _p(Pd[L.name + "/biases"]), _p(sl(self.d_a[L.name])),
-                           B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, pad, pad, LRELU, cfg.lrelu_leak,
-                           H.nconv_grid(prog, B, L.out_hw, L.out_hw), 0, 0, 0, 0, 0, 0.0, 0, stream)
-            elif not L.bn:
-                self._igemm(prog, L.name + tag, 0, prev, w, sl(self.d_a[L.name]), B, L.in_hw, L.in_hw, L.cin,
-                            L.out_hw, L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], act=LRELU, bkn=True,
-                            stream=stream)
-            else:
-                P = self._stats_tiles(0, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw, L.cout, rows, True)
-                part = self._stats_buf(L.bn + tag, P, L.cout)
-                self._igemm(prog, L.name + tag, 0, prev, w, sl(self.d_x[L.name]), B, L.in_hw, L.in_hw, L.cin,
-                            L.out_hw, L.out_hw, L.cout, pad, bias=Pd[L.name + "/biases"], stats=part,
-                            rows_per_group=rows, bkn=True, stream=stream)
-                head_bn = i == len(self.dl) - 1 and self._head_applies_bn()
-                self._bn_fwd_group(prog, L.bn, sl(self.d_x[L.name]), sl(self.d_a[L.name]), rows, L.cout, g, LRELU,
-                                   part, P, update_ema, apply=not head_bn, stream=stream)
-            prev = sl(self.d_a[L.name])
-
-    def _bn_fwd_group(self, prog, name, x, y, rows, C, g, act, part, ppg, update_ema, apply, stream):
-        """_bn_fwd for ONE group g of a two-group (real / fake) BN layer: finalize into row g of
-        the layer's mean / rstd / scale / shift and EMA slot g, then apply + act on that half."""
-        cfgm = self.cfg
-        st = self.bn[name]
-        bnstate = self.model.d_bn if name.startswith("d_") else self.model.g_bn
-        P = self.model.d if name.startswith("d_") else self.model.g
-        ema_m = bnstate.mean[name][g] if update_ema else None
-        ema_v = bnstate.var[name][g] if update_ema else None
-        prog.bn_finalize(name + ".fin" + str(g), _p(part), ppg, 1, C, float(rows), _p(P[name + "/gamma"]),
-                         _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"][g]), _p(st["rstd"][g]),
-                         _p(st["scale"][g]), _p(st["shift"][g]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, stream)
-        if apply:
-            prog.bn_apply_act(name + ".apply" + str(g), _p(x), _p(y), _p(st["scale"][g]), _p(st["shift"][g]), rows,
-                              C, rows, act, cfgm.lrelu_leak, stream)
-
-    def _build_d_head(self, prog):
-        """D's head GEMV (+ the top BN layer's apply when fused) and the 3-loss BCE."""
-        cfg, B = self.cfg, self.B
-        B2 = 2 * B
-        Pd = self.model.d
-        prev = self.d_a[self.dl[-1].name]
         lin = cfg.d_lin_name
         last = self.dl[-1]
         if last.bn and self._head_applies_bn():
@@ -1193,26 +1086,12 @@ class HipEngine:
             pos = a_end
         ex.run(self.progA, [cs, ex.side], pos, -1)
         w = 0
-        own_last = self._gw_last_own() and len(self._g_w) >= 2
-        for k, (m, (_, w_end)) in enumerate(zip(marks, self._g_w)):
-            if own_last and k == len(self._g_w) - 1:
-                # the last G weight gradient (its operand is final last) on its own stream: it
-                # no longer queues behind the previous ones on the D chain's stream
-                ex.wait_mark(ex.extra, m)
-                ex.run(self.progW, [ex.extra, ex.extra], w, w_end)
-            else:
-                ex.wait_mark(ex.alt[0], m)
-                ex.run(self.progW, ex.alt, w, w_end)
+        for m, (_, w_end) in zip(marks, self._g_w):
+            ex.wait_mark(ex.alt[0], m)
+            ex.run(self.progW, ex.alt, w, w_end)
             w = w_end
         ex.wait(cs, ex.alt[0])
-        if own_last:
-            ex.wait(cs, ex.extra)
         ex.run(self.progC, [cs, ex.side])
-
-    def _gw_last_own(self) -> bool:
-        """Fused schedule: the last G weight gradient on a stream of its own
-        (DCGAN_GW_LAST_OWN=0: behind the others on the D chain's stream)."""
-        return os.environ.get("DCGAN_GW_LAST_OWN", "1") != "0"
 
     def _run_ddp(self, ex, cs):
         """The "ddp" schedule: the fused step with the gradient all-reduces on the comm stream,

@@ -21,7 +21,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
-STREAMS = ("main", "side", "alt0", "alt1", "comm", "extra")
+STREAMS = ("main", "side", "alt0", "alt1", "comm")
 
 
 @dataclass
@@ -62,7 +62,6 @@ class RecordingExec:
         self.side = st["side"]
         self.alt = [st["alt0"], st["alt1"]]
         self.comm = st["comm"]
-        self.extra = st["extra"]
         self.vc: Dict[str, Dict[str, int]] = {n: {n: 0} for n in STREAMS}
         self.ops: List[_Op] = []
         self.events: Dict[Tuple[int, int], Dict[str, int]] = {}

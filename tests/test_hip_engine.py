@@ -263,36 +263,6 @@ def test_engine_graph_replay_matches_eager():
     assert e2.global_step == 4
 
 
-def test_engine_split_d_and_fused_head_match_stacked(monkeypatch):
-    """The default forward (D's real half beside G's forward on a second stream, the fused
-    one-launch G head) vs the stacked [real | fake] D forward with the three-launch G head:
-    same losses, gradients, BN statistics and EMA slots up to summation order (B = 128, the
-    headline shape)."""
-    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
-    dev = torch.device("cuda", 0)
-    cfg = DCGANConfig()
-    B = 128
-    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
-    engs = []
-    for split in ("0", "1"):
-        monkeypatch.setenv("DCGAN_SPLIT_D", split)
-        monkeypatch.setenv("DCGAN_G_HEAD", split)
-        e = HipEngine(cfg, B, dev, graph=True, seed=3)
-        assert e._split_d_ok() == (split == "1") and e._fused_g_head() == (split == "1")
-        e.set_batch(real)
-        e.train_step()
-        engs.append(e)
-    torch.cuda.synchronize()
-    a, b = engs
-    la, lb = a.last_losses(), b.last_losses()
-    for k in la:
-        assert abs(la[k] - lb[k]) <= 1e-3 * max(1.0, abs(la[k])), (k, la[k], lb[k])
-    assert rel(b.grad_d.flat, a.grad_d.flat) < 2e-2
-    assert rel(b.grad_g.flat, a.grad_g.flat) < 2e-2
-    assert rel(b.model.d_bn.flat, a.model.d_bn.flat) < 1e-4
-    assert rel(b.model.g_bn.flat, a.model.g_bn.flat) < 1e-4
-
-
 def test_engine_sampler_and_eval():
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     dev = torch.device("cuda", 0)

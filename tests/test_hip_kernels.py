@@ -406,43 +406,6 @@ def test_gan_loss_kernel():
     close(dlg, ggf, 1e-5, "dl_g")
 
 
-@pytest.mark.parametrize("B", [128, 64, 33])
-def test_fused_g_head(B):
-    """misc.hip g_head_kernel (projection + g_bn0 statistics, finalize + EMA, apply + relu in one
-    launch) vs the three-launch path: z (Philox) and the pre-BN output bit-identical, BN
-    statistics / EMA / output vs an fp64 reference of the stored pre-BN values."""
-    h = H()
-    K, N, C = 100, 8192, 512
-    W = rnd(K, N, scale=0.05, seed=130)
-    b = rnd(N, scale=0.1, seed=131)
-    gamma = rnd(C, seed=132).abs() + 0.5
-    beta = rnd(C, scale=0.2, seed=133)
-    step = torch.tensor([11], dtype=torch.int64, device=dev)
-    z1, z2 = torch.empty(B, K, device=dev), torch.full((B, K), float("nan"), device=dev)
-    x1 = torch.empty(B, N, device=dev, dtype=torch.bfloat16)
-    x2, y2 = torch.empty_like(x1), torch.empty_like(x1)
-    st = {k: torch.full((C,), float("nan"), device=dev) for k in ("mean", "rstd", "scale", "shift")}
-    em0, ev0 = rnd(C, scale=0.1, seed=134), rnd(C, seed=135).abs()
-    em, ev = em0.clone(), ev0.clone()
-    assert h.ext().Program.g_head_fits(B, K, N, C)
-    pr = _prog()
-    pr.linear_fwd("lin_gen", _p(z1), _p(W), _p(b), _p(x1), B, K, N, 0, 0, 0, _p(step), 4242)
-    pr.g_head("g_head", _p(z2), _p(W), _p(b), _p(x2), _p(y2), B, K, N, C, _p(step), 4242, _p(gamma), _p(beta), 1e-5,
-              _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]), _p(st["shift"]), _p(em), _p(ev), 0.9, 1, 0.2, 0)
-    h.run(pr)
-    torch.cuda.synchronize()
-    assert torch.equal(z1, z2) and torch.equal(x1, x2)
-    xo = x2.double().reshape(B * N // C, C)
-    mu = xo.mean(0)
-    var = (xo * xo).mean(0) - mu * mu
-    close(st["mean"], mu.float(), 1e-5, "g_head mean")
-    close(st["rstd"], (var + 1e-5).rsqrt().float(), 1e-4, "g_head rstd")
-    close(em, (em0.double() - 0.1 * (em0.double() - mu)).float(), 1e-5, "g_head ema mean")
-    close(ev, (ev0.double() - 0.1 * (ev0.double() - var)).float(), 1e-4, "g_head ema var")
-    yref = torch.relu(xo * st["scale"].double() + st["shift"].double()).reshape(B, N)
-    close(y2, yref.float(), 1e-2, "g_head relu(bn(x))")
-
-
 def test_linear_and_head():
     h = H()
     B, K, N = 33, 100, 8192
