@@ -1086,12 +1086,29 @@ class HipEngine:
             pos = a_end
         ex.run(self.progA, [cs, ex.side], pos, -1)
         w = 0
-        for m, (_, w_end) in zip(marks, self._g_w):
+        n_main = min(self._gw_tail_on_main(), len(self._g_w))
+        for m, (_, w_end) in zip(marks[:len(marks) - n_main], self._g_w[:len(self._g_w) - n_main]):
             ex.wait_mark(ex.alt[0], m)
             ex.run(self.progW, ex.alt, w, w_end)
             w = w_end
+        if n_main:
+            # the last G weight gradients on cs after the G chain (their operands are produced
+            # there): the D chain's stream no longer runs them serially after everything else
+            ex.run(self.progW, [cs, ex.side], w, -1)
         ex.wait(cs, ex.alt[0])
         ex.run(self.progC, [cs, ex.side])
+
+    def _gw_tail_on_main(self) -> int:
+        """Number of trailing G weight-gradient segments the fused step runs on the G chain's
+        stream after that chain instead of behind the D chain (DCGAN_GW_TAIL_ON_MAIN). Default 2:
+        at 64x64 the D chain's stream otherwise still runs g_h2's and g_h1's weight gradients
+        serially for ~70 us after the G chain has finished (profiles/r4/step_profile_r4.txt);
+        measured 0 / 1 / 2 / 3 / 4 -> 114.0k / 115.2k / 116.1k-118.1k / 116.6k / 115.2k img/s
+        (profiles/r4/ab_gw_tail_on_main_r4.txt)."""
+        v = os.environ.get("DCGAN_GW_TAIL_ON_MAIN", "2")
+        if not v.isdigit():
+            raise ValueError("DCGAN_GW_TAIL_ON_MAIN must be a non-negative integer, got %r" % v)
+        return int(v)
 
     def _run_ddp(self, ex, cs):
         """The "ddp" schedule: the fused step with the gradient all-reduces on the comm stream,

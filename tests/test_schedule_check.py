@@ -139,3 +139,22 @@ def test_ddp_schedule_env_selects_the_schedule(monkeypatch, good):
     assert eng._schedule() == good
     hz, _ = SC.check_engine(eng)
     assert hz == []
+
+
+@pytest.mark.parametrize("n", ["0", "1", "2", "4"])
+def test_fused_g_wgrad_tail_on_main_has_no_hazards(monkeypatch, n):
+    """DCGAN_GW_TAIL_ON_MAIN=n: the last n G weight gradients of the fused step on the G chain's
+    stream after that chain -- still free of unordered overlaps."""
+    monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", n)
+    eng = _dry()
+    assert eng._schedule() == "fused" and eng._gw_tail_on_main() == int(n)
+    hz, n_ops = SC.check_engine(eng)
+    assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_fused_g_wgrad_tail_on_main_rejects_bad_values(monkeypatch):
+    monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", "two")
+    eng = _dry()
+    with pytest.raises(ValueError):
+        eng._gw_tail_on_main()
