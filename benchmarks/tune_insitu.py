@@ -115,6 +115,9 @@ def neighbours(key, cur, tiles=False, extra_tiles=()):
         for t2 in extra_tiles:  # e.g. --extra_tiles 9: the 8-wave 128x128 tile, same stages / split
             if t2 != tile:
                 out.append((200 + 10 * ns + t2, sp))
+    # igemm3 configs whose LDS ring does not fit 160 KiB are no candidates (e.g. 226: 8-wave 256x128 at NS = 4)
+    out = [c for c in out if key.startswith("w3,") or c[0] < 200 or
+           (c[0] % 10 in H.IGEMM3_TILES and H.igemm3_lds(c[0]) <= 160 * 1024)]
     seen, res = set(), []
     for c in out:
         if c not in seen and c != cur:
