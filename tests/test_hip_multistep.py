@@ -176,23 +176,24 @@ def test_bf16_engine_tracks_fp32_engine_over_50_steps():
 
 
 def test_generator_learns_flat_colour_images(tmp_path):
-    """Learnability on a real input path: 4,096 flat-colour 28x28x1 images (each image one grey
-    level from {-0.6, +0.6}, so the data mean is 0 and every image has zero spatial variance)
-    written as float64 TFRecords, read by the native loader, 600 bf16 steps. The untrained sampler
-    is far from the data (its images have texture); after training the EMA-BN sampler's images
-    are much flatter (mean per-image spatial std under 0.5x the untrained sampler's; measured
-    0.99 -> 0.36 after 600 steps, with D winning by then) and inside the data's intensity range
-    (|mean| < 0.7; a GAN may favour one of the two modes, so the mean is not pinned to the data
-    mean), and most sampled images have a mean grey level near a data mode (|per-image mean| >=
-    0.3; measured 0.00 untrained -> 0.73 after 600 steps on MI355X, asserted >= 0.6), which a
-    generator collapsed to constant grey fails."""
+    """Learnability on a real input path: 4,096 flat 28x28x1 images (each image one grey level
+    drawn from U(0.4, 0.6): zero spatial variance, intensity 0.5 +- 0.1) written as float64
+    TFRecords, read by the native loader, 600 bf16 steps. The untrained EMA-BN sampler is far from
+    the data (textured images, mean ~0.1, spatial std ~1.0); after training its images are flat
+    (mean spatial std under 0.2x the untrained one) and at the data's intensity: at least 90 % of
+    the samples have a per-image mean in [0.2, 0.8] and the sample mean is within 0.2 of 0.5. A
+    generator collapsed to a constant 0 grey fails both. Measured on MI355X (seeds 4 and 5,
+    benchmarks/study/learn_diag.py, profiles/r4/learnability_diag_r4.txt): from step 400 on,
+    100 % in range, mean 0.51-0.55, spatial std 0.01-0.05. (A two-mode +-0.6 dataset, used until
+    round 4, is unusable here: the GAN hops between the modes and any single checkpoint sees all
+    samples near one mode or none.)"""
     from distributed_tensorflow_for_dcgan_amd.data import pipeline as PL
     from distributed_tensorflow_for_dcgan_amd.data import tfrecord as TR
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     n = 4096
-    lv = rng.choice(np.array([-0.6, 0.6]), size=n)
+    lv = 0.5 + rng.uniform(-0.1, 0.1, size=n)
     imgs = np.broadcast_to(lv[:, None, None, None], (n, 28, 28, 1)).astype(np.float64)
     d = tmp_path / "train"
     d.mkdir()
@@ -205,16 +206,12 @@ def test_generator_learns_flat_colour_images(tmp_path):
                             out_dtype="bf16", num_examples=n)
     z = (torch.rand(B, cfg.z_dim, generator=torch.Generator().manual_seed(3)) * 2 - 1).to(dev)
 
-    def sample_stats():
-        x = eng.sampler(z).float()
-        return float(x.mean()), float(x.flatten(1).std(1).mean())
+    def stats():  # (sample mean, mean per-image spatial std, fraction of per-image means in [0.2, 0.8])
+        x = eng.sampler(z).float().flatten(1)
+        m = x.mean(1)
+        return float(x.mean()), float(x.std(1).mean()), float(((m >= 0.2) & (m <= 0.8)).float().mean())
 
-    def near_mode():  # fraction of sampled images whose mean grey level sits near a data mode (+-0.6)
-        x = eng.sampler(z).float()
-        return float((x.flatten(1).mean(1).abs() >= 0.3).float().mean())
-
-    m0, s0 = sample_stats()
-    f0 = near_mode()
+    m0, s0, f0 = stats()
     try:
         for _ in range(600):
             eng.set_batch(src.next())
@@ -222,13 +219,10 @@ def test_generator_learns_flat_colour_images(tmp_path):
         torch.cuda.synchronize()
     finally:
         src.close()
-    m1, s1 = sample_stats()
-    f1 = near_mode()
-    print("\nsampler before: mean %.3f spatial std %.3f near-mode %.2f; after 600 steps: mean %.3f spatial std %.3f "
-          "near-mode %.2f; losses %s" % (m0, s0, f0, m1, s1, f1, eng.last_losses()))
+    m1, s1, f1 = stats()
+    print("\nsampler before: mean %.3f spatial std %.3f in-range %.2f; after 600 steps: mean %.3f spatial std %.3f "
+          "in-range %.2f; losses %s" % (m0, s0, f0, m1, s1, f1, eng.last_losses()))
     assert all(math.isfinite(v) for v in eng.last_losses().values())
-    assert s1 < 0.5 * s0, (s0, s1)
-    assert abs(m1) < 0.7, m1
-    # a generator collapsed to a constant grey (mean ~0) passes the two checks above; the data
-    # are two modes at +-0.6, so most samples must sit near one of them
-    assert f1 >= 0.6, (f0, f1)
+    assert s1 < 0.2 * s0, (s0, s1)
+    assert f1 >= 0.9, (f0, f1)
+    assert abs(m1 - 0.5) < 0.2, m1
