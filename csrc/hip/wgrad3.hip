@@ -34,6 +34,14 @@ __device__ __forceinline__ void w3_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
+// vmcnt(n * L) for a runtime n in [0, NMAX]
+template <int L, int NMAX>
+__device__ __forceinline__ void w3_wait_vmcnt_n(int n) {
+  if constexpr (NMAX >= 2) { if (n >= 2) { w3_wait_vmcnt<2 * L>(); return; } }
+  if constexpr (NMAX >= 1) { if (n >= 1) { w3_wait_vmcnt<L>(); return; } }
+  w3_wait_vmcnt<0>();
+}
+
 // TT taps per tile (1 or 2): with TT = 2 the tile's BM rows are [tap 2 tg: Mc channels][tap 2 tg + 1:
 // Mc channels] (BM = 2 Mc): both taps share the B (Dm) tile -- half the DMA per MFMA of the 64-row
 // single-tap tile for the 64-channel layers (tap 25 of group 12 reads zeros and is not stored).
@@ -152,12 +160,9 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
 
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (NS >= 3) {
-      if (kt + 1 < nk) w3_wait_vmcnt<LPT * (NS - 2)>();
-      else w3_wait_vmcnt<0>();
-    } else {
-      w3_wait_vmcnt<0>();
-    }
+    // tile kt landed; the younger tiles issued so far (at most NS - 2, fewer at the loop's end) may
+    // stay in flight
+    w3_wait_vmcnt_n<LPT, NS - 2>(min(NS - 2, nk - 1 - kt));
     // all waves' DMA of tile kt landed; all waves are done reading slot (kt-1) % NS
     asm volatile("s_barrier" ::: "memory");
     if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS);
