@@ -1067,7 +1067,10 @@ class HipEngine:
     def _run_fused(self, ex, cs):
         """The "fused" schedule issued onto cs (+ the alt streams); also what gets captured.
         D's backward starts right after the forward: holding it until the g_loss chain has left
-        D (so it overlaps only G's backward) measured 1.314 vs 1.297 ms/step on MI355X."""
+        D (so it overlaps only G's backward) measured 1.314 vs 1.297 ms/step on MI355X, and
+        holding it behind only the first 3-7 G-chain ops measured slower as well
+        (profiles/r4/ab_d_start_after_r4.txt). G's weight gradients run behind the D chain on its
+        stream, except the last _gw_tail_on_main() of them, which follow the G chain on cs."""
         ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
         ex.wait(ex.alt[0], cs)
         ex.run(self.progB, ex.alt)
