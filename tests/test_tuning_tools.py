@@ -1,0 +1,36 @@
+"""CPU tests of the tile-table tooling: the in-situ tuner only proposes legal neighbours, and the
+shipped table's entries name configurations the kernels accept (LDS ring within 160 KiB, known
+tile ids / stage counts)."""
+import json
+import os
+
+import pytest
+
+from distributed_tensorflow_for_dcgan_amd.ops import hip as H
+
+
+def test_tuner_neighbours_fit_lds():
+    T = pytest.importorskip("benchmarks.tune_insitu")
+    for key, cur in (("1,256,8,8,256,16,16,128", (216, 1)), ("0,128,32,32,64,16,16,128", (210, 1)),
+                     ("1,512,4,4,2048,8,8,1024", (210, 2))):
+        for tiles in (False, True):
+            for cfg, sp in T.neighbours(key, cur, tiles=tiles):
+                assert sp >= 1
+                if 200 <= cfg < 300:
+                    assert cfg % 10 in H.IGEMM3_TILES and H.igemm3_lds(cfg) <= 160 * 1024, (key, cfg)
+
+
+def test_shipped_table_entries_are_legal():
+    path = os.path.join(os.path.dirname(H.__file__), "igemm_tuned.json")
+    with open(path) as f:
+        table = json.load(f)
+    assert table
+    for key, val in table.items():
+        cfg, sp = (int(x) for x in val.split(":"))
+        assert sp >= 1, key
+        if key.startswith("w3,"):
+            assert 300 <= cfg < 340 and cfg % 10 in H.WGRAD3_TILES, (key, val)
+        elif cfg >= 200:
+            assert cfg < 240 and cfg % 10 in H.IGEMM3_TILES and H.igemm3_lds(cfg) <= 160 * 1024, (key, val)
+        else:
+            assert cfg % 100 in H.IGEMM_CFGS and sp == 1, (key, val)
