@@ -4,8 +4,9 @@
 ``python bench.py --gpus N --steps K --warmup W`` runs the full reference-semantics
 DCGAN training step (G fwd, D(real)+D(fake) fwd, 3 losses, D/G backward, gradient
 all-reduce over RCCL when N>1, two TF-Adam updates) on synthetic images of the BASELINE
-shape with random-init weights. For N>1 it is launched one rank per GPU by
-``torch.distributed.run``. W untimed warmup steps, then EXACTLY K timed steps between a
+shape with random-init weights. For N>1 it runs one rank per GPU: either under
+``torch.distributed.run`` (WORLD_SIZE set) or, when started directly, by launching N child
+ranks itself (``self_launch``). W untimed warmup steps, then EXACTLY K timed steps between a
 barrier + device sync on both sides; the per-rank time is MAX-reduced over ranks and
 rank 0 prints one JSON line. ``value`` = N * batch * K / max_time (weak scaling).
 """
@@ -40,8 +41,30 @@ def parse():
     return p.parse_args()
 
 
+def self_launch(args) -> int:
+    """``python bench.py --gpus N`` (N > 1) without an outer launcher: start N child ranks, one
+    per GPU, with the torch.distributed.run env contract (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_*; rendezvous on 127.0.0.1). The parent never touches a GPU (it only COUNTS devices,
+    which initialises no HIP context) and never exec()s: it waits for the children, stops the
+    rest when one fails, and returns the worst exit code. Rank 0's JSON line reaches stdout
+    directly (the children inherit it); launcher messages go to stderr. The N-worker reference
+    starts one process per task by hand (``/root/reference/image_train.py:52-67``)."""
+    from distributed_tensorflow_for_dcgan_amd.launch import launch
+    gloo = os.environ.get("DCGAN_DIST_BACKEND", "") == "gloo"
+    n_dev = torch.cuda.device_count()
+    if n_dev < args.gpus and not gloo:
+        # (DCGAN_DIST_BACKEND=gloo: rehearsal, ranks may share a GPU or run on the CPU)
+        print("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, n_dev), file=sys.stderr)
+        return 2
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    return launch(args.gpus, cmd, max_restarts=0, master_addr="127.0.0.1",
+                  log=lambda m: print(m, file=sys.stderr, flush=True))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -52,8 +52,18 @@ def _stop(procs: List[subprocess.Popen], grace: float) -> None:
             p.wait()
 
 
+def _term_as_exit(signum, frame):
+    raise SystemExit(128 + signum)
+
+
 def launch(nproc: int, cmd: List[str], max_restarts: int = 0, master_addr: str = "127.0.0.1",
            master_port: int = 0, grace: float = 10.0, log=print) -> int:
+    # the ranks run in their own sessions, so a SIGTERM to the launcher alone would orphan
+    # them: turn it into an exception that stops them first
+    try:
+        signal.signal(signal.SIGTERM, _term_as_exit)
+    except ValueError:  # not the main thread
+        pass
     attempt = 0
     while True:
         port = master_port or _free_port()
@@ -65,16 +75,20 @@ def launch(nproc: int, cmd: List[str], max_restarts: int = 0, master_addr: str =
             procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
         log("[launch] attempt %d: %d ranks, rendezvous %s:%d" % (attempt, nproc, master_addr, port))
         failed = None
-        while True:
-            codes = [p.poll() for p in procs]
-            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-            if bad:
-                failed = bad[0]
-                break
-            if all(c == 0 for c in codes):
-                log("[launch] all %d ranks finished" % nproc)
-                return 0
-            time.sleep(0.1)
+        try:
+            while True:
+                codes = [p.poll() for p in procs]
+                bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+                if bad:
+                    failed = bad[0]
+                    break
+                if all(c == 0 for c in codes):
+                    log("[launch] all %d ranks finished" % nproc)
+                    return 0
+                time.sleep(0.1)
+        except BaseException:  # SIGTERM (see _term_as_exit) / Ctrl-C: take the ranks down too
+            _stop(procs, grace)
+            raise
         log("[launch] rank %d exited with %d; stopping the other ranks" % failed)
         _stop(procs, grace)
         if attempt >= max_restarts:

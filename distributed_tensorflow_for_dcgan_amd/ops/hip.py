@@ -392,7 +392,11 @@ def nconv_grid(prog, B: int, Ho: int, Wo: int, cap: Optional[int] = None) -> int
     workgroups looping over the tiles) or, with cap <= 0, one workgroup per tile. The default cap
     is NCONV_MAX_GRID; DCGAN_NCONV_CAP overrides it (A/B studies)."""
     if cap is None:
-        cap = int(os.environ.get("DCGAN_NCONV_CAP", NCONV_MAX_GRID))
+        v = os.environ.get("DCGAN_NCONV_CAP", str(NCONV_MAX_GRID))
+        if not v.isdigit():
+            raise ValueError("DCGAN_NCONV_CAP must be a non-negative integer (0 = one workgroup per tile), "
+                             "got %r" % v)
+        cap = int(v)
     tiles = prog.nconv_tiles(B, Ho, Wo)
     return tiles if cap <= 0 else min(tiles, cap)
 

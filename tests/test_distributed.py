@@ -149,3 +149,41 @@ def test_reference_style_worker_hosts_launch(tmp_path):
     assert "rank 0/2 local_rank 0 (worker_hosts)" in outs[0]
     assert "rank 1/2 local_rank 1 (worker_hosts)" in outs[1]
     assert "Epoch: [ 0] step: [ 2]" in outs[0]
+
+
+def _bench_env(**kw):
+    env = dict(os.environ, OMP_NUM_THREADS="2", **kw)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "DCGAN_DIST_BACKEND"):
+        if k not in kw:
+            env.pop(k, None)
+    return env
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """``python bench.py --gpus 2`` without an outer launcher and without 2 visible GPUs exits
+    2 with a message naming the GPU count, before starting any rank."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=_bench_env(), capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode == 2
+    assert "--gpus 2 but only 0 GPU(s) visible" in p.stderr
+    assert p.stdout.strip() == ""
+
+
+def test_bench_self_launches_ranks_gloo_cpu():
+    """The driver's direct form ``python bench.py --gpus 2`` (no torch.distributed.run): bench.py
+    starts two child ranks itself; here over gloo on the CPU with the reference engine. Rank 0
+    prints exactly one JSON line on stdout (launcher messages go to stderr; gloo's own C++
+    connection notices also land on stdout, RCCL prints none)."""
+    import json
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--engine", "reference", "--dtype", "fp32", "--output_size", "28", "--c_dim", "1", "--batch_size", "4"]
+    p = subprocess.run(cmd, env=_bench_env(DCGAN_DIST_BACKEND="gloo"), capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    assert "[launch]" not in p.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["world_size"] == 2 and res["config"]["backend"] == "gloo"
+    assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 8
+    assert "[launch] all 2 ranks finished" in p.stderr

@@ -213,7 +213,7 @@ def test_bf16_wire_holds_the_50_step_envelope(tmp_path):
 
 
 def test_timed_concurrent_schedule_matches_fused():
-    """The per-phase timed step (6 concurrent graph segments, the DDP schedule at W=1) is the
+    """The per-phase timed step (7 concurrent graph segments incl. G_tail, the DDP schedule at W=1) is the
     same computation as the single fused graph, bit for bit; phase ends are reported."""
     a = _make(1, 0, True)
     b = _make(1, 0, True)
@@ -248,6 +248,28 @@ def test_bench_two_ranks_json_contract(tmp_path):
     assert res["n_gpus"] == 2 and res["steps"] == 4 and res["warmup"] == 2
     assert res["config"]["global_batch"] == 256 and res["config"]["parallelism"] == "dp2"
     assert res["value"] > 0 and res["higher_is_better"] is True and res["scaling"] == "weak"
+
+
+def test_bench_direct_two_ranks_self_launch(tmp_path):
+    """``python bench.py --gpus 2`` with NO outer launcher (the driver's own command form):
+    bench.py starts the two ranks itself (child processes, the parent never touches the GPU).
+    gloo lets both ranks share this one GPU; on an 8-GPU node the same path runs RCCL."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DCGAN_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and "[launch]" not in out.stdout, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["config"]["world_size"] == 2 and len(res["config"]["devices"]) == 2
+    assert res["config"]["backend"] == "gloo" and res["value"] > 0
 
 
 def _rccl_worker(out_dir, graph, port, schedule):
