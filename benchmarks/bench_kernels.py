@@ -67,8 +67,10 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
     phases = 4 if mode == 1 else 1
     M = Bn * (-(-Hout // 2)) * (-(-Wout // 2)) if mode == 1 else Bn * Hout * Wout
     kt = (9 if mode == 1 else 25 if mode == 0 else 1) * -(-Kc // 64)
-    for c in range(200, 240):
+    for c in range(200, 260):
         if c % 10 not in H.IGEMM3_TILES or H.igemm3_lds(c) > 160 * 1024:
+            continue
+        if not H.igemm3_pp_ok(c, mode, Kc):
             continue
         bm, bn = H.IGEMM3_TILES[c % 10]
         if bn > N:

@@ -129,14 +129,13 @@ def main():
         gd, gg = eng.grad_d.flat, eng.grad_g.flat
         o = eng._d_top_off
         us3 = [float(x) for x in a.fake_comm_us.split(",")] if a.fake_comm_us else [None] * 3
-        eng._ar_g = fake("g", gg, us3[0])
         eng._ar_dtop = fake("dtop", gd[o:], us3[1])
         eng._ar_drest = fake("drest", gd[:o], us3[2])
         if a.schedule == "ddp":
             eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), gg[lo:hi]) for _, lo, hi in eng._g_cuts]
-        for name, r in list(vars(eng).items()):  # split G buckets of the segmented schedules
-            if name.startswith("_ar_gsplit") and isinstance(r, D.GradAllReducer):
-                setattr(eng, name, fake(name[4:], r.flat))
+        for name, r in list(vars(eng).items()):  # the G buckets of the segmented schedules
+            if name in ("_ar_g", "_ar_g_hi", "_ar_g_lo") and isinstance(r, D.GradAllReducer):
+                setattr(eng, name, fake(name[4:], r.flat, us3[0] if name == "_ar_g" else None))
     eng.set_synthetic_batch(torch.rand(a.batch_size, 64, 64, 3, device=dev) * 2 - 1)
     for _ in range(a.warmup):
         eng.train_step()

@@ -1,6 +1,10 @@
 """Learnability diagnostics for tests/test_hip_multistep.py: per-image mean statistics of the
 EMA sampler and of the last training batch's fakes at checkpoints, for a two-mode (+-0.6) and a
-one-mode (0.5 +- 0.1) flat-grey dataset."""
+one-mode (0.5 +- 0.1) flat-grey dataset. `div` = std over the sampler's images of their means
+(sample diversity; the one-mode data's own is 0.2 / sqrt(12) = 0.058), so a generator that maps
+every z to one grey level shows div ~ 0.
+
+    python benchmarks/study/learn_diag.py [one|two ...] [--seeds 4,5] [--steps 200,400,600]"""
 import sys
 import tempfile
 
@@ -39,16 +43,22 @@ def run(kind, seed, steps=(200, 400, 600, 800, 1000, 1200)):
                 x = eng.sampler(z).float().flatten(1)
                 m = x.mean(1)
                 f = eng.fake.float().flatten(1).mean(1)
-                print("%s seed %d step %4d  sampler: mean %+.3f near(|m|>=.3) %.2f in[.2,.8] %.2f std %.3f | train fakes: "
-                      "mean %+.3f near %.2f in[.2,.8] %.2f" % (
+                print("%s seed %d step %4d  sampler: mean %+.3f near(|m|>=.3) %.2f in[.2,.8] %.2f std %.3f div %.4f | "
+                      "train fakes: mean %+.3f near %.2f in[.2,.8] %.2f div %.4f" % (
                           kind, seed, s, m.mean(), (m.abs() >= 0.3).float().mean(), ((m > 0.2) & (m < 0.8)).float().mean(),
-                          x.std(1).mean(), f.mean(), (f.abs() >= 0.3).float().mean(), ((f > 0.2) & (f < 0.8)).float().mean()),
-                      flush=True)
+                          x.std(1).mean(), m.std(), f.mean(), (f.abs() >= 0.3).float().mean(),
+                          ((f > 0.2) & (f < 0.8)).float().mean(), f.std()), flush=True)
         finally:
             src.close()
 
 
 if __name__ == "__main__":
-    for kind in ("two", "one"):
-        for seed in (4, 5):
-            run(kind, seed)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kinds", nargs="*", default=["two", "one"])
+    ap.add_argument("--seeds", default="4,5")
+    ap.add_argument("--steps", default="200,400,600,800,1000,1200")
+    a = ap.parse_args()
+    for kind in a.kinds:
+        for seed in (int(v) for v in a.seeds.split(",")):
+            run(kind, seed, tuple(int(v) for v in a.steps.split(",")))

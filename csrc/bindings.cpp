@@ -283,14 +283,15 @@ class Program {
         .w(C, (c_rows - 1) * ldc * out_es + (size_t)(cofs + N) * out_es)
         .w(stats, (size_t)mtiles * a.nphases * 2 * N * 4);
     if (bnb_x) {
-      const size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
+      size_t lds = (size_t)(v3 ? ns : 2) * (bm + bn) * 128;
       if (dt_ == 2) throw std::runtime_error("igemm bnb: not available in the fp32 build");
       const size_t nt = v3 ? (size_t)KF(dcg_igemm3_threads)(cfg) : 256;
       // igemm3 (waves along M per tile id, igemm3.hip DCG_IGEMM3_TILES): the row-lane scratch may
       // alias the C tile; v1 keeps them apart
-      static const int kWM3[10] = {2, 4, 1, 2, 2, 2, 4, 2, 8, 2};
+      static const int kWM3[10] = {2, 4, 1, 2, 2, 2, 4, 2, 8, 4};
       const size_t wm = v3 ? (size_t)kWM3[cfg % 10] : 4;
       const size_t ct = (size_t)bm * (bn + 8) * 2, r2 = 64 * nt;
+      if (v3) lds = std::max(lds, (bm + 2 * wm * bn) * 4 + ct);  // igemm3_lds_bytes
       const size_t need = (bm + 2 * wm * bn) * 4 + (v3 ? std::max(ct, r2) : ct + r2);
       if (need > lds || out_f32 || N % 8 || ldc % 8 || cofs % 8)
         throw std::runtime_error("igemm bnb: tile has no LDS for the fused statistics or output is not vectorizable");

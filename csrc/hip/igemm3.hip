@@ -72,7 +72,24 @@ __device__ __forceinline__ void wait_vmcnt_n(int n) {
   wait_vmcnt<0>();
 }
 
-template <int BM, int BN, int WM, int WN, int BKN, int NS, int PL>
+__device__ __forceinline__ void pp_barrier() {
+  // a raw s_barrier pinned in place: no MFMA / ds_read may be scheduled across it (hipcc moves
+  // register-only MFMAs past an asm statement otherwise), and no vmcnt drain (the LDS-DMA of
+  // younger tiles stays in flight across it)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// dynamic LDS of a tile: the NS-stage operand ring, or the epilogue's row offsets + statistics +
+// C tile when that is larger (the 256x256 tile at NS = 2)
+template <int BM, int BN, int WM, int NS>
+constexpr int igemm3_lds_bytes() {
+  constexpr int ring = NS * (BM + BN) * 128, epi = (BM + 2 * WM * BN) * 4 + BM * (BN + 8) * 2;
+  return ring > epi ? ring : epi;
+}
+
+template <int BM, int BN, int WM, int WN, int BKN, int NS, int PL, int PP = 0>
 __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   constexpr bool kStudy = DCG_IGEMM_STUDY != 0;
   constexpr int BK = 64;
@@ -149,9 +166,183 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, (ablate & 1) ? 0u : p.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.Bw, (ablate & 2) ? 0u : p.b_bytes);
 
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int a_chunk = (lane & 7) ^ (lane >> 3);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // fragments of one k-tile (both k32 halves) from LDS stage `slot` into registers
+  elem8 af[2][FM], bfr[2][FN];
+  auto read_frags = [&](int slot) {
+    const lds_char* sa = lds3 + slot * STAGE;
+    const lds_char* sb = sa + A_BYTES;
+    const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16 + fr;
+        af[ks][i] = *reinterpret_cast<const __attribute__((address_space(3))) elem8*>(sa + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+      if constexpr (BKN) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = ks * 32 + 8 * g4 + 4 * h + q4;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int c8 = (wn * TN + j * 16) / 4 + p4;
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                LDS_PTR(s16x4, sb + r * SB + ((c8 ^ kn_swz<SB>(r)) * 8)));
+            const elem4 vb = __builtin_bit_cast(elem4, v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bfr[ks][j][4 * h + e] = vb[e];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * TN + j * 16 + fr;
+          bfr[ks][j] = *reinterpret_cast<const __attribute__((address_space(3))) elem8*>(sb + r * 128 + ((c ^ (r & 7)) << 4));
+        }
+      }
+    }
+  };
+  auto mfma_half = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = DCG_MFMA_16x16x32(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+  };
+
+  if constexpr (PP) {
+    // ================================================================ ping-pong K loop
+    // 8 waves in two groups of 4 (G0 = waves 0-3 = the tile's first BM/2 rows, G1 = the rest);
+    // waves w and w + 4 share a SIMD. Every k-tile t is two barrier-separated phases:
+    //   P0(t): G0 runs its MFMAs of tile t (fragments already in registers) while G1 issues its
+    //          half of the LDS-DMA of tile t + NS - 1 and reads its fragments of tile t;
+    //   P1(t): G1 runs its MFMAs of tile t while G0 issues its half of tile t + NS and reads its
+    //          fragments of tile t + 1.
+    // So each SIMD's matrix pipe alternates between its two waves while the partner loads
+    // (MI355X_MICROARCH.md "Two waves per SIMD"; cdna_hip_programming.md §5 8-phase template).
+    // Each group DMAs its own A rows and half of the shared B tile. Tile u lands in slot u % NS;
+    // that slot was last read by G1 in P0(u - NS) and by G0 in P1(u - NS - 1), so G0 may refill it
+    // from P1(u - NS) on, G1 from its next load phase P0(u - NS + 1) (NS = 2: G1 refills it in its
+    // compute phase P1(u - NS), between its two MFMA halves). Every wave waits for its own pieces
+    // of tile t + 1 at the end of P0(t) with a counted vmcnt (younger tiles stay in flight); the
+    // barrier then publishes the tile to G0's reads in P1(t) and G1's in P0(t + 1).
+    // Addressing is hoisted: per-piece byte offsets (with bounds folded in) are computed once per
+    // tap; a k-tile adds one scalar term per piece.
+    static_assert(NW == 8 && NPA % 8 == 0 && NPB % 8 == 0, "ping-pong: 8 waves, whole pieces per group wave");
+    static_assert(!PL, "ping-pong: conv / deconv modes only (Kc % 64 == 0, host-checked)");
+    constexpr int PA = NPA / 8, PB = NPB / 8;  // pieces per wave per tile (its group's half)
+    constexpr int L = PA + PB;
+    constexpr uint32_t BAD = 0xFFF00000u;      // invalid piece: past every descriptor, + <1 MiB per tile
+    const int grp = wave >> 2, lw = wave & 3;
+    int a_base[PA], a_iy[PA], a_ix[PA];
+    bool a_ok[PA];
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int q = grp * (NPA / 2) + lw + 4 * i;
+      const int m = m0 + 8 * q + (lane >> 3);
+      a_ok[i] = m < M;
+      const uint32_t b = fdiv((uint32_t)m, ph.fd_hw);
+      const uint32_t rem = (uint32_t)m - b * (uint32_t)(ph.Hq * ph.Wq);
+      const uint32_t qy = fdiv(rem, ph.fd_w);
+      const uint32_t qx = rem - qy * (uint32_t)ph.Wq;
+      a_iy[i] = (int)qy * p.sstride + ph.iy0_off;
+      a_ix[i] = (int)qx * p.sstride + ph.ix0_off;
+      a_base[i] = (((int)b * p.H + a_iy[i]) * p.W + a_ix[i]) * Kc + a_chunk * 8;
+    }
+    uint32_t a_off[PA], b_off[PB];
+    int tap_ti = -1;
+    int cur_ti = kt0 / kt_per_tap;
+    int cur_c0 = (kt0 - cur_ti * kt_per_tap) * BK;
+    auto set_tap = [&]() {
+      const int ti = ph.tap[cur_ti];
+      const int dy = (int)(signed char)(ti & 0xff), dx = (int)(signed char)((ti >> 8) & 0xff), wt = ti >> 16;
+      const int delta = (dy * p.W + dx) * Kc;
+#pragma unroll
+      for (int i = 0; i < PA; ++i) {
+        const int iy = a_iy[i] + dy, ix = a_ix[i] + dx;
+        const bool ok = a_ok[i] && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        a_off[i] = ok ? (uint32_t)(a_base[i] + delta) * 2u : BAD;
+      }
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        const int q = grp * (NPB / 2) + lw + 4 * i;
+        if constexpr (BKN) {
+          const int rr = q * B_ROWS_PER_PIECE + lane / (SB / 16);
+          const int n = n0 + ((lane % (SB / 16)) ^ (kn_swz<SB>(rr) >> 1)) * 8;
+          b_off[i] = n < N ? (uint32_t)((wt * Kc + rr) * N + n) * 2u : BAD;
+        } else {
+          const int n = n0 + 8 * q + (lane >> 3);
+          b_off[i] = n < N ? (uint32_t)((wt * N + n) * Kc + a_chunk * 8) * 2u : BAD;
+        }
+      }
+      tap_ti = cur_ti;
+    };
+    auto issue = [&](int slot) {
+      if (tap_ti != cur_ti) set_tap();
+      const uint32_t sa = lds_base + slot * STAGE;
+      const uint32_t sb = sa + A_BYTES;
+      const uint32_t ca = (uint32_t)cur_c0 * 2u, cb = BKN ? (uint32_t)(cur_c0 * N) * 2u : ca;
+#pragma unroll
+      for (int i = 0; i < PA; ++i) dma16_asm_la(ra, sa + (grp * (NPA / 2) + lw + 4 * i) * 1024, a_off[i] + ca);
+#pragma unroll
+      for (int i = 0; i < PB; ++i) dma16_asm_la(rb, sb + (grp * (NPB / 2) + lw + 4 * i) * 1024, b_off[i] + cb);
+      cur_c0 += BK;
+      if (cur_c0 >= Kc) { cur_c0 = 0; ++cur_ti; }
+    };
+    auto mfma_all = [&]() {
+      __builtin_amdgcn_s_setprio(1);
+      mfma_half(0);
+      mfma_half(1);
+      __builtin_amdgcn_s_setprio(0);
+    };
+
+    // prologue: G0 issues tiles 0..NS-1, G1 tiles 0..NS-2 (0..NS-1 at NS = 2)
+    const int pre = (grp == 0 || NS == 2) ? NS : NS - 1;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (s < pre && s < nk) issue(s);
+    if (nk > 0) {
+      wait_vmcnt_n<L, NS - 1>(min(min(nk, pre) - 1, NS - 1));  // tile 0 landed (this wave's pieces)
+      pp_barrier();
+      if (grp == 0) read_frags(0);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      // ---- P0(kt)
+      if (grp == 0) {
+        mfma_all();
+      } else {
+        if (NS > 2 && kt + NS - 1 < nk) issue((kt + NS - 1) % NS);
+        read_frags(kt % NS);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      // tile kt+1 landed for this wave; the younger tiles issued so far stay in flight
+      if (kt + 1 < nk) wait_vmcnt_n<L, NS - 2>(min(NS - 2, nk - 2 - kt));
+      pp_barrier();
+      // ---- P1(kt)
+      if (grp == 1) {
+        __builtin_amdgcn_s_setprio(1);
+        mfma_half(0);
+        if (NS == 2 && kt + NS < nk) issue((kt + NS) % NS);
+        mfma_half(1);
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+        if (kt + NS < nk) issue((kt + NS) % NS);
+        if (kt + 1 < nk) read_frags((kt + 1) % NS);
+      }
+      pp_barrier();
+    }
+  } else {
   // ---- A rows of this lane: piece q = wave + 4 i, row = 8 q + lane / 8, slot = lane & 7,
   //      global 16-byte chunk = slot ^ (row & 7)
-  const int a_chunk = (lane & 7) ^ (lane >> 3);
   int a_base[PPW_A], a_iy[PPW_A], a_ix[PPW_A];
   bool a_ok[PPW_A];
 #pragma unroll
@@ -222,17 +413,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     if (cur_c0 >= Kc) { cur_c0 = 0; ++cur_ti; }
   };
 
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk && !(ablate & 8)) issue(s);
 
-  const int fr = lane & 15, fq = lane >> 4;
   const int g4 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
   if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memtime();
   for (int kt = 0; kt < nk; ++kt) {
@@ -292,6 +476,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
           acc[i][j] = DCG_MFMA_16x16x32(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   }
+  }  // classic K loop
 
   if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memtime();
   // ------------------------------------------------------------------ split-K hand-off
@@ -351,7 +536,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   float* red = reinterpret_cast<float*>(lds) + BM;
   constexpr int CPAD = BN + 8;
   elem_t* ctile = reinterpret_cast<elem_t*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
-  static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= NS * STAGE, "epilogue LDS");
+  constexpr int LDS_TOTAL = igemm3_lds_bytes<BM, BN, WM, NS>();
+  static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= LDS_TOTAL, "epilogue LDS");
   for (int r = tid; r < BM; r += NT) {
     const int m = m0 + r;
     int off = -1;
@@ -380,8 +566,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     // row-lane scratch (64 * NT bytes) after the C tile, or -- when that does not fit (8-wave
     // tiles at NS = 2) -- over the C tile, written after a barrier once the store pass read it
     constexpr int kEpi = (BM + 2 * WM * BN) * 4, kCt = BM * CPAD * 2, kRed2 = 64 * NT;
-    constexpr bool kSep = kEpi + kCt + kRed2 <= NS * STAGE;
-    constexpr bool kAlias = !kSep && kEpi + (kCt > kRed2 ? kCt : kRed2) <= NS * STAGE;
+    constexpr bool kSep = kEpi + kCt + kRed2 <= LDS_TOTAL;
+    constexpr bool kAlias = !kSep && kEpi + (kCt > kRed2 ? kCt : kRed2) <= LDS_TOTAL;
     if constexpr (kSep || kAlias) {
       __syncthreads();
       float* red2 = reinterpret_cast<float*>(reinterpret_cast<char*>(ctile) + (kSep ? kCt : 0));
@@ -431,53 +617,64 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
 // NS = 2 -> 210..219, NS = 4 -> 220..229, NS = 5 -> 230..239). Deeper rings keep more k-tiles of
 // LDS-DMA in flight (issue -> landed is ~1.1 us, several k-tiles of MFMA work), at the cost of
 // workgroups per CU (160 KiB of LDS per CU).
-// ids 6..8: 8-wave workgroups (512 threads, 64x64 per wave): bigger tiles load fewer operand
-// bytes per MFMA (the K loop is bound by the LDS-DMA fill rate, profiles/r2/igemm3_ablations_r2.txt)
+// ids 6..9: 8-wave workgroups (512 threads): bigger tiles load fewer operand bytes per MFMA (the
+// K loop is bound by the LDS-DMA fill rate, profiles/r2/igemm3_ablations_r2.txt).
+// cfg 240..259: the ping-pong K loop (PP) on the 8-wave tiles, NS = 3 (240..249) or 2 (250..259).
 #define DCG_IGEMM3_TILES(X) \
   X(0, 128, 128, 2, 2) X(1, 256, 64, 4, 1) X(2, 64, 256, 1, 4) X(3, 128, 64, 2, 2) \
-  X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2) X(6, 256, 128, 4, 2) X(7, 128, 256, 2, 4) X(8, 512, 64, 8, 1)
+  X(4, 64, 128, 2, 2) X(5, 64, 64, 2, 2) X(6, 256, 128, 4, 2) X(7, 128, 256, 2, 4) X(8, 512, 64, 8, 1) \
+  X(9, 256, 256, 4, 2)
 
-static constexpr int kIgemm3Stages[4] = {3, 2, 4, 5};
+static constexpr int kIgemm3Stages[6] = {3, 2, 4, 5, 3, 2};
 
 extern "C" int DCG_API(dcg_igemm3_tile)(int cfg, int* bm, int* bn, int* ns) {
-  if (cfg < 200 || cfg >= 240) return -1;
+  if (cfg < 200 || cfg >= 260) return -1;
   const int id = cfg % 10;
+  if (cfg >= 240 && id < 6) return -1;  // ping-pong: 8-wave tiles only
   *ns = kIgemm3Stages[(cfg - 200) / 10];
 #define X(id_, BM_, BN_, WM_, WN_) \
-  if (id == id_) { *bm = BM_; *bn = BN_; return (size_t)*ns * (BM_ + BN_) * 128 <= 160 * 1024 ? 0 : -1; }
+  if (id == id_) {                                                                                 \
+    *bm = BM_; *bn = BN_;                                                                          \
+    const size_t epi = (BM_ + 2 * WM_ * BN_) * 4 + BM_ * (BN_ + 8) * 2;                            \
+    return (size_t)*ns * (BM_ + BN_) * 128 <= 160 * 1024 && epi <= 160 * 1024 ? 0 : -1;           \
+  }
   DCG_IGEMM3_TILES(X)
 #undef X
   return -1;
 }
 
-template <int BM, int BN, int WM, int WN, int BKN, int NS>
-static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
-  constexpr size_t shm = (size_t)NS * (BM + BN) * 64 * 2;
-  // plain (im2col'd) GEMMs read their weight k-major only (the host never asks otherwise)
-  if constexpr (BKN) {
-    if (a->plain) {
-      auto k = dcg::igemm3_kernel<BM, BN, WM, WN, 1, NS, 1>;
-      static bool attr_set = false;
-      if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        if (e != hipSuccess) return (int)e;
-        attr_set = true;
-      }
-      hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), shm, s, *a);
-      return (int)hipGetLastError();
-    }
-  } else {
-    if (a->plain) return -1;
-  }
-  auto k = dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS, 0>;
+template <typename K>
+static int launch_k(K k, size_t shm, unsigned blocks, unsigned threads, const dcg::IGemmArgs* a, hipStream_t s) {
+  // one attribute call per instantiation (the maximum dynamic LDS of the kernel)
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), shm, s, *a);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), shm, s, *a);
   return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN, int BKN, int NS, int PP>
+static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
+  constexpr size_t shm = (size_t)dcg::igemm3_lds_bytes<BM, BN, WM, NS>();
+  constexpr unsigned nt = 64 * WM * WN;
+  if constexpr (PP) {
+    if constexpr (WM * WN == 8) {
+      if (a->plain || a->Kc % 64) return -1;  // conv / deconv with whole 64-channel k-tiles only
+      return launch_k(dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS, 0, 1>, shm, blocks, nt, a, s);
+    }
+    return -1;
+  } else {
+    // plain (im2col'd) GEMMs read their weight k-major only (the host never asks otherwise)
+    if constexpr (BKN) {
+      if (a->plain) return launch_k(dcg::igemm3_kernel<BM, BN, WM, WN, 1, NS, 1>, shm, blocks, nt, a, s);
+    } else {
+      if (a->plain) return -1;
+    }
+    return launch_k(dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS, 0>, shm, blocks, nt, a, s);
+  }
 }
 
 extern "C" int DCG_API(dcg_igemm3_threads)(int cfg) {
@@ -488,32 +685,31 @@ extern "C" int DCG_API(dcg_igemm3_threads)(int cfg) {
   return 256;
 }
 
+template <int BM, int BN, int WM, int WN, int NS, int PP>
+static int launch3_ns(const dcg::IGemmArgs* a, int bkn, unsigned blocks, hipStream_t s) {
+  if constexpr ((size_t)NS * (BM + BN) * 128 <= 160 * 1024)
+    return bkn ? launch3<BM, BN, WM, WN, 1, NS, PP>(a, blocks, s) : launch3<BM, BN, WM, WN, 0, NS, PP>(a, blocks, s);
+  return -1;
+}
+
 extern "C" int DCG_API(dcg_igemm3_launch)(const dcg::IGemmArgs* a, int cfg, int bkn, unsigned blocks, hipStream_t s) {
   int bm, bn, ns;
   if (DCG_API(dcg_igemm3_tile)(cfg, &bm, &bn, &ns)) return -1;
   const int id = cfg % 10;
+  const bool pp = cfg >= 240;
 #define X(id_, BM_, BN_, WM_, WN_)                                                              \
   if (id == id_) {                                                                              \
-    if (ns == 3) {                                                                              \
-      if constexpr ((size_t)3 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
-        return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 3>(a, blocks, s)                            \
-                   : launch3<BM_, BN_, WM_, WN_, 0, 3>(a, blocks, s);                           \
+    if (pp) {                                                                                   \
+      if constexpr (WM_ * WN_ == 8) {                                                           \
+        if (ns == 3) return launch3_ns<BM_, BN_, WM_, WN_, 3, 1>(a, bkn, blocks, s);            \
+        return launch3_ns<BM_, BN_, WM_, WN_, 2, 1>(a, bkn, blocks, s);                         \
+      }                                                                                         \
       return -1;                                                                                \
     }                                                                                           \
-    if (ns == 4) {                                                                              \
-      if constexpr ((size_t)4 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
-        return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 4>(a, blocks, s)                            \
-                   : launch3<BM_, BN_, WM_, WN_, 0, 4>(a, blocks, s);                           \
-      return -1;                                                                                \
-    }                                                                                           \
-    if (ns == 5) {                                                                              \
-      if constexpr ((size_t)5 * (BM_ + BN_) * 128 <= 160 * 1024)                                \
-        return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 5>(a, blocks, s)                            \
-                   : launch3<BM_, BN_, WM_, WN_, 0, 5>(a, blocks, s);                           \
-      return -1;                                                                                \
-    }                                                                                           \
-    return bkn ? launch3<BM_, BN_, WM_, WN_, 1, 2>(a, blocks, s)                                \
-               : launch3<BM_, BN_, WM_, WN_, 0, 2>(a, blocks, s);                               \
+    if (ns == 3) return launch3_ns<BM_, BN_, WM_, WN_, 3, 0>(a, bkn, blocks, s);                \
+    if (ns == 4) return launch3_ns<BM_, BN_, WM_, WN_, 4, 0>(a, bkn, blocks, s);                \
+    if (ns == 5) return launch3_ns<BM_, BN_, WM_, WN_, 5, 0>(a, bkn, blocks, s);                \
+    return launch3_ns<BM_, BN_, WM_, WN_, 2, 0>(a, bkn, blocks, s);                             \
   }
   DCG_IGEMM3_TILES(X)
 #undef X

@@ -70,13 +70,24 @@ CU_COUNT = 256
 IGEMM_CFGS = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (32, 64), 5: (64, 32),
               6: (32, 32), 7: (128, 16), 8: (64, 16), 9: (256, 64)}
 IGEMM3_TILES = {0: (128, 128), 1: (256, 64), 2: (64, 256), 3: (128, 64), 4: (64, 128), 5: (64, 64),
-                6: (256, 128), 7: (128, 256), 8: (512, 64)}  # 6..8: 8-wave (512-thread) workgroups
-IGEMM3_WAVES = {6: 8, 7: 8, 8: 8}
-IGEMM3_WM = {0: 2, 1: 4, 2: 1, 3: 2, 4: 2, 5: 2, 6: 4, 7: 2, 8: 8}  # waves along M (igemm3.hip tiles)
-IGEMM3_STAGES = (3, 2, 4, 5)  # LDS stages of igemm3 cfg 200+10k+id
+                6: (256, 128), 7: (128, 256), 8: (512, 64), 9: (256, 256)}  # 6..9: 8-wave (512-thread) workgroups
+IGEMM3_WAVES = {6: 8, 7: 8, 8: 8, 9: 8}
+IGEMM3_WM = {0: 2, 1: 4, 2: 1, 3: 2, 4: 2, 5: 2, 6: 4, 7: 2, 8: 8, 9: 4}  # waves along M (igemm3.hip tiles)
+# LDS stages of igemm3 cfg 200+10k+id; k = 4, 5 (cfg 240..259): the ping-pong K loop (8-wave tiles,
+# conv / deconv modes with Kc % 64 == 0)
+IGEMM3_STAGES = (3, 2, 4, 5, 3, 2)
+
+
+def igemm3_pp_ok(cfg: int, mode: int, Kc: int) -> bool:
+    """Whether igemm3 cfg can run this GEMM: the ping-pong configs (240..259) need an 8-wave tile
+    and whole 64-channel k-tiles of a conv / deconv (no im2col plain mode)."""
+    if cfg < 240:
+        return True
+    return cfg % 10 in IGEMM3_WAVES and mode != 2 and Kc % 64 == 0
 
 
 def igemm3_lds(cfg: int) -> int:
+    """Operand-ring bytes of igemm3 cfg (the launch adds room when the epilogue needs more)."""
     bm, bn = IGEMM3_TILES[cfg % 10]
     return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
 
@@ -87,7 +98,7 @@ IGEMM_F32_TILES = {200: (64, 64), 201: (128, 64), 202: (64, 16), 203: (128, 128)
 
 def tile_of(cfg: int, dtype: int = 0) -> Tuple[int, int]:
     """(BM, BN) of an igemm cfg: 0..9 (+100 LDS-DMA) igemm.hip, 200..239 igemm3.hip; dtype 2
-    (fp32): igemm_f32.hip."""
+    (fp32): igemm_f32.hip; 240..259 igemm3's ping-pong K loop."""
     if dtype == 2:
         return IGEMM_F32_TILES[cfg]
     if cfg >= 200:
@@ -120,7 +131,8 @@ def bnb_fits(cfg: int) -> bool:
     nt = 64 * IGEMM3_WAVES.get(cfg % 10, 4)
     wm = IGEMM3_WM[cfg % 10]
     # igemm3: the row-lane scratch may alias the C tile (the store pass has read it by then)
-    return (bm + 2 * wm * bn) * 4 + max(bm * (bn + 8) * 2, 64 * nt) <= ns * (bm + bn) * 128
+    lds = max(ns * (bm + bn) * 128, (bm + 2 * wm * bn) * 4 + bm * (bn + 8) * 2)  # igemm3_lds_bytes
+    return (bm + 2 * wm * bn) * 4 + max(bm * (bn + 8) * 2, 64 * nt) <= lds
 
 
 WGRAD_CFGS = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64), 4: (32, 64), 5: (64, 32), 6: (32, 32)}
@@ -216,7 +228,7 @@ def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wo
     ent = tuned_table().get("%d,%d,%d,%d,%d,%d,%d,%d" % (mode, Bn, Hin, Win, Kc, Hout, Wout, N))
     if ent is not None:
         cfg, sp = ent
-        ok = cfg >= 200 or (not bkn and sp == 1 and cfg % 100 in IGEMM_CFGS)
+        ok = (cfg >= 200 and igemm3_pp_ok(cfg, mode, Kc)) or (not bkn and sp == 1 and cfg % 100 in IGEMM_CFGS)
         if ok and (rows_per_group is None or rows_per_group % tile_of(cfg)[0] == 0):
             return cfg, sp
     if N % 8 == 0 and N >= 64:

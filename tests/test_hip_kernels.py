@@ -160,6 +160,63 @@ def test_igemm3_conv_all_tiles_layouts_splits(bkn):
                 assert torch.equal(y, y2) and torch.equal(st, st2), "nondeterministic " + tag
 
 
+# ping-pong K loop (240..259) and the deep rings (NS 4 / 5: 220..239, whose tail waits were once
+# wrong): split counts that give every k-split length from 1 to 6 and the full 50 k-tiles
+DEEP = [220, 223, 225, 226, 230, 233, 235]
+PP = [246, 247, 256, 257, 258]
+SPLITS_TAIL = (1, 9, 10, 13, 17, 25, 50)
+
+
+@pytest.mark.parametrize("bkn", [0, 1])
+@pytest.mark.parametrize("cfg", DEEP + PP)
+def test_igemm3_pipeline_tails(cfg, bkn):
+    """Pipeline prologue / tail of the deep-ring and ping-pong K loops: every number of k-tiles
+    per split from 1 to NS + 1 (and 50), both weight layouts, fused lrelu + BN statistics,
+    against the fp32 reference; split results bitwise reproducible."""
+    h = H()
+    B, Hs, Ci, Co = 4, 16, 128, 256
+    if h.igemm3_lds(cfg) > 160 * 1024:
+        pytest.skip("tile does not fit the LDS at this depth")
+    x = bf(rnd(B, Hs, Hs, Ci, seed=140))
+    w = bf(rnd(5, 5, Ci, Co, scale=0.05, seed=141))
+    wt = h.pack_conv_weight(w.float(), "conv", "fwd")
+    ref_pre = R.conv2d_same(x.float(), w.float())
+    wp = w.reshape(25, Ci, Co).contiguous() if bkn else wt
+    for splits in SPLITS_TAIL:
+        y, st = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn), splits=splits)
+        tag = "cfg%d bkn%d s%d" % (cfg, bkn, splits)
+        close(y, R.lrelu(ref_pre), 1.5e-2, tag)
+        s = st.sum(0)
+        close(s[0], ref_pre.reshape(-1, Co).sum(0), 2e-3, "sum " + tag)
+        close(s[1], ref_pre.reshape(-1, Co).pow(2).sum(0), 2e-3, "sumsq " + tag)
+        y2, st2 = h.conv2d_same(x, wp, Co, act="lrelu", stats=True, cfg=cfg, bkn=bool(bkn), splits=splits)
+        assert torch.equal(y, y2) and torch.equal(st, st2), "nondeterministic " + tag
+
+
+@pytest.mark.parametrize("cfg", PP)
+def test_igemm3_pingpong_deconv_dgrad_bnb(cfg):
+    """Ping-pong K loop on the other GEMMs of the step: the 4-phase transposed conv (9/6/6/4 taps),
+    the G data gradient (k-major weight) and the fused BN-backward statistics store pass."""
+    h = H()
+    B, Hi, Ho, Ci, Co = 8, 8, 16, 128, 128
+    x = bf(rnd(B, Hi, Hi, Ci, seed=142))
+    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=143))
+    bias = rnd(Co, scale=0.1, seed=144)
+    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
+    for splits in (1, 2, 5):
+        y = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True, cfg=cfg,
+                                    splits=splits)
+        close(y, ref, 2e-3, "deconv cfg%d s%d" % (cfg, splits))
+    xd = rnd(B, Hi, Hi, Ci, seed=145).requires_grad_(True)
+    yd = R.conv2d_transpose_same(xd, w.float(), (Ho, Ho))
+    dy = bf(rnd(B, Ho, Ho, Co, seed=146))
+    (gx,) = torch.autograd.grad(yd, xd, dy.float())
+    for splits in (1, 4):
+        out = h.conv2d_same(dy, w.reshape(25, Co, Ci), Ci, out_f32=True, cfg=cfg, bkn=True, splits=splits)
+        close(out, gx, 2e-3, "G dgrad cfg%d s%d" % (cfg, splits))
+    test_igemm_fused_bn_backward_stats(cfg)
+
+
 @pytest.mark.parametrize("B,Hi,Ho,Ci,Co", [(8, 4, 8, 256, 128), (2, 4, 7, 64, 64), (4, 8, 16, 128, 64)])
 def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
     h = H()

@@ -51,15 +51,13 @@ def test_checker_finds_the_round1_adam_race():
 
     def round1_order(ex):                # ... issued before the cs <- D-chain join
         cs, alt = ex.main(), ex.alt[0]
-        eng._seg(ex, 0, cs)
+        ex.run(eng.progA, [cs, ex.side], 0, eng._a_fwd)
         ex.wait(alt, cs)
-        eng._seg(ex, 1, alt)
-        eng._seg(ex, 2, cs)
-        eng._seg(ex, 3, alt)
-        eng._seg(ex, 4, cs)
-        eng._seg(ex, 5, cs)
+        ex.run(eng.progB, ex.alt)
+        ex.run(eng.progA, [cs, ex.side], eng._a_fwd, -1)
+        ex.run(eng.progW, [cs, ex.side])
+        ex.run(eng.progC, [cs, ex.side], 0, eng._c_split)
         ex.wait(cs, alt)
-        eng._seg(ex, 6, cs)
 
     eng._run_step = round1_order
     hz, _ = SC.check_engine(eng)
@@ -158,3 +156,39 @@ def test_fused_g_wgrad_tail_on_main_rejects_bad_values(monkeypatch):
     eng = _dry()
     with pytest.raises(ValueError):
         eng._gw_tail_on_main()
+
+
+@pytest.mark.parametrize("gcut", ["-1", "0", "1", "2"])
+@pytest.mark.parametrize("tail", ["0", "2", "4"])
+def test_concurrent_ddp_cuts_have_no_hazards(monkeypatch, gcut, tail):
+    """The segmented DDP step for every G-chain cut of its first backward graph
+    (DCGAN_DDP_GCUT) and every trailing-G-wgrad placement (DCGAN_GW_TAIL_ON_MAIN)."""
+    monkeypatch.setenv("DCGAN_DDP_GCUT", gcut)
+    monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", tail)
+    eng = _dry(world=2)
+    assert eng._schedule() == "concurrent"
+    p = eng._concurrent_plan()
+    assert sorted(p["alt_pieces"] + p["cs_pieces"]) == list(range(len(eng._g_w)))
+    hz, n_ops = SC.check_engine(eng)
+    assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_an_early_g_hi_bucket():
+    """Segmented DDP: issuing the all-reduce of G's deconv layers after the first backward graph
+    (before bwd_b computes their weight gradients) is a race the checker reports."""
+    eng = _dry(world=2)
+
+    def early(ex):
+        cs = ex.main()
+        eng._seg(ex, 0, cs)
+        eng._ar_launch(ex, "g_hi", cs)   # too early
+        eng._seg(ex, 1, cs)
+        eng._seg(ex, 2, cs)
+        eng._ar_join(ex, cs)
+        eng._seg(ex, 3, cs)
+        eng._seg(ex, 4, cs)
+
+    eng._run_step = early
+    hz, _ = SC.check_engine(eng)
+    assert any("allreduce" in h.a or "allreduce" in h.b for h in hz), hz
