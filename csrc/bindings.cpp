@@ -701,15 +701,20 @@ class Program {
   }
   int adam(std::string name, uintptr_t w, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers, size_t n, float lr,
            float b1, float b2, float eps, float gscale, int stream) {
-    return adam_bf(name, w, 0, g, m, v, powers, n, lr, b1, b2, eps, gscale, stream, 0);
+    return adam_bf(name, w, 0, g, m, v, powers, n, lr, b1, b2, eps, gscale, stream, 0, 0);
   }
-  // + elem_t mirror of the updated weights (same flat layout)
+  // + elem_t mirror of the updated weights (same flat layout); gbf: read the gradient from this
+  // bf16 buffer (the all-reduced bf16 wire of the DDP step) instead of g
   int adam_bf(std::string name, uintptr_t w, uintptr_t wbf, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t powers,
-              size_t n, float lr, float b1, float b2, float eps, float gscale, int stream, uintptr_t ls) {
+              size_t n, float lr, float b1, float b2, float eps, float gscale, int stream, uintptr_t ls, uintptr_t gbf) {
+    AccList acc;
+    acc.w(w, n * 4).w(wbf, n * es_).w(m, n * 4).w(v, n * 4).r(powers, 8).r(ls, 12);
+    if (gbf) acc.r(gbf, n * 2);
+    else acc.r(g, n * 4);
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_adam)(P<float>(w), P<elem_t>(wbf), P<const float>(g), P<float>(m), P<float>(v), P<const float>(powers),
-                      n, lr, b1, b2, eps, gscale, P<const float>(ls), s);
-    }, AccList().w(w, n * 4).w(wbf, n * es_).r(g, n * 4).w(m, n * 4).w(v, n * 4).r(powers, 8).r(ls, 12).v);
+                      n, lr, b1, b2, eps, gscale, P<const float>(ls), P<const void>(gbf), s);
+    }, acc.v);
   }
   // both TF-Adams (A first) + beta powers / step counter in one launch (see adam2_kernel)
   int adam2(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA, uintptr_t pA,
@@ -1007,7 +1012,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("adam", &Program::adam)
       .def("adam_bf", &Program::adam_bf, py::arg("name"), py::arg("w"), py::arg("wbf"), py::arg("g"), py::arg("m"),
            py::arg("v"), py::arg("powers"), py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
-           py::arg("gscale"), py::arg("stream"), py::arg("ls") = 0)
+           py::arg("gscale"), py::arg("stream"), py::arg("ls") = 0, py::arg("gbf") = 0)
       .def("step_end", &Program::step_end, py::arg("name"), py::arg("pd"), py::arg("pg"), py::arg("b1d"),
            py::arg("b2d"), py::arg("b1g"), py::arg("b2g"), py::arg("step"), py::arg("stream"), py::arg("ls") = 0,
            py::arg("growth_interval") = 2000)

@@ -502,8 +502,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const elem_t* __restrict_
 
 // ---------------------------------------------------------------- TF Adam
 // lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from device powers (= b^t); w -= lr_t*m/(sqrt(v)+eps)
+// GW = bf16: the gradient is read from the all-reduced bf16 wire buffer (DDP with a bf16 wire:
+// no bf16 -> fp32 copy-back after the collective; the values are the same)
+template <typename GW>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, elem_t* __restrict__ wbf,
-                                                   const float* __restrict__ g, float* __restrict__ m,
+                                                   const GW* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, const float* __restrict__ powers, size_t n,
                                                    float lr, float b1, float b2, float eps, float gscale,
                                                    const float* __restrict__ ls) {
@@ -518,7 +521,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, elem_t
   const float lr_t = lr * sqrtf(1.f - powers[1]) / (1.f - powers[0]);
   const size_t n4 = n / 4;
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i] * gscale;
+    f32x4 gv;
+    if constexpr (sizeof(GW) == 4) {
+      gv = reinterpret_cast<const f32x4*>(g)[i] * gscale;
+    } else {
+      typedef GW gw4 __attribute__((ext_vector_type(4)));
+      const gw4 gb = reinterpret_cast<const gw4*>(g)[i];
+      gv = (f32x4){(float)gb[0], (float)gb[1], (float)gb[2], (float)gb[3]} * gscale;
+    }
     f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
     f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
     f32x4 wv = reinterpret_cast<f32x4*>(w)[i];
@@ -535,7 +545,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, elem_t
     }
   }
   for (size_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const float gv = g[i] * gscale;
+    const float gv = (float)g[i] * gscale;
     m[i] = b1 * m[i] + (1.f - b1) * gv;
     v[i] = b2 * v[i] + (1.f - b2) * gv * gv;
     w[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps);
@@ -878,9 +888,13 @@ extern "C" int DCG_API(dcg_sum_vec)(const float* v, int n, float* out, hipStream
 
 extern "C" int DCG_API(dcg_adam)(float* w, elem_t* wbf, const float* g, float* m, float* v, const float* powers,
                                   size_t n, float lr, float b1, float b2, float eps, float gscale, const float* ls,
-                                  hipStream_t s) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, wbf, g, m, v, powers, n, lr, b1, b2,
-                     eps, gscale, ls);
+                                  const void* g_bf16, hipStream_t s) {
+  if (g_bf16)
+    hipLaunchKernelGGL(adam_kernel<__bf16>, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, wbf,
+                       static_cast<const __bf16*>(g_bf16), m, v, powers, n, lr, b1, b2, eps, gscale, ls);
+  else
+    hipLaunchKernelGGL(adam_kernel<float>, dim3(grid_for(n / 4 + 1)), dim3(256), 0, s, w, wbf, g, m, v, powers, n, lr,
+                       b1, b2, eps, gscale, ls);
   return (int)hipGetLastError();
 }
 

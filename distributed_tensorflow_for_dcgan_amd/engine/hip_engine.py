@@ -173,6 +173,12 @@ class HipEngine:
         self._graphs: List[Optional[torch.cuda.CUDAGraph]] = []
         self.comm_stream = torch.cuda.Stream(device=device) if (self.ddp and not self.dry) else None
         self.allreduce_dtype = allreduce_dtype
+        # bf16 wire of the segmented DDP step (bf16 engine): flat bf16 gradient images that cast
+        # kernels inside the step graphs fill, RCCL reduces in place and Adam reads directly
+        self.wire_d = self.wire_g = None
+        if self.ddp and allreduce_dtype == "bf16" and self.dt == 0:
+            self.wire_d = self.model.d.like(torch.bfloat16)
+            self.wire_g = self.model.g.like(torch.bfloat16)
         self.bucket_mb = bucket_mb
         self._exec = None
         self._alloc()
@@ -289,6 +295,17 @@ class HipEngine:
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
         self._g_cuts = self._g_bucket_cuts()
         self._g_split = self._g_split_plan()
+        self.progX, self._wire_ops = self._prog(), {}
+        if self.wire_d is not None:  # fp32 gradient slice -> its bf16 wire image, one op per collective
+            lo = self._g_split[3] if self._g_split is not None else 0
+            o = self._d_top_off
+            nd, ng = self.grad_d.flat.numel(), self.grad_g.flat.numel()
+            for name, src, dst, a, b in (("dtop", self.grad_d, self.wire_d, o, nd), ("drest", self.grad_d, self.wire_d, 0, o),
+                                         ("g_hi", self.grad_g, self.wire_g, lo, ng), ("g_lo", self.grad_g, self.wire_g, 0, lo)):
+                if b > a:
+                    self._wire_ops[name] = self.progX.size()
+                    self.progX.cast_to_bf16("wire." + name, _p(src.flat) + 4 * a, 0, _p(dst.flat) + 2 * a, b - a,
+                                            1.0, 0.0, 0)
         self.progCast = self._prog()  # fp32 masters -> 16-bit mirrors (init / checkpoint load)
         if not self.f32:
             for ps, pb in ((self.model.d, self.wbf_d), (self.model.g, self.wbf_g)):
@@ -325,11 +342,12 @@ class HipEngine:
         ls = _p(self.loss_scale)
         mg = 0 if self.f32 else _p(self.wbf_g.flat)
         md = 0 if self.f32 else _p(self.wbf_d.flat)
+        wd, wg = (_p(self.wire_d.flat), _p(self.wire_g.flat)) if self._wire_direct() else (0, 0)
         prog.adam_bf("adam_d", _p(self.model.d.flat), md, _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
-                     _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0, ls)
+                     _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0, ls, wd)
         self._c_split = prog.size()
         prog.adam_bf("adam_g", _p(self.model.g.flat), mg, _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
-                     _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0, ls)
+                     _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0, ls, wg)
         prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
                       _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
 
@@ -1036,6 +1054,7 @@ class HipEngine:
             ex.run(A, [cs, sec], 0, self._a_fwd)
             ex.wait(alt, cs)
             ex.run(B, ex.alt, 0, self._b_split)
+            self._wire_cast(ex, "dtop", ex.alt)
             ex.run(A, [cs, sec], self._a_fwd, p["g_cut"])
             ex.wait(cs, alt)
 
@@ -1058,9 +1077,12 @@ class HipEngine:
             for k in p["cs_pieces"]:
                 ex.run(W, [cs, sec], self._w_begin(k), self._g_w[k][1])
             ex.wait(cs, alt)
+            self._wire_cast(ex, "drest", [cs, sec])
+            self._wire_cast(ex, "g_hi", [cs, sec])
 
         def g_tail(ex, cs, sec):
             ex.run(A, [cs, sec], p["a_end"], -1)
+            self._wire_cast(ex, "g_lo", [cs, sec])
         g_tail.empty = p["a_end"] >= A.size()
         bwd_a.empty = bwd_b.empty = False
         return [("bwd_a", bwd_a, M), ("bwd_b", bwd_b, M), ("G_tail", g_tail, M),
@@ -1073,6 +1095,18 @@ class HipEngine:
                 ex.run(prog, [cs, sec], b, e)
         run.empty = all((prog.size() if e < 0 else e) <= b for prog, b, e in parts)
         return run
+
+    def _wire_direct(self) -> bool:
+        """bf16 wire without copies (segmented DDP step, bf16 engine): cast kernels inside the
+        step graphs write each gradient slice's bf16 image when the slice is final, RCCL reduces
+        the image in place, Adam reads it (``adam_bf(gbf=...)``). Other schedules / dtypes use the
+        reducer's own fp32 <-> bf16 copies around each collective."""
+        return self.wire_d is not None and self._schedule() == "concurrent"
+
+    def _wire_cast(self, ex, name: str, streams) -> None:
+        if self._wire_direct() and name in self._wire_ops:
+            i = self._wire_ops[name]
+            ex.run(self.progX, streams, i, i + 1)
 
     def _w_begin(self, k: int) -> int:
         return self._g_w[k - 1][1] if k > 0 else 0
@@ -1326,16 +1360,22 @@ class HipEngine:
             o = self._d_top_off
             cs, mb, wd = self.comm_stream, self.bucket_mb, self.allreduce_dtype
             gf, df = self.grad_g.flat, self.grad_d.flat
-            mk = lambda t: D.GradAllReducer(t, mb, wd, stream=cs, force=True)  # noqa: E731
-            self._ar_dtop = mk(df[o:])
-            self._ar_drest = mk(df[:o])
+            direct = self._wire_direct()
+            wdf = self.wire_d.flat if direct else None
+            wgf = self.wire_g.flat if direct else None
+
+            def mk(t, wire=None):
+                return D.GradAllReducer(t, mb, wd, stream=cs, force=True, wire=wire, prefilled=wire is not None)
+
+            self._ar_dtop = mk(df[o:], wdf[o:] if direct else None)
+            self._ar_drest = mk(df[:o], wdf[:o] if direct else None)
             sch = self._schedule()
             if sch == "serial":
                 self._ar_g = mk(gf)
             elif sch == "concurrent":
                 lo = self._concurrent_plan()["lo"]
-                self._ar_g_hi = mk(gf[lo:])
-                self._ar_g_lo = mk(gf[:lo]) if lo > 0 else None
+                self._ar_g_hi = mk(gf[lo:], wgf[lo:] if direct else None)
+                self._ar_g_lo = mk(gf[:lo], wgf[:lo] if direct else None) if lo > 0 else None
             elif sch == "ddp":  # G's gradient in per-layer buckets (see _g_bucket_cuts)
                 self._ar_gparts = [mk(gf[lo:hi]) for _, lo, hi in self._g_cuts]
 

@@ -165,7 +165,7 @@ def check_engine(eng, steps: int = 2) -> Tuple[List[Hazard], int]:
 
 
 def check(cfg=None, batch_size: int = 8, dtype: str = "bf16", world: int = 1, schedule: Optional[str] = None,
-          timing: bool = False, steps: int = 2):
+          timing: bool = False, steps: int = 2, allreduce_dtype: str = "fp32"):
     """Build a dry-run engine on the CPU and check one schedule. Returns (schedule, hazards, ops)."""
     import torch
 
@@ -173,7 +173,7 @@ def check(cfg=None, batch_size: int = 8, dtype: str = "bf16", world: int = 1, sc
     from .hip_engine import HipEngine
     cfg = cfg or DCGANConfig()
     eng = HipEngine(cfg, batch_size, torch.device("cpu"), dtype=dtype, world=world, schedule=schedule, dry_run=True,
-                    graph=False)
+                    graph=False, allreduce_dtype=allreduce_dtype)
     if timing:
         eng._timing = True
         eng._build_updates()

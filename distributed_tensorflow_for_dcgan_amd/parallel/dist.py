@@ -178,11 +178,15 @@ class GradAllReducer:
     it and issues one all-reduce per bucket there (SUM); ``wait()`` makes the compute
     stream wait for the comm stream and applies the 1/W scale (folded into the Adam
     kernel on the HIP path via ``grad_scale``). With ``wire_dtype=bf16`` the buckets are
-    converted to bf16 for the wire (half the xGMI bytes) and back to fp32.
+    converted to bf16 for the wire (half the xGMI bytes) and back to fp32 -- unless the caller
+    hands in ``wire`` (a bf16 buffer it fills itself, e.g. from a cast kernel inside its step
+    graph) with ``prefilled=True``: then only the wire is all-reduced, and the consumer (the HIP
+    engine's Adam) reads the reduced bf16 values directly -- no copies around the collective.
     """
 
     def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 32.0, wire_dtype: str = "fp32",
-                 reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None, force: bool = False):
+                 reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None, force: bool = False,
+                 wire: Optional[torch.Tensor] = None, prefilled: bool = False):
         self.flat = flat_grad
         self.world = world_size()
         # collectives are issued when there is a peer -- or on a forced one-rank group
@@ -195,7 +199,12 @@ class GradAllReducer:
         # reducers of one engine share a comm stream: their collectives run in issue order
         self.stream = stream if stream is not None else (
             torch.cuda.Stream(device=flat_grad.device) if flat_grad.is_cuda else None)
-        self.wire = (torch.empty(flat_grad.numel(), dtype=torch.bfloat16, device=flat_grad.device)
+        self.prefilled = bool(prefilled)
+        if self.prefilled and (wire is None or wire_dtype != "bf16" or wire.numel() != flat_grad.numel()
+                               or wire.dtype != torch.bfloat16):
+            raise ValueError("prefilled needs a bf16 wire of the gradient's size")
+        self.wire = (wire if wire is not None else
+                     torch.empty(flat_grad.numel(), dtype=torch.bfloat16, device=flat_grad.device)
                      if wire_dtype == "bf16" else None)
         self._works = []
 
@@ -217,7 +226,9 @@ class GradAllReducer:
         if not self.active:
             return
         for s, e in self.buckets:
-            if self.wire is not None:
+            if self.prefilled:
+                dist.all_reduce(self.wire[s:e], op=dist.ReduceOp.SUM)
+            elif self.wire is not None:
                 w = self.wire[s:e]
                 w.copy_(self.flat[s:e])
                 dist.all_reduce(w, op=dist.ReduceOp.SUM)
@@ -227,7 +238,7 @@ class GradAllReducer:
 
     def accesses(self):
         """(ptr, bytes, is_write) ranges one issue() touches (schedule checker)."""
-        out = [(self.flat.data_ptr(), self.flat.numel() * self.flat.element_size(), True)]
+        out = [] if self.prefilled else [(self.flat.data_ptr(), self.flat.numel() * self.flat.element_size(), True)]
         if self.wire is not None:
             out.append((self.wire.data_ptr(), self.wire.numel() * self.wire.element_size(), True))
         return out
@@ -238,6 +249,8 @@ class GradAllReducer:
         if self.stream is not None:
             torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
         if scale_in_place:
+            if self.prefilled:
+                self.flat.copy_(self.wire)
             self.flat.mul_(1.0 / self.world)
 
 

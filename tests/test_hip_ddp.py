@@ -328,3 +328,42 @@ def test_bench_force_ddp_reports_rccl():
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
     assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 5
     assert res["n_gpus"] == 1 and res["value"] > 0
+
+
+def _wire_worker(out_dir, port, schedule):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DCGAN_FORCE_DDP"] = "1"
+    os.environ["DCGAN_DDP_SCHEDULE"] = schedule
+    os.environ.pop("DCGAN_DIST_BACKEND", None)
+    torch.cuda.set_device(0)
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    D.init_distributed(1, 0, torch.device("cuda", 0))
+    dev = torch.device("cuda", 0)
+    eng = HipEngine(DCGANConfig(output_size=64, c_dim=3), B, dev, seed=3, graph=True, rank_seeded_z=False,
+                    allreduce_dtype="bf16")
+    assert eng._schedule() == schedule and eng._wire_direct() == (schedule == "concurrent")
+    real = torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1
+    eng.set_batch(real.to(dev))
+    d, g, _ = _run(eng)
+    torch.save({"d": d, "g": g}, os.path.join(out_dir, "wire_%s.pt" % schedule))
+    D.barrier()
+    D.shutdown()
+
+
+def test_bf16_wire_without_copies_matches_the_copying_reducer(tmp_path):
+    """The segmented step's copy-free bf16 wire (cast kernels inside the step graphs, RCCL reducing
+    the bf16 images in place, Adam reading them) gives bit for bit the weights of the reducer's
+    fp32 -> bf16 -> fp32 copying path (serial schedule), over a one-rank RCCL group."""
+    ctx = mp.get_context("spawn")
+    for sch in ("concurrent", "serial"):
+        p = ctx.Process(target=_wire_worker, args=(str(tmp_path), _free_port(), sch))
+        p.start()
+        p.join(timeout=600)
+        assert p.exitcode == 0, "rank exited with %s" % p.exitcode
+    a = torch.load(tmp_path / "wire_concurrent.pt", weights_only=True)
+    b = torch.load(tmp_path / "wire_serial.pt", weights_only=True)
+    assert torch.equal(a["d"], b["d"]), (a["d"] - b["d"]).abs().max()
+    assert torch.equal(a["g"], b["g"]), (a["g"] - b["g"]).abs().max()

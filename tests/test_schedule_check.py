@@ -192,3 +192,26 @@ def test_checker_finds_an_early_g_hi_bucket():
     eng._run_step = early
     hz, _ = SC.check_engine(eng)
     assert any("allreduce" in h.a or "allreduce" in h.b for h in hz), hz
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("schedule", [None, "serial", "ddp"])
+def test_bf16_wire_schedules_have_no_hazards(dtype, schedule):
+    """bf16 wire: the segmented step's in-graph casts + in-place reduced bf16 images read by
+    Adam (bf16 engine), and the reducer's copying path (other schedules / the fp16 engine)."""
+    sched, hz, n = SC.check(DCGANConfig(), 4, dtype, 2, schedule, False, allreduce_dtype="bf16")
+    assert n > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_bf16_wire_direct_path_is_used():
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False, allreduce_dtype="bf16")
+    assert eng._schedule() == "concurrent" and eng._wire_direct()
+    assert set(eng._wire_ops) == {"dtop", "drest", "g_hi", "g_lo"}
+    eng._ensure_comm()
+    assert eng._ar_dtop.prefilled and eng._ar_g_hi.prefilled
+    # the collective no longer touches the fp32 gradient, only its bf16 image
+    assert all(p != eng.grad_d.flat.data_ptr() for p, _, _ in eng._ar_drest.accesses())
+    names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
+    assert "adam_d" in names and "adam_g" in names
