@@ -234,7 +234,9 @@ __global__ __launch_bounds__(256) void nconv_kernel(NConvArgs p) {
 
 // ------------------------------------------------------------------------------------ nwgrad
 constexpr int NWG_PX = 256;         // pixels per chunk (D tile rows)
-constexpr int NWG_WIN = 1536;       // max staged window pixels (+1 zero pixel after them)
+// max staged window pixels (+1 zero pixel after them): 2 rows of a 128-wide D side (the 256x256
+// ladder's RGB layers) stage 7 x 259 = 1813 window pixels
+constexpr int NWG_WIN = 2048;
 constexpr int NWG_WPT = NWG_WIN / 256;
 
 struct NWGradArgs {

@@ -627,7 +627,7 @@ def test_nconv_bn_backward_stats(B, Hh, act):
 
 @pytest.mark.parametrize("B,Hh,C,dtype", [(4, 64, 3, "bf16"), (2, 28, 1, "bf16"), (3, 33, 4, "bf16"),
                                           (2, 64, 3, "fp16"), (1, 7, 3, "bf16"), (2, 128, 3, "bf16"),
-                                          (40, 64, 3, "bf16")])
+                                          (40, 64, 3, "bf16"), (2, 256, 3, "fp16"), (1, 256, 3, "bf16")])
 def test_nwgrad(B, Hh, C, dtype):
     """narrow2.hip nwgrad vs autograd: the conv role (D layer 0: x = image, d = dL/d(conv out))
     and the deconv role (G's RGB layer: x = dL/d(deconv out), d = the layer input, TF layout
