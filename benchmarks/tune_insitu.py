@@ -89,9 +89,13 @@ def used_keys(cfg, B, dtype="bf16", seed=False):
     return [k for k in seen if k in table]
 
 
-def neighbours(key, cur, tiles=False, extra_tiles=()):
+def neighbours(key, cur, tiles=False, extra_tiles=(), extra_cfgs=()):
     cfg, sp = cur
     out = []
+    if not key.startswith("w3,"):  # explicit igemm3 configs (e.g. the ping-pong 24x / 25x), same split
+        mode, Kc = int(key.split(",")[0]), int(key.split(",")[4])
+        N = int(key.split(",")[7])
+        out += [(c, sp) for c in extra_cfgs if H.igemm3_pp_ok(c, mode, Kc) and H.IGEMM3_TILES[c % 10][1] <= max(N, 64)]
     for s2 in (sp // 2, sp * 2, sp + 1, sp - 1):
         if 1 <= s2 <= 32 and s2 != sp:
             out.append((cfg, s2))
@@ -117,7 +121,7 @@ def neighbours(key, cur, tiles=False, extra_tiles=()):
                 out.append((200 + 10 * ns + t2, sp))
     # igemm3 configs whose LDS ring does not fit 160 KiB are no candidates (e.g. 226: 8-wave 256x128 at NS = 4)
     out = [c for c in out if key.startswith("w3,") or c[0] < 200 or
-           (c[0] % 10 in H.IGEMM3_TILES and H.igemm3_lds(c[0]) <= 160 * 1024)]
+           (c[0] % 10 in H.IGEMM3_TILES and H.igemm3_lds(c[0]) <= 160 * 1024 and H.igemm3_pp_ok(c[0], mode, Kc))]
     seen, res = set(), []
     for c in out:
         if c not in seen and c != cur:
@@ -137,6 +141,7 @@ def main():
     ap.add_argument("--keys", default="", help="'|'-separated full table keys")
     ap.add_argument("--tiles", action="store_true", help="also try sibling tiles (slower)")
     ap.add_argument("--extra_tiles", default="", help="comma-separated igemm3 tile ids to try on every GEMM entry")
+    ap.add_argument("--extra_cfgs", default="", help="comma-separated igemm3 cfgs (e.g. 246,256) to try on every GEMM entry")
     ap.add_argument("--seed", action="store_true", help="tune layers with no table entry from the heuristic")
     ap.add_argument("--output_size", type=int, default=64)
     ap.add_argument("--c_dim", type=int, default=3)
@@ -159,7 +164,8 @@ def main():
         for key in keys:
             cur = table[key]
             extra = tuple(int(x) for x in a.extra_tiles.split(",") if x)
-            for cand in neighbours(key, cur, a.tiles, extra):
+            xcfg = tuple(int(x) for x in a.extra_cfgs.split(",") if x)
+            for cand in neighbours(key, cur, a.tiles, extra, xcfg):
                 table[key] = cand
                 try:
                     ms = step_ms(cfg, a.batch, a.steps, a.warmup, a.dtype)

@@ -330,7 +330,7 @@ def test_bench_force_ddp_reports_rccl():
     assert res["n_gpus"] == 1 and res["value"] > 0
 
 
-def _wire_worker(out_dir, port, schedule):
+def _wire_copyfree_worker(out_dir, port, schedule):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["DCGAN_FORCE_DDP"] = "1"
@@ -359,7 +359,7 @@ def test_bf16_wire_without_copies_matches_the_copying_reducer(tmp_path):
     fp32 -> bf16 -> fp32 copying path (serial schedule), over a one-rank RCCL group."""
     ctx = mp.get_context("spawn")
     for sch in ("concurrent", "serial"):
-        p = ctx.Process(target=_wire_worker, args=(str(tmp_path), _free_port(), sch))
+        p = ctx.Process(target=_wire_copyfree_worker, args=(str(tmp_path), _free_port(), sch))
         p.start()
         p.join(timeout=600)
         assert p.exitcode == 0, "rank exited with %s" % p.exitcode
