@@ -29,7 +29,7 @@ class FakeReducer:
     (fp32 gradient -> bf16 wire buffer before the collective, back after it:
     parallel/dist.py GradAllReducer.issue), so the bf16 rows carry their full cost."""
 
-    def __init__(self, us, flat=None, world=8, esize=4, nwg=32, kind="rccl", cycles_per_us=0.0):
+    def __init__(self, us, flat=None, world=8, esize=4, nwg=32, kind="rccl", cycles_per_us=0.0, prefilled=None):
         self.us = float(us)
         self.flat = flat
         self.numel = 0 if flat is None else flat.numel()
@@ -38,11 +38,14 @@ class FakeReducer:
         self.nwg = int(nwg)
         self.bytes = (int(2.0 * (world - 1) / world * self.numel * esize) // 16) * 16
         self.prog = None
+        # prefilled: the engine's own bf16 image of the slice (copy-free wire: its casts run inside
+        # the step graphs, so the stand-in only streams the image, no copies)
+        self.prefilled = prefilled
         self.wire = (torch.empty(self.numel, device=flat.device, dtype=torch.bfloat16)
-                     if esize == 2 and flat is not None else None)
+                     if esize == 2 and flat is not None and prefilled is None else None)
         if kind == "rccl" and self.bytes > 0 and flat is not None:
             from distributed_tensorflow_for_dcgan_amd.ops import hip as H
-            payload = flat if self.wire is None else self.wire
+            payload = prefilled if prefilled is not None else (flat if self.wire is None else self.wire)
             src_bytes = self.numel * payload.element_size()
             # the wire moves up to 2x the payload: read it twice over when the slice is shorter
             self.src = payload if src_bytes >= self.bytes else payload.repeat(-(-self.bytes // src_bytes))
@@ -65,6 +68,8 @@ class FakeReducer:
     def accesses(self):  # as the real reducer: the gradient slice is read and written
         if self.flat is None:
             return []
+        if self.prefilled is not None:
+            return [(self.prefilled.data_ptr(), self.numel * 2, True)]
         out = [(self.flat.data_ptr(), self.numel * self.flat.element_size(), True)]
         if self.wire is not None:
             out.append((self.wire.data_ptr(), self.numel * 2, True))
@@ -119,23 +124,23 @@ def main():
         eng._build_updates()
         eng._ensure_comm()
 
-        def fake(name, flat, us=None):
+        def fake(name, real, us=None):
+            flat = real.flat
             if us is None:
                 us = (ring_us(flat.numel(), a.fake_busbw_gbs, a.fake_lat_us, a.fake_world, esize)
                       if a.fake_busbw_gbs > 0 else 0.0)
             comm[name] = round(us, 1)
-            return FakeReducer(us, flat, a.fake_world, esize, a.fake_nwg, a.fake_kind, cpu)
+            return FakeReducer(us, flat, a.fake_world, esize, a.fake_nwg, a.fake_kind, cpu,
+                               prefilled=real.wire if real.prefilled else None)
 
-        gd, gg = eng.grad_d.flat, eng.grad_g.flat
-        o = eng._d_top_off
         us3 = [float(x) for x in a.fake_comm_us.split(",")] if a.fake_comm_us else [None] * 3
-        eng._ar_dtop = fake("dtop", gd[o:], us3[1])
-        eng._ar_drest = fake("drest", gd[:o], us3[2])
+        eng._ar_dtop = fake("dtop", eng._ar_dtop, us3[1])
+        eng._ar_drest = fake("drest", eng._ar_drest, us3[2])
         if a.schedule == "ddp":
-            eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), gg[lo:hi]) for _, lo, hi in eng._g_cuts]
+            eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), r) for (_, lo, hi), r in zip(eng._g_cuts, eng._ar_gparts)]
         for name, r in list(vars(eng).items()):  # the G buckets of the segmented schedules
-            if name in ("_ar_g", "_ar_g_hi", "_ar_g_lo") and isinstance(r, D.GradAllReducer):
-                setattr(eng, name, fake(name[4:], r.flat, us3[0] if name == "_ar_g" else None))
+            if (name == "_ar_g" or name.startswith("_ar_gsplit")) and isinstance(r, D.GradAllReducer):
+                setattr(eng, name, fake(name[4:], r, us3[0] if name == "_ar_g" else None))
     eng.set_synthetic_batch(torch.rand(a.batch_size, 64, 64, 3, device=dev) * 2 - 1)
     for _ in range(a.warmup):
         eng.train_step()

@@ -2,7 +2,7 @@
 
 The step (``image_train.py:151-158`` semantics) is recorded ONCE into
 native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buffers, then
-replayed every step -- captured into hipGraphs so a step is one (single process) or five
+replayed every step -- captured into hipGraphs so a step is one (single process) or seven
 (DDP) graph launches:
 
   progA[:a_fwd]  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
@@ -23,14 +23,16 @@ Schedules (``_schedule``), all covered by the stream-hazard checker
 (``engine/schedule_check.py``) and by GPU bit-exactness tests:
   "fused"       single process: ONE hipGraph; the two backward chains on two streams; ONE
                 Adam launch for both models after the join (16-bit dtypes)
-  "concurrent"  DDP (default) and the per-phase timed step: the step cut into 5 hipGraphs, the
-                collectives issued between them from the host on a comm stream
-                (``_concurrent_plan``): "bwd_a" = forward, then D's top layer + head (76 % of D's
-                gradient bytes at 64x64) beside the G chain's start -> its all-reduce; "bwd_b" =
-                the rest of the D chain with G's early weight gradients behind it (as fused)
-                beside the G chain down to its lowest deconv's weight gradient -> the rest of D's
-                and every G deconv layer's slice (83 % of G's bytes); "G_tail" -> the rest of G's;
-                Adam(D) runs under G's all-reduces, then Adam(G)
+  "concurrent"  DDP (default) and the per-phase timed step: the two chains cut into 7 graph
+                segments, the collectives issued between them from the host on a comm stream --
+                D's top layer + head (76 % of D's gradient bytes at 64x64) as soon as the D chain
+                has produced it; G's lowest deconv (64 % of G's bytes) as soon as its weight
+                gradient exists (``_g_split_plan``: the G chain computes it right after its input
+                gradient, the rest of G's backward follows as "G_tail"); the rest of D's when the
+                D chain ends, the rest of G's when the G tail ends; Adam(D) runs under G's last
+                all-reduce. With a bf16 wire (bf16 engine) each segment ends with the cast of its
+                finished gradient slice into a flat bf16 image that RCCL reduces in place and
+                Adam reads (``_wire_direct``): no copies around the collectives
   "ddp"         DCGAN_DDP_SCHEDULE=ddp (RCCL): the fused schedule with the gradient all-reduces on
                 the comm stream INSIDE the same single hipGraph (RCCL collectives are captured);
                 G's gradients go out in per-layer buckets as G's weight gradients land
@@ -297,11 +299,12 @@ class HipEngine:
         self._g_split = self._g_split_plan()
         self.progX, self._wire_ops = self._prog(), {}
         if self.wire_d is not None:  # fp32 gradient slice -> its bf16 wire image, one op per collective
-            lo = self._g_split[3] if self._g_split is not None else 0
             o = self._d_top_off
             nd, ng = self.grad_d.flat.numel(), self.grad_g.flat.numel()
+            lo, hi = self._g_split[3:] if self._g_split is not None else (0, ng)
             for name, src, dst, a, b in (("dtop", self.grad_d, self.wire_d, o, nd), ("drest", self.grad_d, self.wire_d, 0, o),
-                                         ("g_hi", self.grad_g, self.wire_g, lo, ng), ("g_lo", self.grad_g, self.wire_g, 0, lo)):
+                                         ("g", self.grad_g, self.wire_g, 0, ng), ("g_a", self.grad_g, self.wire_g, lo, hi),
+                                         ("g_b", self.grad_g, self.wire_g, hi, ng), ("g_c", self.grad_g, self.wire_g, 0, lo)):
                 if b > a:
                     self._wire_ops[name] = self.progX.size()
                     self.progX.cast_to_bf16("wire." + name, _p(src.flat) + 4 * a, 0, _p(dst.flat) + 2 * a, b - a,
@@ -1046,47 +1049,26 @@ class HipEngine:
             return [("fwd+G_bwd", lin([(A, 0, -1), (W, 0, -1)]), M), ("D_bwd_top", lin([(B, 0, self._b_split)]), M),
                     ("D_bwd_rest", lin([(B, self._b_split, -1)]), M), ("adam_G", lin([(C, 0, self._c_split)]), M),
                     ("adam_D", lin([(C, self._c_split, -1)]), M)]
-        # "concurrent": three backward graphs around the collectives (see _concurrent_plan)
-        p = self._concurrent_plan()
-
-        def bwd_a(ex, cs, sec):  # forward; then D's top layer + head (alt) beside the G chain's start (cs)
-            alt = ex.alt[0]
-            ex.run(A, [cs, sec], 0, self._a_fwd)
-            ex.wait(alt, cs)
-            ex.run(B, ex.alt, 0, self._b_split)
-            self._wire_cast(ex, "dtop", ex.alt)
-            ex.run(A, [cs, sec], self._a_fwd, p["g_cut"])
-            ex.wait(cs, alt)
-
-        def bwd_b(ex, cs, sec):  # rest of the D chain + G weight gradients behind it (alt) beside the G chain (cs)
-            alt = ex.alt[0]
-            ex.wait(alt, cs)
-            pos, marks = p["g_cut"], {}
-            for k in p["alt_pieces"]:
-                a_end = self._g_w[k][0]
-                if a_end > pos:
-                    ex.run(A, [cs, sec], pos, a_end)
-                    pos = a_end
-                marks[k] = ex.mark(cs) if a_end > p["g_cut"] else None
-            ex.run(A, [cs, sec], pos, p["a_end"])
-            ex.run(B, ex.alt, self._b_split, -1)
-            for k in p["alt_pieces"]:
-                if marks[k] is not None:
-                    ex.wait_mark(alt, marks[k])
-                ex.run(W, ex.alt, self._w_begin(k), self._g_w[k][1])
-            for k in p["cs_pieces"]:
-                ex.run(W, [cs, sec], self._w_begin(k), self._g_w[k][1])
-            ex.wait(cs, alt)
-            self._wire_cast(ex, "drest", [cs, sec])
-            self._wire_cast(ex, "g_hi", [cs, sec])
-
-        def g_tail(ex, cs, sec):
-            ex.run(A, [cs, sec], p["a_end"], -1)
-            self._wire_cast(ex, "g_lo", [cs, sec])
-        g_tail.empty = p["a_end"] >= A.size()
-        bwd_a.empty = bwd_b.empty = False
-        return [("bwd_a", bwd_a, M), ("bwd_b", bwd_b, M), ("G_tail", g_tail, M),
-                ("adam_D", lin([(C, 0, self._c_split)]), M), ("adam_G", lin([(C, self._c_split, -1)]), M)]
+        # "concurrent": one graph per chain segment, each on its own stream; the collectives go
+        # out between them (ROCm refuses events recorded inside a graph that outside work waits
+        # on: profiles/r2/probe_external_event_r2.txt). Graphs that fork and join both streams
+        # around the collectives measured slower (profiles/r5/ab_ddp_5graph_joined_r5.txt).
+        X = self.progX
+        wx = lambda name: ([(X, self._wire_ops[name], self._wire_ops[name] + 1)]  # noqa: E731
+                           if self._wire_direct() and name in self._wire_ops else [])
+        sp = self._g_split
+        if sp is None:
+            g_chain, g_tail = [(A, self._a_fwd, -1), (W, 0, -1)] + wx("g"), []
+        else:  # G's lowest deconv weight gradient ends the chain; the rest of G's backward follows
+            a_need, wb, we = sp[:3]
+            g_chain = [(A, self._a_fwd, a_need), (W, wb, we)] + wx("g_a")
+            g_tail = [(A, a_need, -1), (W, 0, wb), (W, we, -1)] + wx("g_b") + wx("g_c")
+        return [("fwd", lin([(A, 0, self._a_fwd)]), M),
+                ("D_bwd_top", lin([(B, 0, self._b_split)] + wx("dtop")), self.ALT),
+                ("G_chain", lin(g_chain), M),
+                ("D_bwd_rest", lin([(B, self._b_split, -1)] + wx("drest")), self.ALT),
+                ("G_tail", lin(g_tail), M), ("adam_D", lin([(C, 0, self._c_split)]), M),
+                ("adam_G", lin([(C, self._c_split, -1)]), M)]
 
     @staticmethod
     def _lin_segment(parts):
@@ -1110,48 +1092,6 @@ class HipEngine:
 
     def _w_begin(self, k: int) -> int:
         return self._g_w[k - 1][1] if k > 0 else 0
-
-    def _concurrent_plan(self):
-        """Where the segmented ("concurrent") step cuts the two backward chains into hipGraphs.
-        The collectives can only start between graphs (ROCm refuses events recorded inside a
-        graph that outside work waits on: profiles/r2/probe_external_event_r2.txt), so:
-          bwd_a: the forward, then D's top layer + head (its 13.1 MB gradient slice is final at
-                 the end: the "dtop" all-reduce) beside the G chain's first part, up to g_cut;
-          bwd_b: the rest of the D chain with G's early weight gradients queued behind it on the
-                 D chain's stream (as in the fused step), beside the G chain down to the point
-                 where the lowest G deconv's weight gradient can run (a_end), then the last G
-                 weight gradients on the G chain's stream (DCGAN_GW_TAIL_ON_MAIN, as fused). At
-                 its end D's gradient and G's [lo:] slice (every deconv layer: 17 MB at 64x64)
-                 are final: "drest" + "g_hi";
-          G_tail: the lowest deconv's data gradient, g_bn0, the projection's gradient: "g_lo".
-        g_cut defaults to the G chain position where its first weight gradient can run (the
-        image gradient: the g_loss chain has left D); DCGAN_DDP_GCUT=k moves it to piece k's
-        position (-1: no G work beside D's top layer)."""
-        nw = len(self._g_w)
-        sp = self._g_split
-        n_main = min(self._gw_tail_on_main(), nw)
-        if sp is not None:
-            k1 = self._g_w_layer.index(self.gl[0].name)
-            a_end = sp[0]
-        else:
-            k1, a_end = None, self.progA.size()
-        cs_pieces = list(range(nw - n_main, nw))
-        if k1 is not None and k1 not in cs_pieces:
-            cs_pieces.append(k1)  # the big slice must be computed inside bwd_b
-        # pieces whose operands need progA beyond a_end cannot run before G_tail
-        cs_pieces = [k for k in cs_pieces if self._g_w[k][0] <= a_end]
-        alt_pieces = [k for k in range(nw) if k not in cs_pieces and self._g_w[k][0] <= a_end]
-        late = [k for k in range(nw) if self._g_w[k][0] > a_end]
-        if late:  # never the case for the DCGAN ladder (the projection's gradient is in progA)
-            raise RuntimeError("G weight-gradient pieces after the G tail cut: %s" % late)
-        v = os.environ.get("DCGAN_DDP_GCUT", "0")
-        try:
-            kc = int(v)
-        except ValueError:
-            raise ValueError("DCGAN_DDP_GCUT must be an integer piece index (-1: none), got %r" % v)
-        g_cut = self._a_fwd if (kc < 0 or nw == 0) else min(self._g_w[min(kc, nw - 1)][0], a_end)
-        return {"g_cut": max(g_cut, self._a_fwd), "a_end": a_end, "alt_pieces": alt_pieces,
-                "cs_pieces": sorted(cs_pieces), "lo": sp[3] if sp is not None else 0}
 
     def enable_timing(self) -> None:
         """Per-phase GPU timers: the step runs as segments with events between
@@ -1287,10 +1227,10 @@ class HipEngine:
         run(ex, stream, ex.side if which == self.MAIN else ex.alt[1])
 
     def _ar_launch(self, ex, which: str, src) -> None:
-        """All-reduce one gradient slice ("g", "dtop", "drest", "g_hi", "g_lo") on the comm stream
+        """All-reduce one gradient slice ("g", "dtop", "drest", "gsplit_a/b/c") on the comm stream
         once `src`'s queued work is done."""
         if self.ddp:
-            r = getattr(self, "_ar_" + which)
+            r = getattr(self, "_ar_" + which, None)
             if r is None:
                 return
             ex.wait(ex.comm, src)
@@ -1313,25 +1253,38 @@ class HipEngine:
                 self._run_ddp(ex, cs)
             return
         if sch == "concurrent":
+            alt = ex.alt[0]
             self._tick(0, cs)
-            self._seg(ex, 0, cs)               # fwd; D top + head beside the G chain's start
+            self._seg(ex, 0, cs)               # z, G fwd, D fwd (real | fake), losses
             self._tick(1, cs)
-            self._ar_launch(ex, "dtop", cs)    # D's top layer + head, under bwd_b
-            self._seg(ex, 1, cs)               # rest of D (+ early G wgrads) beside the G chain
-            self._tick(2, cs)
-            self._ar_launch(ex, "drest", cs)   # grad_d final
-            d_done = ex.mark(ex.comm) if self.ddp else None
-            self._ar_launch(ex, "g_hi", cs)    # every G deconv layer's slice, under G_tail + Adam(D)
-            self._seg(ex, 2, cs)               # G tail: lowest deconv's dgrad, g_bn0, projection
+            ex.wait(alt, cs)
+            self._seg(ex, 1, alt)              # D chain: head + top layer gradients
+            self._tick(2, alt)
+            self._ar_launch(ex, "dtop", alt)
+            self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward to g_h1's wgrad
             self._tick(3, cs)
-            self._ar_launch(ex, "g_lo", cs)
-            if d_done is not None:
-                ex.wait_mark(cs, d_done)
-            self._seg(ex, 3, cs)               # Adam D -> D mirror (overlaps G's all-reduces)
-            self._tick(4, cs)
-            self._ar_join(ex, cs)              # G's collectives
-            self._seg(ex, 4, cs)               # Adam G, step counter, G mirror
+            if self._g_split is not None:
+                self._ar_launch(ex, "gsplit_a", cs)  # g_h1's slice, under the rest of both chains
+            self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
+            self._tick(4, alt)
+            self._seg(ex, 4, cs)               # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
             self._tick(5, cs)
+            # D's last bucket, then the rest of G's; Adam(D) runs while G's is in flight
+            self._ar_launch(ex, "drest", alt)
+            d_done = ex.mark(ex.comm) if self.ddp else None
+            if self._g_split is not None:
+                self._ar_launch(ex, "gsplit_b", cs)
+                self._ar_launch(ex, "gsplit_c", cs)
+            else:
+                self._ar_launch(ex, "g", cs)
+            if d_done is not None:
+                ex.wait_mark(cs, d_done)       # dtop + drest (and g_h1's) collectives
+            ex.wait(cs, alt)                   # (W = 1, timed: the D chain itself)
+            self._seg(ex, 5, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
+            self._tick(6, cs)
+            self._ar_join(ex, cs)              # G's collectives
+            self._seg(ex, 6, cs)               # Adam G, step counter, G mirror
+            self._tick(7, cs)
             return
         self._tick(0, cs)
         self._seg(ex, 0, cs)                   # fwd, g_loss chain through D(fake), G backward -> grad_g final
@@ -1370,12 +1323,13 @@ class HipEngine:
             self._ar_dtop = mk(df[o:], wdf[o:] if direct else None)
             self._ar_drest = mk(df[:o], wdf[:o] if direct else None)
             sch = self._schedule()
-            if sch == "serial":
-                self._ar_g = mk(gf)
-            elif sch == "concurrent":
-                lo = self._concurrent_plan()["lo"]
-                self._ar_g_hi = mk(gf[lo:], wgf[lo:] if direct else None)
-                self._ar_g_lo = mk(gf[:lo], wgf[:lo] if direct else None) if lo > 0 else None
+            if sch == "serial" or (sch == "concurrent" and self._g_split is None):
+                self._ar_g = mk(gf, wgf if direct else None)
+            elif sch == "concurrent":  # g_h1's slice first, then the two others
+                lo, hi = self._g_split[3:]
+                self._ar_gsplit_a = mk(gf[lo:hi], wgf[lo:hi] if direct else None)
+                self._ar_gsplit_b = mk(gf[hi:], wgf[hi:] if direct else None)
+                self._ar_gsplit_c = mk(gf[:lo], wgf[:lo] if direct else None) if lo > 0 else None
             elif sch == "ddp":  # G's gradient in per-layer buckets (see _g_bucket_cuts)
                 self._ar_gparts = [mk(gf[lo:hi]) for _, lo, hi in self._g_cuts]
 

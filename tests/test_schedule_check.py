@@ -158,36 +158,34 @@ def test_fused_g_wgrad_tail_on_main_rejects_bad_values(monkeypatch):
         eng._gw_tail_on_main()
 
 
-@pytest.mark.parametrize("gcut", ["-1", "0", "1", "2"])
 @pytest.mark.parametrize("tail", ["0", "2", "4"])
-def test_concurrent_ddp_cuts_have_no_hazards(monkeypatch, gcut, tail):
-    """The segmented DDP step for every G-chain cut of its first backward graph
-    (DCGAN_DDP_GCUT) and every trailing-G-wgrad placement (DCGAN_GW_TAIL_ON_MAIN)."""
-    monkeypatch.setenv("DCGAN_DDP_GCUT", gcut)
+def test_concurrent_ddp_gw_placements_have_no_hazards(monkeypatch, tail):
+    """The segmented DDP step for every trailing-G-wgrad placement (DCGAN_GW_TAIL_ON_MAIN)."""
     monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", tail)
     eng = _dry(world=2)
     assert eng._schedule() == "concurrent"
-    p = eng._concurrent_plan()
-    assert sorted(p["alt_pieces"] + p["cs_pieces"]) == list(range(len(eng._g_w)))
     hz, n_ops = SC.check_engine(eng)
     assert n_ops > 100
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
-def test_checker_finds_an_early_g_hi_bucket():
-    """Segmented DDP: issuing the all-reduce of G's deconv layers after the first backward graph
-    (before bwd_b computes their weight gradients) is a race the checker reports."""
+def test_checker_finds_an_early_g_bucket():
+    """Segmented DDP: issuing the all-reduce of g_h1's slice before the G chain segment that
+    computes its weight gradient is a race the checker reports."""
     eng = _dry(world=2)
 
     def early(ex):
-        cs = ex.main()
+        cs, alt = ex.main(), ex.alt[0]
         eng._seg(ex, 0, cs)
-        eng._ar_launch(ex, "g_hi", cs)   # too early
-        eng._seg(ex, 1, cs)
-        eng._seg(ex, 2, cs)
+        ex.wait(alt, cs)
+        eng._seg(ex, 1, alt)
+        eng._ar_launch(ex, "gsplit_a", cs)   # too early: G_chain has not run
+        for i, st in ((2, cs), (3, alt), (4, cs)):
+            eng._seg(ex, i, st)
+        ex.wait(cs, alt)
         eng._ar_join(ex, cs)
-        eng._seg(ex, 3, cs)
-        eng._seg(ex, 4, cs)
+        eng._seg(ex, 5, cs)
+        eng._seg(ex, 6, cs)
 
     eng._run_step = early
     hz, _ = SC.check_engine(eng)
@@ -208,9 +206,9 @@ def test_bf16_wire_direct_path_is_used():
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False, allreduce_dtype="bf16")
     assert eng._schedule() == "concurrent" and eng._wire_direct()
-    assert set(eng._wire_ops) == {"dtop", "drest", "g_hi", "g_lo"}
+    assert {"dtop", "drest", "g_a", "g_b", "g_c"} <= set(eng._wire_ops)
     eng._ensure_comm()
-    assert eng._ar_dtop.prefilled and eng._ar_g_hi.prefilled
+    assert eng._ar_dtop.prefilled and eng._ar_gsplit_a.prefilled and eng._ar_gsplit_c.prefilled
     # the collective no longer touches the fp32 gradient, only its bf16 image
     assert all(p != eng.grad_d.flat.data_ptr() for p, _, _ in eng._ar_drest.accesses())
     names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
