@@ -152,6 +152,7 @@ def main():
                        "schedule": eng._schedule() if hasattr(eng, "_schedule") else None,
                        "graphs_per_step": sum(g is not None for g in getattr(eng, "_graphs", [])) or None,
                        "backend": backend, "world_size": world_seen, "devices": devices,
+                       "collectives": getattr(eng, "comm_kind", None),
                        "kernels_per_step": eng.kernel_count() if hasattr(eng, "kernel_count") else None,
                        "gflop_per_image": round(cfg.flops_per_image() / 1e9, 4),
                        "tflops_achieved": round(value * cfg.flops_per_image() / 1e12, 2),

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "hip/kernels.h"
+#include "comm.h"
 extern "C" {
 #include "hip/narrow2.inc"
 }
@@ -161,6 +162,20 @@ class Program {
     return add("copy", stream, [d, sp, bytes](hipStream_t s) {
       return (int)hipMemcpyAsync(d, sp, bytes, hipMemcpyDeviceToDevice, s);
     }, AccList().r(src, bytes).w(dst, bytes).v);
+  }
+
+  // in-place SUM all-reduce of `count` elements (dtype 0 fp32 / 1 bf16 / 2 fp16) over a native
+  // RCCL communicator (comm.h), enqueued on the op's stream: a collective the C++ replay (and a
+  // hipGraph capture) issues in program order with the kernels, no Python in between
+  int allreduce(const std::string& name, std::shared_ptr<dcg_comm::Comm> comm, uintptr_t ptr, size_t count, int dtype,
+                int stream) {
+    const size_t es = dtype == 0 ? 4 : 2;
+    dcg_comm::Comm* c = comm.get();
+    comms_.push_back(comm);  // keep the communicator alive as long as the program
+    return add(name, stream, [c, ptr, count, dtype](hipStream_t s) {
+      c->all_reduce(ptr, count, dtype, reinterpret_cast<uintptr_t>(s));
+      return 0;
+    }, AccList().w(ptr, count * es).v);
   }
 
   // RCCL stand-in for schedule studies (csrc/hip/comm_emu.hip): nwg workgroups copy `bytes` from
@@ -908,6 +923,7 @@ class Program {
   std::vector<Op> ops_;
   std::vector<void*> dev_allocs_;
   std::vector<hipEvent_t> events_;
+  std::vector<std::shared_ptr<dcg_comm::Comm>> comms_;
   int last_mtiles_ = 0, last_nphases_ = 0;
   int dt_ = 0;       // element type of every activation / weight-mirror pointer
   size_t es_ = 2;    // its size in bytes
@@ -952,6 +968,15 @@ PYBIND11_MODULE(_dcgan_hip, m) {
   m.attr("OP_LAUNCH") = (int)OP_LAUNCH;
   m.attr("OP_RECORD") = (int)OP_RECORD;
   m.attr("OP_WAIT") = (int)OP_WAIT;
+  py::class_<dcg_comm::Comm, std::shared_ptr<dcg_comm::Comm>>(m, "RcclComm")
+      .def(py::init<const std::string&, int, int, const std::string&, int>(), py::arg("lib_path"), py::arg("nranks"),
+           py::arg("rank"), py::arg("unique_id"), py::arg("device"))
+      .def_static("unique_id", [](const std::string& lib) { return py::bytes(dcg_comm::Comm::unique_id(lib)); })
+      .def("all_reduce", &dcg_comm::Comm::all_reduce, py::arg("ptr"), py::arg("count"), py::arg("dtype"),
+           py::arg("stream"))
+      .def("destroy", &dcg_comm::Comm::destroy)
+      .def_property_readonly("nranks", &dcg_comm::Comm::nranks)
+      .def_property_readonly("rank", &dcg_comm::Comm::rank);
   py::class_<Program>(m, "Program")
       .def(py::init<int, bool>(), py::arg("dtype") = 0, py::arg("dry") = false)
       .def_property_readonly("f16", &Program::f16)
@@ -968,6 +993,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("memset", &Program::memset)
       .def("copy", &Program::copy)
       .def("comm_emulate", &Program::comm_emulate)
+      .def("allreduce", &Program::allreduce)
       .def("igemm", &Program::igemm)
       .def("igemm_ex", &Program::igemm_ex, py::arg("name"), py::arg("mode"), py::arg("A"), py::arg("Bw"), py::arg("C"),
            py::arg("Bn"), py::arg("Hin"), py::arg("Win"), py::arg("Kc"), py::arg("Hout"), py::arg("Wout"), py::arg("N"),

@@ -1083,7 +1083,8 @@ class HipEngine:
         step graphs write each gradient slice's bf16 image when the slice is final, RCCL reduces
         the image in place, Adam reads it (``adam_bf(gbf=...)``). Other schedules / dtypes use the
         reducer's own fp32 <-> bf16 copies around each collective."""
-        return self.wire_d is not None and self._schedule() == "concurrent"
+        return (self.wire_d is not None and self._schedule() == "concurrent"
+                and os.environ.get("DCGAN_WIRE_DIRECT", "1") != "0")  # =0: the copying reducer (A/B)
 
     def _wire_cast(self, ex, name: str, streams) -> None:
         if self._wire_direct() and name in self._wire_ops:
@@ -1317,8 +1318,13 @@ class HipEngine:
             wdf = self.wire_d.flat if direct else None
             wgf = self.wire_g.flat if direct else None
 
+            native = D.native_comm(self.device) if not self.dry else None
+            self.comm_kind = ("rccl-native" if native is not None else
+                              "torch.distributed(%s)" % (D.backend() or "none"))
+
             def mk(t, wire=None):
-                return D.GradAllReducer(t, mb, wd, stream=cs, force=True, wire=wire, prefilled=wire is not None)
+                return D.GradAllReducer(t, mb, wd, stream=cs, force=True, wire=wire, prefilled=wire is not None,
+                                        native=native)
 
             self._ar_dtop = mk(df[o:], wdf[o:] if direct else None)
             self._ar_drest = mk(df[:o], wdf[:o] if direct else None)

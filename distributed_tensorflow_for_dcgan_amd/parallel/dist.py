@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 _PG_INITIALISED_HERE = False
+_NATIVE = None  # native RCCL communicator over the default group's ranks (native_comm)
 
 
 def is_initialized() -> bool:
@@ -86,11 +87,42 @@ def init_distributed(world: int, rank_: int, device: torch.device, master_addr: 
     return dist.group.WORLD
 
 
+def _rccl_path() -> str:
+    """The RCCL that PyTorch loaded (its bundled librccl.so): one RCCL per process."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so"
+
+
+def native_comm(device: torch.device):
+    """A native RCCL communicator (csrc/comm.h) over the default process group's ranks, for the
+    gradient all-reduces: ncclAllReduce straight onto the engine's comm stream from C++ -- no
+    ProcessGroupNCCL internal stream, event hand-offs or Python call per collective, and
+    capturable into a hipGraph. Rank 0 makes the unique id, the process group broadcasts it.
+    None without an RCCL ("nccl") group or with DCGAN_NATIVE_RCCL=0 (torch.distributed then
+    issues the collectives)."""
+    global _NATIVE
+    if _NATIVE is None:
+        if (not is_initialized() or dist.get_backend() != "nccl" or device.type != "cuda"
+                or os.environ.get("DCGAN_NATIVE_RCCL", "1") == "0"):
+            return None
+        from ..ops import hip as H
+        ext = H.ext()
+        lib = _rccl_path()
+        obj = [ext.RcclComm.unique_id(lib) if dist.get_rank() == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        _NATIVE = ext.RcclComm(lib, dist.get_world_size(), dist.get_rank(), obj[0], device.index or 0)
+    return _NATIVE
+
+
 def shutdown() -> None:
-    global _PG_INITIALISED_HERE
+    global _PG_INITIALISED_HERE, _NATIVE
+    if _NATIVE is not None:
+        _NATIVE.destroy()
+        _NATIVE = None
     if is_initialized() and _PG_INITIALISED_HERE:
         dist.destroy_process_group()
         _PG_INITIALISED_HERE = False
+_NATIVE = None  # native RCCL communicator over the default group's ranks (native_comm)
 
 
 def barrier() -> None:
@@ -186,8 +218,9 @@ class GradAllReducer:
 
     def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 32.0, wire_dtype: str = "fp32",
                  reverse: bool = True, stream: "Optional[torch.cuda.Stream]" = None, force: bool = False,
-                 wire: Optional[torch.Tensor] = None, prefilled: bool = False):
+                 wire: Optional[torch.Tensor] = None, prefilled: bool = False, native=None):
         self.flat = flat_grad
+        self.native = native  # native_comm(): ncclAllReduce on the current stream, from C++
         self.world = world_size()
         # collectives are issued when there is a peer -- or on a forced one-rank group
         self.active = is_initialized() and (self.world > 1 or force)
@@ -227,14 +260,21 @@ class GradAllReducer:
             return
         for s, e in self.buckets:
             if self.prefilled:
-                dist.all_reduce(self.wire[s:e], op=dist.ReduceOp.SUM)
+                self._sum(self.wire[s:e])
             elif self.wire is not None:
                 w = self.wire[s:e]
                 w.copy_(self.flat[s:e])
-                dist.all_reduce(w, op=dist.ReduceOp.SUM)
+                self._sum(w)
                 self.flat[s:e].copy_(w)
             else:
-                dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM)
+                self._sum(self.flat[s:e])
+
+    def _sum(self, t: torch.Tensor) -> None:
+        if self.native is not None:
+            code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t.dtype]
+            self.native.all_reduce(t.data_ptr(), t.numel(), code, torch.cuda.current_stream(t.device).cuda_stream)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
 
     def accesses(self):
         """(ptr, bytes, is_write) ranges one issue() touches (schedule checker)."""

@@ -327,6 +327,7 @@ def test_bench_force_ddp_reports_rccl():
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
+    assert res["config"]["collectives"] == "rccl-native"
     assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 7
     assert res["n_gpus"] == 1 and res["value"] > 0
 
@@ -368,3 +369,48 @@ def test_bf16_wire_without_copies_matches_the_copying_reducer(tmp_path):
     b = torch.load(tmp_path / "wire_serial.pt", weights_only=True)
     assert torch.equal(a["d"], b["d"]), (a["d"] - b["d"]).abs().max()
     assert torch.equal(a["g"], b["g"]), (a["g"] - b["g"]).abs().max()
+
+
+def _native_worker(out_dir, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.pop("DCGAN_DIST_BACKEND", None)
+    torch.cuda.set_device(0)
+    from distributed_tensorflow_for_dcgan_amd.ops import hip as H
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    D.init_distributed(1, 0, torch.device("cuda", 0), force=True)
+    comm = D.native_comm(torch.device("cuda", 0))
+    assert comm is not None and comm.nranks == 1 and comm.rank == 0
+    x = torch.randn(3000, device="cuda")
+    ref = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    comm.all_reduce(x.data_ptr(), x.numel(), 0, s.cuda_stream)  # one rank: the sum is the input
+    torch.cuda.current_stream().wait_stream(s)
+    ok1 = torch.equal(x, ref)
+    y = torch.randn(4096, device="cuda").to(torch.bfloat16)
+    yref = y.clone()
+    prog = H.ext().Program()
+    prog.allreduce("ar", comm, y.data_ptr(), y.numel(), 1, 0)
+    g = torch.cuda.CUDAGraph()  # the recorded collective is graph-capturable
+    with torch.cuda.graph(g):
+        H.run(prog)
+    g.replay()
+    torch.cuda.synchronize()
+    torch.save({"ok1": ok1, "ok2": torch.equal(y, yref)}, os.path.join(out_dir, "native.pt"))
+    D.shutdown()
+
+
+def test_native_rccl_communicator():
+    """The engine's native RCCL communicator (csrc/comm.h: PyTorch's librccl via dlopen, our own
+    ncclComm from a broadcast unique id): ncclAllReduce on a given stream, and as a recorded
+    Program op inside a captured hipGraph, over a one-rank group."""
+    import tempfile
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as d:
+        p = ctx.Process(target=_native_worker, args=(d, _free_port()))
+        p.start()
+        p.join(timeout=300)
+        assert p.exitcode == 0, "rank exited with %s" % p.exitcode
+        r = torch.load(os.path.join(d, "native.pt"), weights_only=True)
+    assert r["ok1"] and r["ok2"]
