@@ -33,7 +33,9 @@ def parse():
     p.add_argument("--c_dim", type=int, default=3)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     p.add_argument("--engine", default="hip", choices=["hip", "reference"])
-    p.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip engine)")
+    # eager C++ replay of the recorded Programs (0) measured 1.1-1.5 % faster than hipGraph replay (1)
+    # for the fused step and 3 % for the segmented DDP step (profiles/r5/ab_eager_vs_graph_r5.txt)
+    p.add_argument("--graph", type=int, default=0, help="1: replay the step as hipGraph(s) (hip engine); 0: C++ replay")
     p.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--force_ddp", action="store_true",

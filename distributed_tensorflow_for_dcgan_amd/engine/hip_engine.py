@@ -1318,7 +1318,11 @@ class HipEngine:
             wdf = self.wire_d.flat if direct else None
             wgf = self.wire_g.flat if direct else None
 
-            native = D.native_comm(self.device) if not self.dry else None
+            # native RCCL only where the collectives are captured into the step's hipGraph ("ddp"):
+            # issued eagerly, each ncclAllReduce cost ~50-60 us more than torch.distributed's
+            # (profiles/r5/ab_native_rccl_eager_graph_r5.txt); captured, both cost the same
+            native = (D.native_comm(self.device) if not self.dry and self._schedule() == "ddp" and self.graph_requested
+                      else None)
             self.comm_kind = ("rccl-native" if native is not None else
                               "torch.distributed(%s)" % (D.backend() or "none"))
 

@@ -58,7 +58,8 @@ EXTRA_FLAGS: List[Tuple[str, str, Any, str]] = [
     ("keep_checkpoints", "int", 5, "number of checkpoints to keep (TF Saver default 5)"),
     ("sample_every", "int", 100, "sample when global_step %% sample_every == 1 (reference: 100)"),
     ("engine", "str", "auto", "auto | hip | reference : which training step implementation"),
-    ("graph", "bool", True, "capture the HIP training step into a hipGraph"),
+    ("graph", "bool", False, "replay the HIP training step as hipGraph(s) instead of the C++ launch replay "
+                              "(measured 1-3 %% slower: profiles/r5/ab_eager_vs_graph_r5.txt)"),
     ("bucket_mb", "float", 32.0, "gradient all-reduce bucket size in MiB (HIP engine: one call per overlap window)"),
     ("allreduce_dtype", "str", "fp32", "gradient all-reduce wire dtype: fp32 | bf16"),
     ("shard_data", "bool", True, "give every rank a disjoint shard of the input files"),

@@ -323,11 +323,11 @@ def test_bench_force_ddp_reports_rccl():
     env = dict(os.environ)
     env.pop("DCGAN_DIST_BACKEND", None)
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "5", "--warmup", "2",
-                          "--force_ddp"], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+                          "--force_ddp", "--graph", "1"], cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
-    assert res["config"]["collectives"] == "rccl-native"
+    assert res["config"]["collectives"] == "torch.distributed(nccl)"
     assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 7
     assert res["n_gpus"] == 1 and res["value"] > 0
 
