@@ -387,8 +387,10 @@ class Program {
 
   // weight gradient v3 (wgrad3.hip): the 25-tap gather GEMM with the split-K reduction in-kernel,
   // written scaled straight into the fp32 gradient dst [25][Mc][Nc] -- one launch, no slabs pass
+  // adam = (w, m, v, powers, lr, b1, b2, eps) of this weight: TF-Adam in the store pass (or empty)
   int wgrad3(std::string name, uintptr_t G, int Hg, int Wg, int Mc, uintptr_t Dm, int Bn, int Hd, int Wd, int Nc,
-             int pad, int cfg, int splits, uintptr_t dst, float scale, int stream) {
+             int pad, int cfg, int splits, uintptr_t dst, float scale, int stream,
+             std::tuple<uintptr_t, uintptr_t, uintptr_t, uintptr_t, float, float, float, float> adam) {
     int bm = 0, bn = 0, ns = 0;
     if (KF(dcg_wgrad3_tile)(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
     const int al = (int)(16 / es_);
@@ -411,6 +413,13 @@ class Program {
     a.out = P<float>(dst); a.scale = scale;
     AccList acc;
     acc.r(G, g_elems * es_).r(Dm, d_elems * es_).w(dst, (size_t)25 * Mc * Nc * 4);
+    if (std::get<0>(adam)) {
+      const size_t nw = (size_t)25 * Mc * Nc;
+      a.aw = P<float>(std::get<0>(adam)); a.am = P<float>(std::get<1>(adam)); a.av = P<float>(std::get<2>(adam));
+      a.apow = P<const float>(std::get<3>(adam));
+      a.alr = std::get<4>(adam); a.ab1 = std::get<5>(adam); a.ab2 = std::get<6>(adam); a.aeps = std::get<7>(adam);
+      acc.w(std::get<0>(adam), nw * 4).w(std::get<1>(adam), nw * 4).w(std::get<2>(adam), nw * 4).r(std::get<3>(adam), 8);
+    }
     const int tt = KF(dcg_wgrad3_taps_per_tile)(cfg);
     if (tt == 2 && 2 * Mc != bm) throw std::runtime_error("wgrad3: two-tap tiles need BM = 2 Mc");
     const size_t tiles = (size_t)(tt == 2 ? 1 : (Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * ((25 + tt - 1) / tt);
@@ -748,6 +757,38 @@ class Program {
                            P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
     }, acc.v);
   }
+  // the end of the step when wgrad3 ran the big weights' Adam in its store pass: Adam over the
+  // remaining ranges, mirror casts over the others, beta powers + step (misc.hip adam_rest_kernel).
+  // ranges: [(set 0=A / 1=D, cast_only, offset, count)] in elements, offsets / counts % 4 == 0
+  int adam_rest(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA, uintptr_t pA,
+                size_t nA, float lrA, float b1A, float b2A, float epsA, uintptr_t wD, uintptr_t wbfD, uintptr_t gD,
+                uintptr_t mD, uintptr_t vD, uintptr_t pD, size_t nD, float lrD, float b1D, float b2D, float epsD,
+                std::vector<std::tuple<int, int, size_t, size_t>> ranges, float gscale, uintptr_t step, int stream) {
+    struct Blk { unsigned long long off4; unsigned n4; int set; int cast; int pad; };
+    std::vector<Blk> blks;
+    constexpr size_t kChunk4 = 256 * 8;  // float4s per workgroup
+    for (auto& r : ranges) {
+      const int set = std::get<0>(r), cast = std::get<1>(r);
+      const size_t off = std::get<2>(r), n = std::get<3>(r);
+      if (off % 4 || n % 4 || off + n > (set == 0 ? nA : nD)) throw std::runtime_error("adam_rest: bad range");
+      for (size_t o4 = off / 4; o4 < (off + n) / 4; o4 += kChunk4)
+        blks.push_back({(unsigned long long)o4, (unsigned)std::min(kChunk4, (off + n) / 4 - o4), set, cast, 0});
+    }
+    if (blks.empty()) throw std::runtime_error("adam_rest: no ranges");
+    void* table = dev_alloc(blks.size() * sizeof(Blk), blks.data());
+    void* ctr = dev_alloc(sizeof(unsigned), nullptr, true);
+    const int nb = (int)blks.size();
+    AccList acc;
+    acc.w(wA, nA * 4).w(wbfA, nA * es_).r(gA, nA * 4).w(mA, nA * 4).w(vA, nA * 4).w(pA, 8)
+        .w(wD, nD * 4).w(wbfD, nD * es_).r(gD, nD * 4).w(mD, nD * 4).w(vD, nD * 4).w(pD, 8).w(step, 8)
+        .w((uintptr_t)ctr, 4);
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_adam_rest)(P<float>(wA), P<elem_t>(wbfA), P<const float>(gA), P<float>(mA), P<float>(vA),
+                               P<float>(pA), nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD),
+                               P<float>(mD), P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, table, nb, gscale,
+                               P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
+    }, acc.v);
+  }
   // narrow2.hip: TF-SAME stride-2 5x5 conv, 1..4 input -> 64 output channels, persistent `grid`
   // workgroups (<= tiles: nconv_tiles). bx != 0: fused BN-backward statistics of the layer below
   // (x = bx, y = by, one BN group), one partial row [2][64] per workgroup into part.
@@ -1005,7 +1046,11 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("last_mtiles", &Program::last_mtiles)
       .def("last_nphases", &Program::last_nphases)
       .def("wgrad", &Program::wgrad)
-      .def("wgrad3", &Program::wgrad3)
+      .def("wgrad3", &Program::wgrad3, py::arg("name"), py::arg("G"), py::arg("Hg"), py::arg("Wg"), py::arg("Mc"),
+           py::arg("Dm"), py::arg("Bn"), py::arg("Hd"), py::arg("Wd"), py::arg("Nc"), py::arg("pad"), py::arg("cfg"),
+           py::arg("splits"), py::arg("dst"), py::arg("scale"), py::arg("stream"),
+           py::arg("adam") = std::make_tuple((uintptr_t)0, (uintptr_t)0, (uintptr_t)0, (uintptr_t)0, 0.f, 0.f, 0.f, 0.f))
+      .def("adam_rest", &Program::adam_rest)
       .def("colstats", &Program::colstats)
       .def("bn_finalize", &Program::bn_finalize)
       .def("bn_coef_eval", &Program::bn_coef_eval, py::arg("name"), py::arg("C"), py::arg("gamma"), py::arg("beta"),

@@ -280,8 +280,19 @@ class HipEngine:
         self._keep.append(buf)
         return buf
 
+    def _wgrad_adam_wanted(self) -> bool:
+        """TF-Adam of the big conv / deconv weights inside their weight-gradient kernels (wgrad3
+        store pass) instead of in the update pass after the join: single-process bf16 "fused"
+        step only (DDP must all-reduce the gradient first; fp16 must check for overflow first).
+        The update pass then runs Adam over the remaining ranges and only re-writes the 16-bit
+        mirrors of the others. DCGAN_WGRAD_ADAM=0 turns it off (A/B)."""
+        return (not self.ddp and self.dt == 0 and self._schedule() == "fused"
+                and os.environ.get("DCGAN_WGRAD_ADAM", "1") != "0")
+
     def _build(self):
         self._keep: List[torch.Tensor] = []
+        self._wgrad_adam = self._wgrad_adam_wanted()
+        self._adam_fused: List[Tuple[int, int, int]] = []  # (set 0 = G / 1 = D, offset, numel)
         self.progA = self._prog()
         self.progB = self._prog()
         self.progW = self._prog()  # G's weight gradients (see _build_gloss_and_g_backward)
@@ -641,7 +652,7 @@ class HipEngine:
                                 gD[L.name + "/w"])
                 else:
                     self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
-                                gD[L.name + "/w"])
+                                gD[L.name + "/w"], adam_of=("d", L.name + "/w"))
                 if i == len(self.dl) - 1:
                     # head + top layer gradients final: DDP splits the segment here so their
                     # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
@@ -767,14 +778,26 @@ class HipEngine:
             prog.colsum_small(name, _p(x), rows, C, _p(sp), blocks, 0)
             prog.sum_partials(name + ".sum", _p(sp), blocks, C, C, _p(dst), 0)
 
-    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst, stream=0):
+    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst, stream=0, adam_of=None):
+        """adam_of = ("g" | "d", tensor name): with _wgrad_adam, the wgrad3 store pass also runs
+        that weight's TF-Adam (see _wgrad_adam_wanted)."""
         K = Bn * Hd * Wd
         taps = 1 if mode == 2 else 25
         if mode == 0 and not self.f32:  # 25-tap layers: LDS-DMA pipelined kernel, split-K reduced in-kernel
             plan = H.wgrad3_cfg_for(Mc, Nc, Bn, Hd, Wd, Hg)
             if plan is not None:
+                adam = (0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0)
+                if self._wgrad_adam and adam_of is not None:
+                    which, tname = adam_of
+                    ps, opt = (self.model.g, self.opt_g) if which == "g" else (self.model.d, self.opt_d)
+                    off, shape = ps.offsets[tname]
+                    assert dst.data_ptr() == self.grad_g.flat.data_ptr() + 4 * off if which == "g" else \
+                        dst.data_ptr() == self.grad_d.flat.data_ptr() + 4 * off
+                    adam = (_p(ps.flat) + 4 * off, _p(opt.m.flat) + 4 * off, _p(opt.v.flat) + 4 * off, _p(opt.powers),
+                            opt.lr, opt.beta1, opt.beta2, opt.eps)
+                    self._adam_fused.append((0 if which == "g" else 1, off, dst.numel()))
                 prog.wgrad3(name + ".wgrad", _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, plan[0], plan[1],
-                            _p(dst), 1.0, stream)
+                            _p(dst), 1.0, stream, adam)
                 return
         cfg, splits = H.pick_wgrad(Mc, Nc, K, taps, dtype=self.dt)
         if mode == 0 and not self.f32:
@@ -934,7 +957,7 @@ class HipEngine:
             pad = same_pads(L.out_hw)[0]
             w0 = progw.size()
             self._wgrad(progw, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
-                        gG[L.name + "/w"])
+                        gG[L.name + "/w"], adam_of=("g", L.name + "/w"))
             self._w_mark(prog, progw, w0, L.name)
             r = self._dgrad_bnb(prog, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc,
                                 src, 1, RELU)
@@ -983,9 +1006,29 @@ class HipEngine:
 
     def _build_update_fused(self, prog):
         """Single-process bf16: both TF-Adams + the beta-power / global-step update in one launch
-        (adam2_kernel), G's buffer first -- the same arithmetic as the separate kernels."""
+        (adam2_kernel), G's buffer first -- the same arithmetic as the separate kernels. When the
+        big weights' Adam already ran in their wgrad3 kernels (_wgrad_adam): adam_rest_kernel --
+        Adam over the other ranges, the 16-bit mirror re-written for those weights."""
         od, og = self.opt_d, self.opt_g
         G, Dm = self.model.g, self.model.d
+        if self._adam_fused:
+            ranges = []
+            for st, ps in ((0, G), (1, Dm)):
+                done = sorted((off, -(-n // 4) * 4) for s_, off, n in self._adam_fused if s_ == st)
+                pos = 0
+                for off, n in done:
+                    if off > pos:
+                        ranges.append((st, 0, pos, off - pos))
+                    ranges.append((st, 1, off, n))
+                    pos = off + n
+                if ps.flat.numel() > pos:
+                    ranges.append((st, 0, pos, ps.flat.numel() - pos))
+            prog.adam_rest("adam_rest", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
+                           _p(og.v.flat), _p(og.powers), G.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
+                           _p(Dm.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
+                           _p(od.powers), Dm.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, ranges, 1.0 / self.world,
+                           _p(self.step_counter), 0)
+            return
         prog.adam2("adam_gd", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
                    _p(og.powers), G.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat), _p(self.wbf_d.flat),
                    _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers), Dm.flat.numel(), od.lr,
@@ -1103,7 +1146,10 @@ class HipEngine:
         if self._graphs or self._step_host:
             raise RuntimeError("enable_timing() must precede the first train_step")
         self._timing = True
-        self._build_updates()
+        if self._wgrad_adam:  # the recorded wgrad kernels run Adam: re-record the step without it
+            self._build()
+        else:
+            self._build_updates()
         self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self._segments()) + 1)]
 
     def phase_times(self) -> Dict[str, float]:

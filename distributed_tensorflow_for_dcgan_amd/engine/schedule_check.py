@@ -174,9 +174,9 @@ def check(cfg=None, batch_size: int = 8, dtype: str = "bf16", world: int = 1, sc
     cfg = cfg or DCGANConfig()
     eng = HipEngine(cfg, batch_size, torch.device("cpu"), dtype=dtype, world=world, schedule=schedule, dry_run=True,
                     graph=False, allreduce_dtype=allreduce_dtype)
-    if timing:
+    if timing:  # (enable_timing without its CUDA events)
         eng._timing = True
-        eng._build_updates()
+        eng._build() if eng._wgrad_adam else eng._build_updates()
     hz, n = check_engine(eng, steps)
     return eng._schedule(), hz, n
 

@@ -425,3 +425,30 @@ def test_engine_sampler_zero_debias():
     ref_nodebias.g_bn.flat.copy_(eng.model.g_bn.flat)
     assert rel(s, s_ref) < 5e-2
     assert rel(s, s_ref) < rel(s, ref_nodebias.sampler(z))
+
+
+def test_wgrad_fused_adam_matches_the_update_pass(monkeypatch):
+    """Single-process bf16: TF-Adam of the six conv / deconv weights inside their wgrad3 store pass
+    (+ adam_rest over the remaining ranges and the mirrors) gives bit for bit the weights, Adam
+    slots, beta powers and losses of the one-launch update pass after the join (DCGAN_WGRAD_ADAM=0),
+    over 5 steps (graph replay)."""
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    dev = torch.device("cuda", 0)
+    cfg = DCGANConfig()
+    B = 16
+    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(2)) * 2 - 1).to(dev)
+    e1 = HipEngine(cfg, B, dev, graph=True, seed=2)
+    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
+    e2 = HipEngine(cfg, B, dev, graph=True, seed=2)
+    assert e1._wgrad_adam and not e2._wgrad_adam
+    e1.set_batch(real)
+    e2.set_batch(real)
+    for _ in range(5):
+        e1.train_step()
+        e2.train_step()
+    torch.cuda.synchronize()
+    for a, b in ((e1.model.g.flat, e2.model.g.flat), (e1.model.d.flat, e2.model.d.flat),
+                 (e1.wbf_g.flat, e2.wbf_g.flat), (e1.opt_g.m.flat, e2.opt_g.m.flat), (e1.opt_d.v.flat, e2.opt_d.v.flat),
+                 (e1.opt_g.powers, e2.opt_g.powers), (e1.opt_d.powers, e2.opt_d.powers)):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+    assert e1.last_losses() == e2.last_losses() and e1.global_step == e2.global_step == 5

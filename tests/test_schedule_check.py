@@ -34,7 +34,7 @@ def _dry(world=1, timing=False, schedule=None):
     eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=world, dry_run=True, graph=False, schedule=schedule)
     if timing:
         eng._timing = True
-        eng._build_updates()
+        eng._build() if eng._wgrad_adam else eng._build_updates()
     return eng
 
 
@@ -92,7 +92,8 @@ def test_op_accesses_are_recorded():
             if kind == eng.ext.OP_LAUNCH:
                 assert acc, "op %s records no accesses" % name
                 assert all(n > 0 for _, n, _ in acc)
-    assert ("adam_gd" in names or {"adam_g", "adam_d"} <= names) and any(n.startswith("d_head") and n.endswith("+loss") for n in names)
+    assert ("adam_gd" in names or "adam_rest" in names or {"adam_g", "adam_d"} <= names)
+    assert any(n.startswith("d_head") and n.endswith("+loss") for n in names)
     launches = sum(p.op_info(i)[2] == eng.ext.OP_LAUNCH for p in (eng.progA, eng.progB, eng.progW, eng.progC)
                    for i in range(p.size()))
     assert eng.kernel_count() == launches
@@ -213,3 +214,28 @@ def test_bf16_wire_direct_path_is_used():
     assert all(p != eng.grad_d.flat.data_ptr() for p, _, _ in eng._ar_drest.accesses())
     names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
     assert "adam_d" in names and "adam_g" in names
+
+
+def test_wgrad_adam_ranges_tile_both_buffers():
+    """Single-process bf16: the six conv / deconv weights get their TF-Adam in the wgrad3 store
+    pass; the update pass covers every other element of both flat buffers exactly once (Adam) and
+    re-writes the mirrors of the six (cast)."""
+    eng = _dry()
+    assert eng._wgrad_adam and len(eng._adam_fused) == 2 * (len(eng.gl) - 1)
+    names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
+    assert names == ["adam_rest"]
+    for s_, off, n in eng._adam_fused:
+        ps = eng.model.g if s_ == 0 else eng.model.d
+        assert any(o == off for o, _ in ps.offsets.values())
+    d2 = _dry(timing=True)  # the timed (segmented) step re-records without it
+    assert not d2._wgrad_adam and not d2._adam_fused
+    names = [d2.progC.op_info(i)[0] for i in range(d2.progC.size())]
+    assert "adam_rest" not in names
+
+
+def test_wgrad_adam_can_be_disabled(monkeypatch):
+    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
+    eng = _dry()
+    assert not eng._wgrad_adam
+    names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
+    assert names == ["adam_gd"]
