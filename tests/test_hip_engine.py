@@ -71,13 +71,16 @@ def _lrelu_d(a):
 @pytest.mark.parametrize("size,c_dim,B,dtype", [(64, 3, 16, "bf16"), (28, 1, 8, "bf16"), (128, 3, 4, "bf16"),
                                                 (256, 3, 4, "bf16"), (64, 3, 16, "fp16"), (256, 3, 4, "fp16"),
                                                 (64, 3, 8, "fp32"), (28, 1, 8, "fp32")])
-def test_engine_stagewise(size, c_dim, B, dtype):
+def test_engine_stagewise(size, c_dim, B, dtype, monkeypatch):
     """fp16 runs with the dynamic loss scale in the gradient seeds: every stage is compared
     against a recomputation from the engine's own (scaled) inputs, so the scale cancels.
-    Program A holds no optimiser op: the G stages are recomputed from the pre-update G weights.
-    fp32 (the reference precision) is held to 1e-4 per stage."""
+    Programs A / B / W hold no optimiser op here (the wgrad-fused Adam is off: it would update the
+    weights the oracle reads; test_wgrad_fused_adam_matches_the_update_pass covers it): the G
+    stages are recomputed from the pre-update G weights. fp32 (the reference precision) is held
+    to 1e-4 per stage."""
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     from distributed_tensorflow_for_dcgan_amd.ops import hip as H
+    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig(output_size=size, c_dim=c_dim)
     eng = HipEngine(cfg, B, dev, graph=False, seed=3, dtype=dtype)
