@@ -285,9 +285,12 @@ class HipEngine:
         store pass) instead of in the update pass after the join: single-process bf16 "fused"
         step only (DDP must all-reduce the gradient first; fp16 must check for overflow first).
         The update pass then runs Adam over the remaining ranges and only re-writes the 16-bit
-        mirrors of the others. DCGAN_WGRAD_ADAM=0 turns it off (A/B)."""
+        mirrors of the others. Bit-identical to the update pass, but measured 17 % SLOWER
+        (1.26 vs 1.07 ms/step: the last-arriving split-K workgroups run the whole tile's Adam
+        serially on the chains' critical path; profiles/r5/ab_wgrad_adam_r5.txt), so off unless
+        DCGAN_WGRAD_ADAM=1."""
         return (not self.ddp and self.dt == 0 and self._schedule() == "fused"
-                and os.environ.get("DCGAN_WGRAD_ADAM", "1") != "0")
+                and os.environ.get("DCGAN_WGRAD_ADAM", "0") == "1")
 
     def _build(self):
         self._keep: List[torch.Tensor] = []

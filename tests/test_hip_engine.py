@@ -440,6 +440,7 @@ def test_wgrad_fused_adam_matches_the_update_pass(monkeypatch):
     cfg = DCGANConfig()
     B = 16
     real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(2)) * 2 - 1).to(dev)
+    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "1")
     e1 = HipEngine(cfg, B, dev, graph=True, seed=2)
     monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
     e2 = HipEngine(cfg, B, dev, graph=True, seed=2)

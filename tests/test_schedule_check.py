@@ -140,6 +140,14 @@ def test_ddp_schedule_env_selects_the_schedule(monkeypatch, good):
     assert hz == []
 
 
+@pytest.mark.parametrize("wa", ["0", "1"])
+def test_wgrad_adam_schedule_has_no_hazards(monkeypatch, wa):
+    monkeypatch.setenv("DCGAN_WGRAD_ADAM", wa)
+    eng = _dry()
+    hz, _ = SC.check_engine(eng)
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
 @pytest.mark.parametrize("n", ["0", "1", "2", "4"])
 def test_fused_g_wgrad_tail_on_main_has_no_hazards(monkeypatch, n):
     """DCGAN_GW_TAIL_ON_MAIN=n: the last n G weight gradients of the fused step on the G chain's
@@ -216,10 +224,11 @@ def test_bf16_wire_direct_path_is_used():
     assert "adam_d" in names and "adam_g" in names
 
 
-def test_wgrad_adam_ranges_tile_both_buffers():
-    """Single-process bf16: the six conv / deconv weights get their TF-Adam in the wgrad3 store
-    pass; the update pass covers every other element of both flat buffers exactly once (Adam) and
-    re-writes the mirrors of the six (cast)."""
+def test_wgrad_adam_ranges_tile_both_buffers(monkeypatch):
+    """DCGAN_WGRAD_ADAM=1, single-process bf16: the six conv / deconv weights get their TF-Adam
+    in the wgrad3 store pass; the update pass covers every other element of both flat buffers
+    exactly once (Adam) and re-writes the mirrors of the six (cast)."""
+    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "1")
     eng = _dry()
     assert eng._wgrad_adam and len(eng._adam_fused) == 2 * (len(eng.gl) - 1)
     names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
@@ -233,8 +242,7 @@ def test_wgrad_adam_ranges_tile_both_buffers():
     assert "adam_rest" not in names
 
 
-def test_wgrad_adam_can_be_disabled(monkeypatch):
-    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
+def test_wgrad_adam_is_off_by_default():
     eng = _dry()
     assert not eng._wgrad_adam
     names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
