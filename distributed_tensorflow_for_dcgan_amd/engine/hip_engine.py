@@ -1184,16 +1184,20 @@ class HipEngine:
         stream, except the last _gw_tail_on_main() of them, which follow the G chain on cs."""
         ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
         ex.wait(ex.alt[0], cs)
+        # host issue order (eager replay): the first DCGAN_G_FIRST ops of the G chain go out before
+        # the D chain's, so they sit first in the forward's queue
+        g_first = min(self._a_fwd + self._g_first(), self._g_w[0][0] if self._g_w else self.progA.size())
+        ex.run(self.progA, [cs, ex.side], self._a_fwd, g_first)
         ex.run(self.progB, ex.alt)
         # the G chain: data gradients on cs; each G weight gradient on the D chain's stream after
         # that chain, once cs has produced its operand (a mark after that progA position)
         if not self._g_wgrad_on_d_stream():  # every G gradient on cs
-            ex.run(self.progA, [cs, ex.side], self._a_fwd, -1)
+            ex.run(self.progA, [cs, ex.side], g_first, -1)
             ex.run(self.progW, [cs, ex.side])
             ex.wait(cs, ex.alt[0])
             ex.run(self.progC, [cs, ex.side])
             return
-        pos, marks = self._a_fwd, []
+        pos, marks = g_first, []
         for a_end, _ in self._g_w:
             ex.run(self.progA, [cs, ex.side], pos, a_end)
             marks.append(ex.mark(cs))
@@ -1211,6 +1215,13 @@ class HipEngine:
             ex.run(self.progW, [cs, ex.side], w, -1)
         ex.wait(cs, ex.alt[0])
         ex.run(self.progC, [cs, ex.side])
+
+    def _g_first(self) -> int:
+        """DCGAN_G_FIRST=k: issue the G chain's first k ops before the D chain's (study switch)."""
+        v = os.environ.get("DCGAN_G_FIRST", "0")
+        if not v.isdigit():
+            raise ValueError("DCGAN_G_FIRST must be a non-negative integer, got %r" % v)
+        return int(v)
 
     def _gw_tail_on_main(self) -> int:
         """Number of trailing G weight-gradient segments the fused step runs on the G chain's
