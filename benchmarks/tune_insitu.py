@@ -26,9 +26,12 @@ from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
 from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
 
 
+GRAPH = False  # --graph: time the hipGraph replay instead of the (default) C++ launch replay
+
+
 def step_ms(cfg, B, steps, warmup, dtype="bf16"):
     dev = torch.device("cuda", 0)
-    eng = HipEngine(cfg, B, dev, seed=0, dtype=dtype)
+    eng = HipEngine(cfg, B, dev, seed=0, dtype=dtype, graph=GRAPH)
     real = torch.rand(B, cfg.output_size, cfg.output_size, cfg.c_dim, device=dev) * 2 - 1
     eng.set_synthetic_batch(real)
     for _ in range(warmup):
@@ -147,8 +150,11 @@ def main():
     ap.add_argument("--c_dim", type=int, default=3)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--write", action="store_true")
+    ap.add_argument("--graph", type=int, default=0, help="1: tune under hipGraph replay (the pre-round-5 default)")
     ap.add_argument("--out", default="", help="also write the resulting table (JSON) here")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = bool(a.graph)
     cfg = DCGANConfig(output_size=a.output_size, c_dim=a.c_dim)
     table = H.tuned_table()
     keys = used_keys(cfg, a.batch, a.dtype, a.seed)
