@@ -544,6 +544,44 @@ class Program {
                               P<elem_t>(dx), R, C, rows_per_group, act, leak, s);
     }, acc.v);
   }
+  // BN finalize + apply in one launch (bnfold.hip): each workgroup reduces its own group's partial
+  // rows for its 64 channels; the same reads and writes as bn_finalize + bn_apply_act together
+  bool bn_fold_ok(int ppg, int groups, int C, int rows_per_group) const {
+    return KF(dcg_bnfold_ok)(ppg, groups, C, rows_per_group) != 0;
+  }
+  int bn_fold_fwd(std::string name, uintptr_t part, int ppg, int groups, int C, double count, uintptr_t gamma,
+                  uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
+                  uintptr_t ema_mean, uintptr_t ema_var, float decay, uintptr_t x, uintptr_t y, int R, int act,
+                  float leak, int stream) {
+    if (R % groups || !bn_fold_ok(ppg, groups, C, R / groups)) throw std::runtime_error(name + ": bn_fold_fwd shape");
+    const size_t gc = (size_t)groups * C * 4, t = (size_t)R * C * es_;
+    AccList acc;
+    acc.r(part, (size_t)groups * ppg * 2 * C * 4).r(gamma, (size_t)C * 4).r(beta, (size_t)C * 4)
+        .w(mean, gc).w(rstd, gc).w(scale, gc).w(shift, gc).w(ema_mean, gc).w(ema_var, gc).r(x, t).w(y, t);
+    const int rpg = R / groups;
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_bnfold_fwd)(P<const float>(part), ppg, groups, C, rpg, count, P<const float>(gamma),
+                                P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
+                                P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, P<const elem_t>(x),
+                                P<elem_t>(y), act, leak, s);
+    }, acc.v);
+  }
+  int bn_fold_bwd(std::string name, uintptr_t part, int ppg, int groups, int C, float count, uintptr_t gamma,
+                  uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, uintptr_t dy,
+                  uintptr_t y, uintptr_t x, uintptr_t dx, int R, int act, float leak, int stream) {
+    if (R % groups || !bn_fold_ok(ppg, groups, C, R / groups)) throw std::runtime_error(name + ": bn_fold_bwd shape");
+    const size_t gc = (size_t)groups * C * 4, t = (size_t)R * C * es_;
+    AccList acc;
+    acc.r(part, (size_t)groups * ppg * 2 * C * 4).r(gamma, (size_t)C * 4).r(mean, gc).r(rstd, gc)
+        .w(dgamma, (size_t)C * 4).w(dbeta, (size_t)C * 4).w(coef, 3 * gc).r(dy, t).r(x, t).r(y, t).w(dx, t);
+    const int rpg = R / groups;
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_bnfold_bwd)(P<const float>(part), ppg, groups, C, rpg, count, P<const float>(gamma),
+                                P<const float>(mean), P<const float>(rstd), P<float>(dgamma), P<float>(dbeta),
+                                P<float>(coef), P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x),
+                                P<elem_t>(dx), act, leak, s);
+    }, acc.v);
+  }
   int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_act_bwd)(P<const elem_t>(dy), P<const elem_t>(y), P<elem_t>(dx), n, act, leak, s);
@@ -1097,6 +1135,9 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("head_bwd_rs", &Program::head_bwd_rs)
       .def("narrow_deconv_bnin", &Program::narrow_deconv_bnin)
       .def("nwgrad_ok", &Program::nwgrad_ok)
+      .def("bn_fold_ok", &Program::bn_fold_ok)
+      .def("bn_fold_fwd", &Program::bn_fold_fwd)
+      .def("bn_fold_bwd", &Program::bn_fold_bwd)
       .def("nwgrad", &Program::nwgrad, py::arg("name"), py::arg("x"), py::arg("B"), py::arg("H"), py::arg("W"),
            py::arg("Cin"), py::arg("d"), py::arg("Hd"), py::arg("Wd"), py::arg("pad"), py::arg("dst"), py::arg("stream"),
            py::arg("chunks_per_wg") = 0)

@@ -79,14 +79,30 @@ def _kpad(c: int) -> int:
     return -(-25 * c // 16) * 16
 
 
+_STREAMS: Dict[int, Tuple["torch.cuda.Stream", ...]] = {}
+
+
+def _engine_streams(dev: torch.device):
+    """The side / D-chain streams, created ONCE per device and process: HIP maps each new stream
+    onto one of a few hardware queues in turn, so an engine built after many others could get its
+    D-chain stream on the main stream's queue -- the two backward chains then serialise (seen as
+    28 % slower steps every few engine builds in the in-situ tuner). Shared streams keep the first
+    engine's mapping for every later one (engines of a process never run concurrently)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _STREAMS:
+        _STREAMS[key] = tuple(torch.cuda.Stream(device=dev) for _ in range(3))
+    return _STREAMS[key]
+
+
 class _TorchExec:
     """Issues a schedule onto real HIP streams (torch.cuda.Stream objects)."""
 
     def __init__(self, eng: "HipEngine"):
         dev = eng.device
         self.dev = dev
-        self.side = torch.cuda.Stream(device=dev)                        # slot 1 of main-stream segments
-        self.alt = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]  # D chain (+ its slot 1)
+        side, a0, a1 = _engine_streams(dev)
+        self.side = side                 # slot 1 of main-stream segments
+        self.alt = [a0, a1]              # D chain (+ its slot 1)
         self.comm = eng.comm_stream
 
     def main(self):
@@ -470,12 +486,27 @@ class HipEngine:
         P = self.model.d if name.startswith("d_") else self.model.g
         ema_m = bnstate.mean[name] if update_ema else None
         ema_v = bnstate.var[name] if update_ema else None
+        if apply and self._bn_fold(prog, ppg, groups, C, rows):
+            prog.bn_fold_fwd(name + ".fin_apply", _p(part), ppg, groups, C, float(rows // groups),
+                             _p(P[name + "/gamma"]), _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]),
+                             _p(st["rstd"]), _p(st["scale"]), _p(st["shift"]), _p(ema_m), _p(ema_v),
+                             cfgm.bn_momentum, _p(x), _p(y), rows, act, cfgm.lrelu_leak, 0)
+            return
         prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
                          _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
                          _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
         if apply:
             prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
                               rows // groups, act, cfgm.lrelu_leak, 0)
+
+    def _bn_fold(self, prog, ppg: int, groups: int, C: int, rows: int) -> bool:
+        """BN finalize folded into the apply launch (bnfold.hip) when a group has at most
+        DCGAN_BN_FOLD partial rows (default 64; 0 = never): every apply workgroup then reduces
+        its own channels' partial rows -- cheap only while they are few."""
+        v = os.environ.get("DCGAN_BN_FOLD", "64")
+        if not v.isdigit():
+            raise ValueError("DCGAN_BN_FOLD must be a non-negative integer, got %r" % v)
+        return 0 < ppg <= min(int(v), 256) and rows % groups == 0 and prog.bn_fold_ok(ppg, groups, C, rows // groups)
 
     @staticmethod
     def _rows_per_block(rows_per_group: int, C: int) -> int:
@@ -831,6 +862,11 @@ class HipEngine:
                           self.cfg.lrelu_leak, rows, C, rpb, rpg, _p(part), 0)
         dg = grads[name + "/gamma"] if write_param_grads else None
         db = grads[name + "/beta"] if write_param_grads else None
+        if self._bn_fold(prog, Pn // groups, groups, C, rows):
+            prog.bn_fold_bwd(name + ".bwd_fin_apply", _p(part), Pn // groups, groups, C, float(rpg),
+                             _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), _p(dy), _p(y),
+                             _p(x), _p(dx), rows, act, self.cfg.lrelu_leak, 0)
+            return
         prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg),
                              _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
         prog.bn_bwd_apply(name + ".bwd_apply", _p(dy), _p(y), _p(x), _p(coef), _p(dx), rows, C, rpg, act,

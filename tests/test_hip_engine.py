@@ -456,3 +456,34 @@ def test_wgrad_fused_adam_matches_the_update_pass(monkeypatch):
                  (e1.opt_g.powers, e2.opt_g.powers), (e1.opt_d.powers, e2.opt_d.powers)):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max()
     assert e1.last_losses() == e2.last_losses() and e1.global_step == e2.global_step == 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,B", [("bf16", 128), ("bf16", 16), ("fp32", 32)])
+def test_bn_fold_is_bit_identical_to_finalize_then_apply(monkeypatch, dtype, B):
+    """BN finalize folded into the apply launch (bnfold.hip, DCGAN_BN_FOLD=256: every layer with
+    <= 256 partial rows per group) gives bit for bit the weights, Adam slots, BN moving averages
+    and losses of the two-launch path (DCGAN_BN_FOLD=0) over 3 steps, with fewer launches."""
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    dev = torch.device("cuda", 0)
+    cfg = DCGANConfig()
+    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(3)) * 2 - 1).to(dev)
+    monkeypatch.setenv("DCGAN_BN_FOLD", "256")
+    e1 = HipEngine(cfg, B, dev, dtype=dtype, graph=False, seed=3)
+    monkeypatch.setenv("DCGAN_BN_FOLD", "0")
+    e2 = HipEngine(cfg, B, dev, dtype=dtype, graph=False, seed=3)
+    assert e1.kernel_count() < e2.kernel_count()
+    e1.set_batch(real)
+    e2.set_batch(real)
+    for _ in range(3):
+        e1.train_step()
+        e2.train_step()
+    torch.cuda.synchronize()
+    pairs = [(e1.model.g.flat, e2.model.g.flat), (e1.model.d.flat, e2.model.d.flat),
+             (e1.opt_g.m.flat, e2.opt_g.m.flat), (e1.opt_d.v.flat, e2.opt_d.v.flat)]
+    for bs1, bs2 in ((e1.model.g_bn, e2.model.g_bn), (e1.model.d_bn, e2.model.d_bn)):
+        for k in bs1.mean:
+            pairs += [(bs1.mean[k], bs2.mean[k]), (bs1.var[k], bs2.var[k])]
+    for a, b in pairs:
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+    assert e1.last_losses() == e2.last_losses()

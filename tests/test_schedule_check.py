@@ -148,6 +148,20 @@ def test_wgrad_adam_schedule_has_no_hazards(monkeypatch, wa):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
+@pytest.mark.parametrize("fold", ["0", "64", "256"])
+def test_bn_fold_schedule_has_no_hazards(monkeypatch, fold):
+    """BN finalize folded into the apply launches (DCGAN_BN_FOLD): same hazard-free step, one
+    launch fewer per folded layer."""
+    monkeypatch.setenv("DCGAN_BN_FOLD", fold)
+    eng = _dry()
+    hz, _ = SC.check_engine(eng)
+    assert hz == [], "\n".join(map(str, hz[:10]))
+    names = [eng.progA.op_info(i)[0] for i in range(eng.progA.size())]
+    names += [eng.progB.op_info(i)[0] for i in range(eng.progB.size())]
+    n_fold = sum(1 for n in names if n.endswith("fin_apply"))
+    assert (n_fold == 0) == (fold == "0"), n_fold
+
+
 @pytest.mark.parametrize("n", ["0", "1", "2", "4"])
 def test_fused_g_wgrad_tail_on_main_has_no_hazards(monkeypatch, n):
     """DCGAN_GW_TAIL_ON_MAIN=n: the last n G weight gradients of the fused step on the G chain's
