@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void bn_apply_act_kernel(const elem_t* __restr
     load8f(scale + g * C + c, sc);
     load8f(shift + g * C + c, sh);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xv[i] = apply_act(xv[i] * sc[i] + sh[i], act, leak);
+    for (int i = 0; i < 8; ++i) xv[i] = apply_act(__builtin_fmaf(xv[i], sc[i], sh[i]), act, leak);
     store8(y + (size_t)v * 8, xv);
   }
 }
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const elem_t* __restr
     load8f(coef + (g * 3 + 1) * C + c, cb);
     load8f(coef + (g * 3 + 2) * C + c, cc);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dv[i] = ca[i] * (dv[i] * ag[i]) + cb[i] * xv[i] + cc[i];
+    for (int i = 0; i < 8; ++i) dv[i] = __builtin_fmaf(ca[i], dv[i] * ag[i], __builtin_fmaf(cb[i], xv[i], cc[i]));
     store8(dx + (size_t)v * 8, dv);
   }
 }

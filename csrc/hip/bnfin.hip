@@ -89,11 +89,11 @@ __global__ __launch_bounds__(256) void bnfin_fwd_kernel(const float* __restrict_
     rstd_out[idx] = r;
     const float sc = gamma[c] * r;
     scale_out[idx] = sc;
-    shift_out[idx] = beta[c] - mf * sc;
+    shift_out[idx] = __builtin_fmaf(-mf, sc, beta[c]);  // explicit fma: bnfold.hip computes the same bits
     if (ema_mean) {  // TF ExponentialMovingAverage, slot = group
       const float al = 1.f - decay;
-      ema_mean[idx] -= al * (ema_mean[idx] - mf);
-      ema_var[idx] -= al * (ema_var[idx] - vf);
+      ema_mean[idx] = __builtin_fmaf(-al, ema_mean[idx] - mf, ema_mean[idx]);
+      ema_var[idx] = __builtin_fmaf(-al, ema_var[idx] - vf, ema_var[idx]);
     }
   }
 }
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void bnfin_bwd_kernel(const float* __restrict_
       const float bb = -A * s1 / count;
       coef[(g * 3 + 0) * C + c] = A;
       coef[(g * 3 + 1) * C + c] = c2 * r;
-      coef[(g * 3 + 2) * C + c] = bb - c2 * mu * r;
+      coef[(g * 3 + 2) * C + c] = __builtin_fmaf(-(c2 * mu), r, bb);
     }
     __syncthreads();
   }

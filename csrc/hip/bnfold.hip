@@ -10,7 +10,8 @@
 //
 // The reduction order is bnfin.hip's (partial row 64 w + l on lane l of slot w, an xor butterfly
 // per slot in double, slots added in order), so the statistics are bit-identical to the
-// two-launch path. Reference op: batch_norm + moments + EMA, /root/reference/distriubted_model.py:37-50.
+// two-launch path, and every multiply-add is an explicit fma in both (bn.hip / bnfin.hip too), so
+// the outputs are bit-identical as well. Reference op: batch_norm + moments + EMA, /root/reference/distriubted_model.py:37-50.
 #include "kernels.h"
 
 namespace dcg {
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void bnfold_fwd_kernel(
     if (v < 0.0) v = 0.0;
     const float mf = (float)m, vf = (float)v;
     const float r = rsqrtf(vf + eps);
-    const float sc = gamma[c] * r, sh = beta[c] - mf * sc;
+    const float sc = gamma[c] * r, sh = __builtin_fmaf(-mf, sc, beta[c]);
     sc_s[tid] = sc;
     sh_s[tid] = sh;
     if (ch == 0) {
@@ -117,8 +118,8 @@ __global__ __launch_bounds__(256) void bnfold_fwd_kernel(
       shift_out[idx] = sh;
       if (ema_mean) {  // TF ExponentialMovingAverage, slot = group
         const float al = 1.f - decay;
-        ema_mean[idx] -= al * (ema_mean[idx] - mf);
-        ema_var[idx] -= al * (ema_var[idx] - vf);
+        ema_mean[idx] = __builtin_fmaf(-al, ema_mean[idx] - mf, ema_mean[idx]);
+        ema_var[idx] = __builtin_fmaf(-al, ema_var[idx] - vf, ema_var[idx]);
       }
     }
   }
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256) void bnfold_fwd_kernel(
     if (r < r1) {
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = apply_act((float)xr[it][i] * sc[i] + sh[i], act, leak);
+      for (int i = 0; i < 8; ++i) v[i] = apply_act(__builtin_fmaf((float)xr[it][i], sc[i], sh[i]), act, leak);
       bnf_store8(y + (size_t)r * C + vc, v);
     }
   }
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void bnfold_bwd_kernel(
       const float A = gamma[c] * r;
       const float c2 = -A * s2 / count;
       const float bb = -A * s1 / count;
-      const float cb = c2 * r, cc = bb - c2 * mu * r;
+      const float cb = c2 * r, cc = __builtin_fmaf(-(c2 * mu), r, bb);
       if (gg == g) {
         ca_s[tid] = A;
         cb_s[tid] = cb;
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void bnfold_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float ag = act_grad_from_out((float)yr[it][i], act, leak);
-        dv[i] = ca[i] * ((float)dr[it][i] * ag) + cb[i] * (float)xr[it][i] + cc[i];
+        dv[i] = __builtin_fmaf(ca[i], (float)dr[it][i] * ag, __builtin_fmaf(cb[i], (float)xr[it][i], cc[i]));
       }
       bnf_store8(dx + (size_t)r * C + vc, dv);
     }

@@ -501,9 +501,12 @@ class HipEngine:
 
     def _bn_fold(self, prog, ppg: int, groups: int, C: int, rows: int) -> bool:
         """BN finalize folded into the apply launch (bnfold.hip) when a group has at most
-        DCGAN_BN_FOLD partial rows (default 64; 0 = never): every apply workgroup then reduces
-        its own channels' partial rows -- cheap only while they are few."""
-        v = os.environ.get("DCGAN_BN_FOLD", "64")
+        DCGAN_BN_FOLD partial rows (0 = never, the default): every apply workgroup then reduces its
+        own channels' partial rows. Bit-identical, but measured slower: 64x64 step 113.7k-114.8k
+        img/s with the 8 layers of <= 64 rows folded (61 launches), 96.1k-96.7k with all 13 of
+        <= 256 (55 launches), vs 120.0k-120.7k unfolded (profiles/r5/ab_bn_fold_r5.txt): the
+        per-workgroup fp64 reduction sits in front of every apply workgroup, on the chain."""
+        v = os.environ.get("DCGAN_BN_FOLD", "0")
         if not v.isdigit():
             raise ValueError("DCGAN_BN_FOLD must be a non-negative integer, got %r" % v)
         return 0 < ppg <= min(int(v), 256) and rows % groups == 0 and prog.bn_fold_ok(ppg, groups, C, rows // groups)
