@@ -33,48 +33,52 @@ __device__ __forceinline__ void bnf_store8(elem_t* p, const float* f) {
 }
 
 // sums of the partial rows [p0, p0 + n) (n <= 256) of both statistics for channels c0..c0+63 into
-// tot[2][64] (LDS, double). Wave q takes channel quads q, q + 4, q + 8, q + 12.
+// tot[2][64] (LDS, double). Lane group (16 lanes) q = threadIdx.x / 16 owns channel quad q; its
+// lane l (0..15) adds rows l, l+16, l+32, l+48 of each 64-row slot as (r0 + r32) + (r16 + r48) --
+// exactly what lane l holds after the xor-32 and xor-16 steps of bnfin.hip's 64-lane butterfly --
+// then runs that butterfly's xor 8 / 4 / 2 / 1 steps; slots are added in order. So the sums are
+// bnfin's bit for bit, with a quarter of its shuffles and every quad reduced at once.
 __device__ __forceinline__ void bnf_sums(const float* __restrict__ part, int p0, int n, int C, int c0, double* tot) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l = threadIdx.x & 15, q = threadIdx.x >> 4, c = c0 + 4 * q;
   const int nslot = (n + 63) >> 6;
+  double acc[8];
 #pragma unroll
-  for (int qq = 0; qq < 4; ++qq) {
-    const int q = wave + 4 * qq, c = c0 + 4 * q;
-    double acc[8];
+  for (int i = 0; i < 8; ++i) acc[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.0;
+  for (int w = 0; w < 4; ++w) {
+    if (w < nslot) {  // workgroup-uniform
+      double v[4][8];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      if (w < nslot) {  // wave-uniform
-        const int r = 64 * w + lane;
-        double a[8];
+      for (int j = 0; j < 4; ++j) {
+        const int r = 64 * w + l + 16 * j;
         if (r < n) {
           const float* row = part + (size_t)(p0 + r) * 2 * C + c;
           const f32x4 s = *reinterpret_cast<const f32x4*>(row);
           const f32x4 t = *reinterpret_cast<const f32x4*>(row + C);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            a[i] = (double)s[i];
-            a[4 + i] = (double)t[i];
+            v[j][i] = (double)s[i];
+            v[j][4 + i] = (double)t[i];
           }
         } else {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = 0.0;
+          for (int i = 0; i < 8; ++i) v[j][i] = 0.0;
         }
+      }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 8; ++i) {
+        double a = (v[0][i] + v[2][i]) + (v[1][i] + v[3][i]);
 #pragma unroll
-          for (int o = 32; o > 0; o >>= 1) a[i] += __shfl_xor(a[i], o, 64);
-          acc[i] = w == 0 ? a[i] : acc[i] + a[i];
-        }
+        for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        acc[i] = w == 0 ? a : acc[i] + a;
       }
     }
-    if (lane == 0) {
+  }
+  if (l == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        tot[4 * q + i] = acc[i];
-        tot[BNF_CW + 4 * q + i] = acc[4 + i];
-      }
+    for (int i = 0; i < 4; ++i) {
+      tot[4 * q + i] = acc[i];
+      tot[BNF_CW + 4 * q + i] = acc[4 + i];
     }
   }
 }

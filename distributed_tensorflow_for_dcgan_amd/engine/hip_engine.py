@@ -504,8 +504,10 @@ class HipEngine:
         DCGAN_BN_FOLD partial rows (0 = never, the default): every apply workgroup then reduces its
         own channels' partial rows. Bit-identical, but measured slower: 64x64 step 113.7k-114.8k
         img/s with the 8 layers of <= 64 rows folded (61 launches), 96.1k-96.7k with all 13 of
-        <= 256 (55 launches), vs 120.0k-120.7k unfolded (profiles/r5/ab_bn_fold_r5.txt): the
-        per-workgroup fp64 reduction sits in front of every apply workgroup, on the chain."""
+        <= 256 (55 launches), vs 120.0k-120.7k unfolded; with the cheaper 16-lane-group reduction
+        116.1k-116.8k / 113.0k-113.5k vs 118.7k-120.5k (profiles/r5/ab_bn_fold_r5.txt): each fused
+        launch still runs the whole dependent chain (partials -> fp64 sums -> coefficients ->
+        apply) in every workgroup, and the kernel boundary it removes costs ~1 us."""
         v = os.environ.get("DCGAN_BN_FOLD", "0")
         if not v.isdigit():
             raise ValueError("DCGAN_BN_FOLD must be a non-negative integer, got %r" % v)
