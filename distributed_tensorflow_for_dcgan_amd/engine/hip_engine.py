@@ -321,12 +321,12 @@ class HipEngine:
         self._a_fwd = self.progA.size()  # forward done: D's d_loss backward may start from here
         self._build_gloss_and_g_backward(self.progA, self.progW)
         self._build_d_backward_dloss(self.progB)  # sets self._b_split (top layer done)
-        self._build_updates()
         # D-gradient slice final after the D chain's first segment: the top conv layer (+ its BN)
         # and the head, which the ParamSet lays out last
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
         self._g_cuts = self._g_bucket_cuts()
         self._g_split = self._g_split_plan()
+        self._build_updates()  # (after the G split: Adam(G) follows its collectives)
         self.progX, self._wire_ops = self._prog(), {}
         if self.wire_d is not None:  # fp32 gradient slice -> its bf16 wire image, one op per collective
             o = self._d_top_off
@@ -359,12 +359,12 @@ class HipEngine:
         sch = self._schedule()
         if sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
-            self._c_split = self.progC.size()
+            self._c_split = self._c_split_a = self.progC.size()
         elif sch in ("concurrent", "ddp") and not self.f16:
             self._build_update_d_first(self.progC)
         else:
             self._build_update(self.progC, first=True)
-            self._c_split = self.progC.size()
+            self._c_split = self._c_split_a = self.progC.size()
             self._build_update(self.progC, first=False)
 
     def _build_update_d_first(self, prog):
@@ -379,8 +379,24 @@ class HipEngine:
         prog.adam_bf("adam_d", _p(self.model.d.flat), md, _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
                      _p(od.powers), self.model.d.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, 0, ls, wd)
         self._c_split = prog.size()
-        prog.adam_bf("adam_g", _p(self.model.g.flat), mg, _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
-                     _p(og.powers), self.model.g.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, gs, 0, ls, wg)
+        G = self.model.g
+        es = 0 if self.f32 else self.wbf_g.flat.element_size()
+
+        def adam_g(name, a, b):  # Adam(G) over G's flat range [a, b)
+            if b > a:
+                prog.adam_bf(name, _p(G.flat) + 4 * a, mg + es * a if mg else 0, _p(self.grad_g.flat) + 4 * a,
+                             _p(og.m.flat) + 4 * a, _p(og.v.flat) + 4 * a, _p(og.powers), b - a, og.lr, og.beta1,
+                             og.beta2, og.eps, gs, 0, ls, wg + 2 * a if wg else 0)
+        n = G.flat.numel()
+        if self._adam_g_split():
+            lo, hi = self._g_split[3:]
+            adam_g("adam_g_a", lo, hi)      # g_h1's slice: right after its own collective
+            self._c_split_a = prog.size()
+            adam_g("adam_g_b", hi, n)
+            adam_g("adam_g_c", 0, lo)
+        else:
+            self._c_split_a = self._c_split
+            adam_g("adam_g", 0, n)
         prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
                       _p(self.step_counter), 0, ls, self.LOSS_SCALE_GROWTH)
 
@@ -1150,12 +1166,15 @@ class HipEngine:
             a_need, wb, we = sp[:3]
             g_chain = [(A, self._a_fwd, a_need), (W, wb, we)] + wx("g_a")
             g_tail = [(A, a_need, -1), (W, 0, wb), (W, we, -1)] + wx("g_b") + wx("g_c")
-        return [("fwd", lin([(A, 0, self._a_fwd)]), M),
+        segs = [("fwd", lin([(A, 0, self._a_fwd)]), M),
                 ("D_bwd_top", lin([(B, 0, self._b_split)] + wx("dtop")), self.ALT),
                 ("G_chain", lin(g_chain), M),
                 ("D_bwd_rest", lin([(B, self._b_split, -1)] + wx("drest")), self.ALT),
-                ("G_tail", lin(g_tail), M), ("adam_D", lin([(C, 0, self._c_split)]), M),
-                ("adam_G", lin([(C, self._c_split, -1)]), M)]
+                ("G_tail", lin(g_tail), M)]
+        if self._adam_g_split():
+            segs.append(("adam_G_a", lin([(C, self._c_split, self._c_split_a)]), M))
+        return segs + [("adam_D", lin([(C, 0, self._c_split)]), M),
+                       ("adam_G", lin([(C, self._c_split_a, -1)]), M)]
 
     @staticmethod
     def _lin_segment(parts):
@@ -1164,6 +1183,16 @@ class HipEngine:
                 ex.run(prog, [cs, sec], b, e)
         run.empty = all((prog.size() if e < 0 else e) <= b for prog, b, e in parts)
         return run
+
+    def _adam_g_split(self) -> bool:
+        """Segmented DDP step: Adam over g_h1's gradient slice runs as soon as that slice's
+        collective (the first G one, the largest) has landed, beside the remaining collectives;
+        Adam over the rest of G after the last one (DCGAN_ADAM_G_SPLIT=0: one Adam(G) at the end).
+        Under the RCCL-like stand-in at W=8: 1.383 vs 1.394-1.399 ms (fp32 wire, 150 GB/s), 1.305 vs
+        1.317-1.319 (bf16), 1.310 vs 1.320 (fp32, 300 GB/s); at W=1 within the spread
+        (profiles/r5/ab_adam_g_split_r5.txt)."""
+        return (self._schedule() == "concurrent" and self._g_split is not None and not self.f16
+                and os.environ.get("DCGAN_ADAM_G_SPLIT", "1") != "0")
 
     def _wire_direct(self) -> bool:
         """bf16 wire without copies (segmented DDP step, bf16 engine): cast kernels inside the
@@ -1365,8 +1394,10 @@ class HipEngine:
             self._ar_launch(ex, "dtop", alt)
             self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward to g_h1's wgrad
             self._tick(3, cs)
+            a_done = None
             if self._g_split is not None:
                 self._ar_launch(ex, "gsplit_a", cs)  # g_h1's slice, under the rest of both chains
+                a_done = ex.mark(ex.comm) if self.ddp else None
             self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
             self._seg(ex, 4, cs)               # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
@@ -1379,14 +1410,21 @@ class HipEngine:
                 self._ar_launch(ex, "gsplit_c", cs)
             else:
                 self._ar_launch(ex, "g", cs)
+            i = 5
+            if self._adam_g_split():
+                if a_done is not None:
+                    ex.wait_mark(cs, a_done)   # g_h1's collective (dtop's too: comm-stream order)
+                self._seg(ex, i, cs)           # Adam over g_h1's slice, beside the other collectives
+                i += 1
+                self._tick(i, cs)
             if d_done is not None:
                 ex.wait_mark(cs, d_done)       # dtop + drest (and g_h1's) collectives
             ex.wait(cs, alt)                   # (W = 1, timed: the D chain itself)
-            self._seg(ex, 5, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
-            self._tick(6, cs)
+            self._seg(ex, i, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
+            self._tick(i + 1, cs)
             self._ar_join(ex, cs)              # G's collectives
-            self._seg(ex, 6, cs)               # Adam G, step counter, G mirror
-            self._tick(7, cs)
+            self._seg(ex, i + 1, cs)           # Adam G (the rest), step counter, G mirror
+            self._tick(i + 2, cs)
             return
         self._tick(0, cs)
         self._seg(ex, 0, cs)                   # fwd, g_loss chain through D(fake), G backward -> grad_g final

@@ -67,7 +67,7 @@ def _worker(rank, world, port, graph, out_dir, schedule="concurrent"):
                                             (False, "ddp")])
 def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
     """The DDP schedules over two ranks: "concurrent" (D chain and G chain on separate streams,
-    7 graph segments, collectives issued from both chains), "serial" (DCGAN_SERIAL_DBWD=1) and
+    8 graph segments, collectives issued from both chains), "serial" (DCGAN_SERIAL_DBWD=1) and
     "ddp" (the one-graph RCCL schedule with per-layer G buckets, run eagerly under gloo)."""
     ctx = mp.get_context("spawn")
     port = _free_port()
@@ -223,8 +223,8 @@ def test_timed_concurrent_schedule_matches_fused():
     d1, g1, _ = _run(b)
     assert torch.equal(d0, d1) and torch.equal(g0, g1)
     pt = b.phase_times()
-    assert set(pt) == {"fwd@end", "D_bwd_top@end", "G_chain@end", "D_bwd_rest@end", "G_tail@end", "adam_G@end",
-                       "adam_D@end"}
+    assert set(pt) == {"fwd@end", "D_bwd_top@end", "G_chain@end", "D_bwd_rest@end", "G_tail@end", "adam_G_a@end",
+                       "adam_G@end", "adam_D@end"}
     assert all(v > 0 for v in pt.values())
 
 
@@ -295,7 +295,7 @@ def _rccl_worker(out_dir, graph, port, schedule):
 def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule):
     """The REAL collective path on a one-GPU box: a one-rank RCCL (backend "nccl") process group
     (DCGAN_FORCE_DDP=1). "ddp": the RCCL all-reduces captured INSIDE the step's single hipGraph
-    (per-layer G buckets); "concurrent": issued on the comm stream between 7 graph segments.
+    (per-layer G buckets); "concurrent": issued on the comm stream between 8 graph segments.
     Both bit-identical to the fused single-graph step."""
     ctx = mp.get_context("spawn")
     p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port(), schedule))
@@ -305,7 +305,7 @@ def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule):
     r = torch.load(tmp_path / "rccl.pt", weights_only=True)
     assert r["backend"] == "nccl" and r["world"] == 1 and r["step"] == STEPS and r["graph"] == graph
     if graph:
-        assert r["graphs"] == (1 if schedule == "ddp" else 7)
+        assert r["graphs"] == (1 if schedule == "ddp" else 8)
     eng = _make(1, 0, True)
     assert not eng.ddp and eng._schedule() == "fused"
     d, g, _ = _run(eng)
@@ -328,7 +328,7 @@ def test_bench_force_ddp_reports_rccl():
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["backend"] == "nccl" and res["config"]["world_size"] == 1
     assert res["config"]["collectives"] == "torch.distributed(nccl)"
-    assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 7
+    assert res["config"]["schedule"] == "concurrent" and res["config"]["graphs_per_step"] == 8
     assert res["n_gpus"] == 1 and res["value"] > 0
 
 

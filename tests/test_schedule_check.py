@@ -99,6 +99,53 @@ def test_op_accesses_are_recorded():
     assert eng.kernel_count() == launches
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_adam_g_split_has_no_hazards(monkeypatch, split, wire):
+    """Segmented DDP step with Adam over g_h1's slice right after its collective (and the rest of
+    Adam(G) after the last one) -- and without the split: no unordered overlaps, any wire."""
+    monkeypatch.setenv("DCGAN_ADAM_G_SPLIT", split)
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False,
+                    allreduce_dtype=wire)
+    names = [n for n, _, _ in eng._segments()]
+    assert ("adam_G_a" in names) == (split == "1"), names
+    hz, n_ops = SC.check_engine(eng)
+    assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_adam_g_a_before_its_collective():
+    """Adam over g_h1's slice issued without waiting for that slice's collective: the checker
+    reports the race on the gradient slice."""
+    eng = _dry(world=2)
+    names = [n for n, _, _ in eng._segments()]
+    assert names.index("adam_G_a") == 5
+
+    def racy(ex):
+        cs, alt = ex.main(), ex.alt[0]
+        eng._seg(ex, 0, cs)
+        ex.wait(alt, cs)
+        eng._seg(ex, 1, alt)
+        eng._ar_launch(ex, "dtop", alt)
+        eng._seg(ex, 2, cs)
+        eng._ar_launch(ex, "gsplit_a", cs)
+        eng._seg(ex, 3, alt)
+        eng._seg(ex, 4, cs)
+        eng._seg(ex, 5, cs)                  # no wait for gsplit_a's collective
+        eng._ar_launch(ex, "drest", alt)
+        eng._ar_launch(ex, "gsplit_b", cs)
+        eng._ar_launch(ex, "gsplit_c", cs)
+        ex.wait(cs, alt)
+        eng._ar_join(ex, cs)
+        eng._seg(ex, 6, cs)
+        eng._seg(ex, 7, cs)
+
+    eng._run_step = racy
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed Adam(g_h1) racing its all-reduce"
+
+
 def test_checker_finds_an_early_g_bucket():
     """One-graph DDP: issuing G's first bucket one weight-gradient piece too early (before the
     piece that finalises it) is a race between the collective and that wgrad."""
@@ -207,8 +254,8 @@ def test_checker_finds_an_early_g_bucket():
             eng._seg(ex, i, st)
         ex.wait(cs, alt)
         eng._ar_join(ex, cs)
-        eng._seg(ex, 5, cs)
-        eng._seg(ex, 6, cs)
+        for i in range(5, len(eng._segments())):
+            eng._seg(ex, i, cs)
 
     eng._run_step = early
     hz, _ = SC.check_engine(eng)
@@ -235,7 +282,7 @@ def test_bf16_wire_direct_path_is_used():
     # the collective no longer touches the fp32 gradient, only its bf16 image
     assert all(p != eng.grad_d.flat.data_ptr() for p, _, _ in eng._ar_drest.accesses())
     names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
-    assert "adam_d" in names and "adam_g" in names
+    assert "adam_d" in names and {"adam_g_a", "adam_g_b", "adam_g_c"} <= set(names)
 
 
 def test_wgrad_adam_ranges_tile_both_buffers(monkeypatch):
