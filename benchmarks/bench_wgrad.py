@@ -82,6 +82,16 @@ def main():
                 p = ext.Program()
                 p.wgrad3(name, G.data_ptr(), Hg, Wg, Mc, Dm.data_ptr(), Bn, Hd, Wd, Nc, pad, c3, sp, o.data_ptr(), 1.0, 0)
                 progs[(c3, sp)], outs[(c3, sp)] = p, o
+        for c5 in sorted(H.WGRAD5_CFGS):  # wgrad5.hip: halo rows, one kernel row of taps per workgroup
+            if not H.wgrad5_fits(c5, Mc, Hd, Wd):
+                continue
+            for sp in (1, 2, 4, 8, 16, 24, 32, 48, 64):
+                if sp > 1 and kt // sp < 4:
+                    continue
+                o = torch.empty(25, Mc, Nc, device=dev)
+                p = ext.Program()
+                p.wgrad3(name, G.data_ptr(), Hg, Wg, Mc, Dm.data_ptr(), Bn, Hd, Wd, Nc, pad, c5, sp, o.data_ptr(), 1.0, 0)
+                progs[(c5, sp)], outs[(c5, sp)] = p, o
         cands = list(progs)
         s = torch.cuda.current_stream()
         for c in cands:
@@ -110,6 +120,9 @@ def main():
         print("%-14s Mc=%4d Nc=%4d K=%7d  wgrad.hip %7.1f us | best %3d:%-2d %7.1f us %6.0f TF/s | bad %s | %s" %
               (name, Mc, Nc, K, old_t, bc, bsp, best_t, fl / best_t / 1e6, sorted(bad) or "-",
                " ".join("%d:%d:%.0f" % (c[0], c[1], t) for t, c in good[:6])), flush=True)
+        w5 = [r for r in good if r[1][0] >= 400]
+        if w5:
+            print("%-14s   wgrad5: %s" % (name, " ".join("%d:%d:%.1f" % (c[0], c[1], t) for t, c in w5[:8])), flush=True)
         table[H.wgrad3_key(Mc, Nc, Bn, Hd, Wd, Hg)] = "%d:%d" % (bc, bsp)
     if a.write:
         path = H.TUNED_PATH

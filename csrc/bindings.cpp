@@ -391,8 +391,17 @@ class Program {
   int wgrad3(std::string name, uintptr_t G, int Hg, int Wg, int Mc, uintptr_t Dm, int Bn, int Hd, int Wd, int Nc,
              int pad, int cfg, int splits, uintptr_t dst, float scale, int stream,
              std::tuple<uintptr_t, uintptr_t, uintptr_t, uintptr_t, float, float, float, float> adam) {
-    int bm = 0, bn = 0, ns = 0;
-    if (KF(dcg_wgrad3_tile)(cfg, &bm, &bn, &ns)) throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
+    int bm = 0, bn = 0, ns = 0, w5_wd = 0;
+    const bool w5 = cfg >= 400;  // wgrad5.hip: one kernel row (5 taps) x all Mc x bn per workgroup
+    if (w5) {
+      if (KF(dcg_wgrad5_tile)(cfg, &bm, &bn, &w5_wd, &ns)) throw std::runtime_error("bad wgrad5 cfg " + std::to_string(cfg));
+      if (Mc != bm || Wd != w5_wd || Hd % (64 / w5_wd))
+        throw std::runtime_error("wgrad5 cfg " + std::to_string(cfg) + " does not fit Mc=" + std::to_string(Mc) +
+                                 " Hd=" + std::to_string(Hd) + " Wd=" + std::to_string(Wd));
+      if (std::get<0>(adam)) throw std::runtime_error("wgrad5: no fused Adam");
+    } else if (KF(dcg_wgrad3_tile)(cfg, &bm, &bn, &ns)) {
+      throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
+    }
     const int al = (int)(16 / es_);
     if (Mc % al || Nc % al) throw std::runtime_error("wgrad3 needs 16-byte channel rows (Mc, Nc multiples of 16 bytes)");
     if (splits < 1) throw std::runtime_error("splits must be >= 1");
@@ -420,15 +429,19 @@ class Program {
       a.alr = std::get<4>(adam); a.ab1 = std::get<5>(adam); a.ab2 = std::get<6>(adam); a.aeps = std::get<7>(adam);
       acc.w(std::get<0>(adam), nw * 4).w(std::get<1>(adam), nw * 4).w(std::get<2>(adam), nw * 4).r(std::get<3>(adam), 8);
     }
-    const int tt = KF(dcg_wgrad3_taps_per_tile)(cfg);
+    const int tt = w5 ? 1 : KF(dcg_wgrad3_taps_per_tile)(cfg);
     if (tt == 2 && 2 * Mc != bm) throw std::runtime_error("wgrad3: two-tap tiles need BM = 2 Mc");
-    const size_t tiles = (size_t)(tt == 2 ? 1 : (Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * ((25 + tt - 1) / tt);
+    // wgrad5: 5 * ceil(Nc / bn) tiles of 5 taps x Mc x bn; wgrad3: tap (group) x m x n tiles of bm x bn
+    const size_t tiles = w5 ? (size_t)5 * ((Nc + bn - 1) / bn)
+                            : (size_t)(tt == 2 ? 1 : (Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * ((25 + tt - 1) / tt);
+    const size_t slab = (size_t)(w5 ? 5 : 1) * bm * bn;
     if (splits > 1) {
-      if ((size_t)splits * bm * bn * 4 >= OOB) throw std::runtime_error("wgrad3: split slabs too large");
-      a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * (size_t)bm * bn * sizeof(float)));
+      if ((size_t)splits * slab * 4 >= OOB) throw std::runtime_error("wgrad3: split slabs too large");
+      a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * slab * sizeof(float)));
       a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
-      acc.w((uintptr_t)a.ws, tiles * splits * (size_t)bm * bn * 4).w((uintptr_t)a.counters, tiles * 4);
+      acc.w((uintptr_t)a.ws, tiles * splits * slab * 4).w((uintptr_t)a.counters, tiles * 4);
     }
+    if (w5) return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad5_launch)(&a, cfg, s); }, acc.v);
     return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad3_launch)(&a, cfg, s); }, acc.v);
   }
 

@@ -230,21 +230,32 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) tot[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < S; ++s) {
-      if (s == split) {
+    // several slabs' loads in flight per round trip (a round per slab left the small tiles' reduction
+    // latency-bound: one L2/HBM round trip per split at the kernel's tail); summed in split order
+    constexpr int U = FM * FN >= 16 ? 1 : 16 / (FM * FN);  // <= 16 loads in flight per thread
+    for (int s0 = 0; s0 < S; s0 += U) {
+      f32x4 v[U][FM][FN];
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) tot[i][j] += acc[i][j];
-      } else {
+      for (int u = 0; u < U; ++u) {
+        const int s = s0 + u;
         const uint32_t base = (uint32_t)s * (BM * BN * 4);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            tot[i][j] += __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (uint32_t)(((i * FN + j) * 256 + tid) * 16), 0, 16));
+            v[u][i][j] = (s < S && s != split)
+                             ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             rw, base + (uint32_t)(((i * FN + j) * 256 + tid) * 16), 0, 16))
+                             : acc[i][j];
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (s0 + u < S) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) tot[i][j] += v[u][i][j];
+        }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)

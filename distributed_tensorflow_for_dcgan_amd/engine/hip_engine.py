@@ -842,7 +842,7 @@ class HipEngine:
             plan = H.wgrad3_cfg_for(Mc, Nc, Bn, Hd, Wd, Hg)
             if plan is not None:
                 adam = (0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0)
-                if self._wgrad_adam and adam_of is not None:
+                if self._wgrad_adam and adam_of is not None and plan[0] < 400:  # (wgrad5: no fused Adam)
                     which, tname = adam_of
                     ps, opt = (self.model.g, self.opt_g) if which == "g" else (self.model.d, self.opt_d)
                     off, shape = ps.offsets[tname]

@@ -311,6 +311,41 @@ def test_wgrad_conv_and_deconv():
     close(outd.reshape(5, 5, Co, Ci), gwd, 2e-3, "deconv wgrad")
 
 
+@pytest.mark.parametrize("cfg,B,Hs,Ci,Co", [(400, 4, 32, 64, 128), (401, 3, 32, 64, 64), (402, 4, 16, 64, 64),
+                                            (403, 2, 64, 64, 64), (404, 2, 16, 128, 128), (405, 2, 32, 128, 64),
+                                            (406, 2, 16, 128, 80), (407, 2, 32, 128, 32)])
+def test_wgrad5_halo_rows_conv_and_deconv(cfg, B, Hs, Ci, Co):
+    """wgrad5.hip (a kernel row of 5 taps per workgroup, the input rows staged once as a window)
+    vs autograd: every configuration, split-K 1/3/5 (uneven and empty-tail splits), a partial last
+    channel block (Nc = 80 over 32-wide blocks), conv and deconv operand roles; a second launch of
+    the recorded op gives the same bits (split counters re-armed)."""
+    h = H()
+    Ho = Hs // 2
+    pad = (max((Ho - 1) * 2 + 5 - Hs, 0)) // 2
+    x = bf(rnd(B, Hs, Hs, Ci, seed=180))
+    w = rnd(5, 5, Ci, Co, scale=0.05, seed=181).requires_grad_(True)
+    dy = bf(rnd(B, Ho, Ho, Co, seed=182))
+    (gw,) = torch.autograd.grad(R.conv2d_same(x.float(), w), w, dy.float())
+    for sp in (1, 3, 5):
+        out = h.conv_wgrad3(x, dy, pad, cfg=cfg, splits=sp, scale=0.5)
+        close(out.reshape(5, 5, Ci, Co), 0.5 * gw, 2e-3, "conv wgrad5 cfg%d sp%d" % (cfg, sp))
+    if Co == Ci:  # deconv roles: G-operand = dY (Co = Mc channels, gathered), Dm = X
+        Xd = bf(rnd(B, Ho, Ho, Ci, seed=183))
+        wd = rnd(5, 5, Co, Ci, scale=0.05, seed=184).requires_grad_(True)
+        yd = R.conv2d_transpose_same(Xd.float(), wd, (Hs, Hs))
+        dyd = bf(rnd(B, Hs, Hs, Co, seed=185))
+        (gwd,) = torch.autograd.grad(yd, wd, dyd.float())
+        outd = h.conv_wgrad3(dyd, Xd, pad, cfg=cfg, splits=4)
+        close(outd.reshape(5, 5, Co, Ci), gwd, 2e-3, "deconv wgrad5 cfg%d" % cfg)
+    prog = h.ext().Program()
+    o = torch.empty(25, Ci, Co, device=dev)
+    prog.wgrad3("w5", h._p(x), Hs, Hs, Ci, h._p(dy), B, Ho, Ho, Co, pad, cfg, 3, h._p(o), 1.0, 0)
+    h.run(prog)
+    first = o.clone()
+    h.run(prog)
+    assert torch.equal(first, o)
+
+
 @pytest.mark.parametrize("B,Hs,Ci,Co", [(4, 16, 64, 128), (2, 8, 128, 256), (3, 7, 64, 64), (2, 14, 256, 128)])
 def test_wgrad3_conv_and_deconv_all_tiles(B, Hs, Ci, Co):
     """wgrad3.hip (LDS-DMA pipeline, in-kernel split-K) vs autograd: every tile x LDS-stage

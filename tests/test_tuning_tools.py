@@ -28,9 +28,23 @@ def test_shipped_table_entries_are_legal():
     for key, val in table.items():
         cfg, sp = (int(x) for x in val.split(":"))
         assert sp >= 1, key
-        if key.startswith("w3,"):
+        if key.startswith("w3,") and cfg >= 400:
+            Mc, Hd, Wd = (int(v) for v in (key.split(",")[1], key.split(",")[4], key.split(",")[5]))
+            assert H.wgrad5_fits(cfg, Mc, Hd, Wd), (key, val)
+        elif key.startswith("w3,"):
             assert 300 <= cfg < 340 and cfg % 10 in H.WGRAD3_TILES, (key, val)
         elif cfg >= 200:
             assert cfg < 240 and cfg % 10 in H.IGEMM3_TILES and H.igemm3_lds(cfg) <= 160 * 1024, (key, val)
         else:
             assert cfg % 100 in H.IGEMM_CFGS and sp == 1, (key, val)
+
+
+def test_tuner_offers_fitting_wgrad5_configs():
+    """The in-situ tuner's weight-gradient neighbours include exactly the wgrad5 configurations
+    whose channel count and output width match the layer."""
+    T = pytest.importorskip("benchmarks.tune_insitu")
+    nb = T.neighbours("w3,64,128,128,16,16,32", (311, 16))
+    assert {(400, 16), (401, 16)} <= set(nb)
+    assert not any(c in (402, 403, 404, 405, 406, 407) for c, _ in nb)
+    nb = T.neighbours("w3,128,256,256,8,8,16", (310, 4))
+    assert {(404, 4), (406, 4)} <= set(nb) and not any(c in (400, 401, 405) for c, _ in nb)
