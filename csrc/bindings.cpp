@@ -438,8 +438,11 @@ class Program {
     if (splits > 1) {
       if ((size_t)splits * slab * 4 >= OOB) throw std::runtime_error("wgrad3: split slabs too large");
       a.ws = reinterpret_cast<float*>(dev_alloc(tiles * splits * slab * sizeof(float)));
-      a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
-      acc.w((uintptr_t)a.ws, tiles * splits * slab * 4).w((uintptr_t)a.counters, tiles * 4);
+      acc.w((uintptr_t)a.ws, tiles * splits * slab * 4);
+      if (!(w5 && cfg >= 410)) {  // wgrad5 cfg 41x: the split sum is a second kernel, no counters
+        a.counters = reinterpret_cast<unsigned*>(dev_alloc(tiles * sizeof(unsigned), nullptr, true));
+        acc.w((uintptr_t)a.counters, tiles * 4);
+      }
     }
     if (w5) return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad5_launch)(&a, cfg, s); }, acc.v);
     return add(name, stream, [this, a, cfg](hipStream_t s) { return KF(dcg_wgrad3_launch)(&a, cfg, s); }, acc.v);

@@ -201,6 +201,19 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
   // ---- split-K hand-off (as wgrad3.hip): sc1 slab stores, drain, agent-scope counter; the last
   //      arrival sums the S slabs in split order and re-arms the counter
   constexpr int NF = 5 * FM * FN;
+  if (S > 1 && p.counters == nullptr) {
+    // separate reduction (cfg 41x): store this split's slab (accumulator-register order, one 4 KiB
+    // block per fragment) and leave the sum to wgrad5_reduce_kernel, which spreads it over the GPU
+    float* wsl = p.ws + ((size_t)tile_id * S + split) * (5 * MC * BN);
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          *reinterpret_cast<f32x4*>(wsl + (size_t)(((x * FM + i) * FN + j) * 256 + tid) * 4) = acc[x][i][j];
+    return;
+  }
   if (S > 1) {
     int& last_flag = *reinterpret_cast<int*>(lds);
     const __amdgpu_buffer_rsrc_t rw =
@@ -278,16 +291,48 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
       }
 }
 
+// the split sum of the separate-reduction variant: one thread per f32x4 of one tile's slab (the same
+// thread -> (m, n) map as the producing kernel), splits added in order (8 loads in flight)
+template <int MC, int BN>
+__global__ __launch_bounds__(256) void wgrad5_reduce_kernel(const float* __restrict__ ws, int S, int Nc, float scale,
+                                                            float* __restrict__ out) {
+  constexpr int TM = MC / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16, NF = 5 * FM * FN;
+  const int tile_id = blockIdx.x / NF, f = blockIdx.x - tile_id * NF, tid = threadIdx.x;
+  const int x = f / (FM * FN), i = (f / FN) % FM, j = f % FN;
+  const int ky = tile_id % 5, n0 = (tile_id / 5) * BN;
+  const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1, g4 = lane >> 4, li = lane & 15;
+  const float* src = ws + (size_t)tile_id * S * (5 * MC * BN) + (size_t)(f * 256 + tid) * 4;
+  f32x4 tot = (f32x4){0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 8;
+  for (int s0 = 0; s0 < S; s0 += U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = s0 + u < S ? *reinterpret_cast<const f32x4*>(src + (size_t)(s0 + u) * (5 * MC * BN)) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (s0 + u < S) tot += v[u];
+  }
+  const int n = n0 + wn * TN + j * 16 + li;
+  if (n < Nc) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = wm * TM + i * 16 + g4 * 4 + r;
+      out[((size_t)(ky * 5 + x) * MC + m) * Nc + n] = tot[r] * scale;
+    }
+  }
+}
+
 }  // namespace dcg
 
-// cfg 400 + id: (Mc, BN, Wd, NS)
+// cfg 400 + id: (Mc, BN, Wd, NS); 410 + id: the same with the split sum in a second, GPU-wide kernel
 #define DCG_WGRAD5_CFGS(X) \
   X(0, 64, 64, 16, 2) X(1, 64, 64, 16, 3) X(2, 64, 64, 8, 2) X(3, 64, 64, 32, 2) X(4, 128, 64, 8, 2) \
   X(5, 128, 64, 16, 2) X(6, 128, 32, 8, 2) X(7, 128, 32, 16, 2)
 
 extern "C" int DCG_API(dcg_wgrad5_tile)(int cfg, int* mc, int* bn, int* wd, int* ns) {
-  if (cfg < 400 || cfg >= 408) return -1;
-  const int id = cfg - 400;
+  if (cfg < 400 || cfg >= 418 || cfg % 10 >= 8) return -1;
+  const int id = cfg % 10;
 #define X(id_, MC_, BN_, WD_, NS_) if (id == id_) { *mc = MC_; *bn = BN_; *wd = WD_; *ns = NS_; return 0; }
   DCG_WGRAD5_CFGS(X)
 #undef X
@@ -309,14 +354,29 @@ static int w5launch(const dcg::WGrad3Args* a, unsigned blocks, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+template <int MC, int BN>
+static int w5reduce(const dcg::WGrad3Args* a, unsigned tiles, hipStream_t s) {
+  constexpr int NF = 5 * (MC / 32) * (BN / 32);  // f32x4 blocks of 256 threads per tile
+  auto k = dcg::wgrad5_reduce_kernel<MC, BN>;
+  hipLaunchKernelGGL(k, dim3(tiles * NF), dim3(256), 0, s, a->ws, a->splits, a->Nc, a->scale, a->out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int DCG_API(dcg_wgrad5_launch)(const dcg::WGrad3Args* a, int cfg, hipStream_t s) {
   int mc, bn, wd, ns;
   if (DCG_API(dcg_wgrad5_tile)(cfg, &mc, &bn, &wd, &ns)) return -1;
   // shapes the kernel assumes (the host binding checks them too)
   if (a->Mc != mc || a->Wd != wd || a->Hd % (64 / wd) || a->K != a->K / (a->Hd * a->Wd) * a->Hd * a->Wd) return -2;
-  const unsigned blocks = 5u * (unsigned)((a->Nc + bn - 1) / bn) * (unsigned)a->splits;
-  const int id = cfg - 400;
-#define X(id_, MC_, BN_, WD_, NS_) if (id == id_) return w5launch<MC_, BN_, WD_, NS_>(a, blocks, s);
+  const unsigned tiles = 5u * (unsigned)((a->Nc + bn - 1) / bn);
+  const unsigned blocks = tiles * (unsigned)a->splits;
+  const bool sep = cfg >= 410 && a->splits > 1;  // (the binding allocates no counters for 41x)
+  if ((cfg >= 410) != (a->counters == nullptr) && a->splits > 1) return -3;
+  const int id = cfg % 10;
+#define X(id_, MC_, BN_, WD_, NS_)                                 \
+  if (id == id_) {                                                 \
+    const int e = w5launch<MC_, BN_, WD_, NS_>(a, blocks, s);      \
+    return (e || !sep) ? e : w5reduce<MC_, BN_>(a, tiles, s);      \
+  }
   DCG_WGRAD5_CFGS(X)
 #undef X
   return -1;

@@ -278,6 +278,8 @@ WGRAD3_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64)}
 # kernel row (5 taps) x all Mc x BN channels, a k-tile is 64 / Wd whole output rows of one image
 WGRAD5_CFGS = {400: (64, 64, 16, 2), 401: (64, 64, 16, 3), 402: (64, 64, 8, 2), 403: (64, 64, 32, 2),
                404: (128, 64, 8, 2), 405: (128, 64, 16, 2), 406: (128, 32, 8, 2), 407: (128, 32, 16, 2)}
+# 410 + id: the same tiles with the split-K sum in a second, GPU-wide kernel (no last-arrival tail)
+WGRAD5_CFGS.update({c + 10: v for c, v in list(WGRAD5_CFGS.items())})
 
 
 def wgrad5_fits(cfg: int, Mc: int, Hd: int, Wd: int) -> bool:
