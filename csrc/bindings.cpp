@@ -395,7 +395,7 @@ class Program {
     const bool w5 = cfg >= 400;  // wgrad5.hip: one kernel row (5 taps) x all Mc x bn per workgroup
     if (w5) {
       if (KF(dcg_wgrad5_tile)(cfg, &bm, &bn, &w5_wd, &ns)) throw std::runtime_error("bad wgrad5 cfg " + std::to_string(cfg));
-      if (Mc != bm || Wd != w5_wd || Hd % (64 / w5_wd))
+      if (Mc % bm || Wd != w5_wd || Hd % (64 / w5_wd))
         throw std::runtime_error("wgrad5 cfg " + std::to_string(cfg) + " does not fit Mc=" + std::to_string(Mc) +
                                  " Hd=" + std::to_string(Hd) + " Wd=" + std::to_string(Wd));
       if (std::get<0>(adam)) throw std::runtime_error("wgrad5: no fused Adam");
@@ -432,7 +432,7 @@ class Program {
     const int tt = w5 ? 1 : KF(dcg_wgrad3_taps_per_tile)(cfg);
     if (tt == 2 && 2 * Mc != bm) throw std::runtime_error("wgrad3: two-tap tiles need BM = 2 Mc");
     // wgrad5: 5 * ceil(Nc / bn) tiles of 5 taps x Mc x bn; wgrad3: tap (group) x m x n tiles of bm x bn
-    const size_t tiles = w5 ? (size_t)5 * ((Nc + bn - 1) / bn)
+    const size_t tiles = w5 ? (size_t)5 * ((Nc + bn - 1) / bn) * (Mc / bm)
                             : (size_t)(tt == 2 ? 1 : (Mc + bm - 1) / bm) * ((Nc + bn - 1) / bn) * ((25 + tt - 1) / tt);
     const size_t slab = (size_t)(w5 ? 5 : 1) * bm * bn;
     if (splits > 1) {

@@ -6,7 +6,7 @@
 //
 // (reference ops: the conv2d / conv2d_transpose weight gradients of
 // /root/reference/distriubted_model.py:109-111,118, computed by TF's Conv2DBackpropFilter) -- but a
-// workgroup owns one kernel ROW ky (all five kx taps) of one (all Mc) x BN channel block, and a
+// workgroup owns one kernel ROW ky (all five kx taps) of one MC x BN channel block, and a
 // k-tile is R = 64 / Wd whole output rows of one image. For those 64 pixels the five taps read the
 // SAME R input rows 2y+ky-pl at columns 2x+kx-pl, so the A operand is staged once per k-tile as an
 // R x (2 Wd + 4)-pixel window (every tap's pixels inside it, stride 2) instead of five 64-pixel
@@ -74,8 +74,8 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
   // ---- tile decode: XCD remap, then (ky, n block) fastest and the k split slowest, so one XCD's
   //      run of workgroups shares its pixel range (its G rows and Dm tile) in that XCD's L2
   const int S = p.splits;
-  const int ntn = (p.Nc + BN - 1) / BN;
-  const int total = 5 * ntn * S;
+  const int ntn = (p.Nc + BN - 1) / BN, ntm = p.Mc / MC;  // MC = the tile's channel block (host: Mc % MC == 0)
+  const int total = 5 * ntn * ntm * S;
   int t = blockIdx.x;
   {
     const int q = total >> 3, rr = total & 7, xcd = t & 7;
@@ -84,9 +84,11 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
   const int ky = t % 5;
   int r_ = t / 5;
   const int nt = r_ % ntn;
-  const int split = r_ / ntn;
-  const int tile_id = nt * 5 + ky;
-  const int n0 = nt * BN;
+  r_ /= ntn;
+  const int mt = r_ % ntm;
+  const int split = r_ / ntm;
+  const int tile_id = (mt * ntn + nt) * 5 + ky;
+  const int n0 = nt * BN, m0 = mt * MC;
 
   const int KT = p.K / BK;                 // host: Hd % R == 0, so K is whole tiles of one image each
   const int kt0 = split * p.kt_per_split;
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
     const int c = jj < W2 / 2 ? 2 * jj : 2 * (jj - W2 / 2) + 1;  // its column: even ones first, then odd
     a_ry[i] = ry;
     a_ix[i] = c - p.pl;
-    a_m[i] = ((lane % CA) ^ (w5_swz<SA>(wp) >> 1)) * 8;
+    a_m[i] = m0 + ((lane % CA) ^ (w5_swz<SA>(wp) >> 1)) * 8;
     a_ok[i] = ry < R && c < 2 * WD + 3 && (unsigned)(c - p.pl) < (unsigned)p.Wg;
   }
   int b_row[PPW_B], b_n[PPW_B];
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
       const int iy = 2 * (y0 + a_ry[i]) + ky - p.pl;
       const bool ok = a_ok[i] && (unsigned)iy < (unsigned)p.Hg;
       dma16_asm_la(rg, sa + (wave + 4 * i) * 1024,
-                   oob_unless(ok, (uint32_t)(((b * p.Hg + iy) * p.Wg + a_ix[i]) * MC + a_m[i]) * 2u));
+                   oob_unless(ok, (uint32_t)(((b * p.Hg + iy) * p.Wg + a_ix[i]) * p.Mc + a_m[i]) * 2u));
     }
 #pragma unroll
     for (int i = 0; i < PPW_B; ++i) {
@@ -285,8 +287,8 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
         const int n = n0 + wn * TN + j * 16 + li;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = wm * TM + i * 16 + g4 * 4 + r;
-          if (n < p.Nc) p.out[((size_t)(ky * 5 + x) * MC + m) * p.Nc + n] = acc[x][i][j][r] * p.scale;
+          const int m = m0 + wm * TM + i * 16 + g4 * 4 + r;
+          if (n < p.Nc) p.out[((size_t)(ky * 5 + x) * p.Mc + m) * p.Nc + n] = acc[x][i][j][r] * p.scale;
         }
       }
 }
@@ -294,12 +296,13 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
 // the split sum of the separate-reduction variant: one thread per f32x4 of one tile's slab (the same
 // thread -> (m, n) map as the producing kernel), splits added in order (8 loads in flight)
 template <int MC, int BN>
-__global__ __launch_bounds__(256) void wgrad5_reduce_kernel(const float* __restrict__ ws, int S, int Nc, float scale,
-                                                            float* __restrict__ out) {
+__global__ __launch_bounds__(256) void wgrad5_reduce_kernel(const float* __restrict__ ws, int S, int Mc, int Nc,
+                                                            float scale, float* __restrict__ out) {
   constexpr int TM = MC / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16, NF = 5 * FM * FN;
   const int tile_id = blockIdx.x / NF, f = blockIdx.x - tile_id * NF, tid = threadIdx.x;
   const int x = f / (FM * FN), i = (f / FN) % FM, j = f % FN;
-  const int ky = tile_id % 5, n0 = (tile_id / 5) * BN;
+  const int ntn = (Nc + BN - 1) / BN, ky = tile_id % 5, nt = (tile_id / 5) % ntn, mt = tile_id / 5 / ntn;
+  const int n0 = nt * BN, m0 = mt * MC;
   const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1, g4 = lane >> 4, li = lane & 15;
   const float* src = ws + (size_t)tile_id * S * (5 * MC * BN) + (size_t)(f * 256 + tid) * 4;
   f32x4 tot = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -317,21 +320,22 @@ __global__ __launch_bounds__(256) void wgrad5_reduce_kernel(const float* __restr
   if (n < Nc) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = wm * TM + i * 16 + g4 * 4 + r;
-      out[((size_t)(ky * 5 + x) * MC + m) * Nc + n] = tot[r] * scale;
+      const int m = m0 + wm * TM + i * 16 + g4 * 4 + r;
+      out[((size_t)(ky * 5 + x) * Mc + m) * Nc + n] = tot[r] * scale;
     }
   }
 }
 
 }  // namespace dcg
 
-// cfg 400 + id: (Mc, BN, Wd, NS); 410 + id: the same with the split sum in a second, GPU-wide kernel
+// cfg 400 + id: (MC channel block, BN, Wd, NS); 410 + id: the same with the split sum in a second,
+// GPU-wide kernel
 #define DCG_WGRAD5_CFGS(X) \
   X(0, 64, 64, 16, 2) X(1, 64, 64, 16, 3) X(2, 64, 64, 8, 2) X(3, 64, 64, 32, 2) X(4, 128, 64, 8, 2) \
-  X(5, 128, 64, 16, 2) X(6, 128, 32, 8, 2) X(7, 128, 32, 16, 2)
+  X(5, 128, 64, 16, 2) X(6, 128, 32, 8, 2) X(7, 128, 32, 16, 2) X(8, 64, 64, 64, 2)
 
 extern "C" int DCG_API(dcg_wgrad5_tile)(int cfg, int* mc, int* bn, int* wd, int* ns) {
-  if (cfg < 400 || cfg >= 418 || cfg % 10 >= 8) return -1;
+  if (cfg < 400 || cfg >= 419 || cfg % 10 >= 9) return -1;
   const int id = cfg % 10;
 #define X(id_, MC_, BN_, WD_, NS_) if (id == id_) { *mc = MC_; *bn = BN_; *wd = WD_; *ns = NS_; return 0; }
   DCG_WGRAD5_CFGS(X)
@@ -358,7 +362,7 @@ template <int MC, int BN>
 static int w5reduce(const dcg::WGrad3Args* a, unsigned tiles, hipStream_t s) {
   constexpr int NF = 5 * (MC / 32) * (BN / 32);  // f32x4 blocks of 256 threads per tile
   auto k = dcg::wgrad5_reduce_kernel<MC, BN>;
-  hipLaunchKernelGGL(k, dim3(tiles * NF), dim3(256), 0, s, a->ws, a->splits, a->Nc, a->scale, a->out);
+  hipLaunchKernelGGL(k, dim3(tiles * NF), dim3(256), 0, s, a->ws, a->splits, a->Mc, a->Nc, a->scale, a->out);
   return (int)hipGetLastError();
 }
 
@@ -366,8 +370,8 @@ extern "C" int DCG_API(dcg_wgrad5_launch)(const dcg::WGrad3Args* a, int cfg, hip
   int mc, bn, wd, ns;
   if (DCG_API(dcg_wgrad5_tile)(cfg, &mc, &bn, &wd, &ns)) return -1;
   // shapes the kernel assumes (the host binding checks them too)
-  if (a->Mc != mc || a->Wd != wd || a->Hd % (64 / wd) || a->K != a->K / (a->Hd * a->Wd) * a->Hd * a->Wd) return -2;
-  const unsigned tiles = 5u * (unsigned)((a->Nc + bn - 1) / bn);
+  if (a->Mc % mc || a->Wd != wd || a->Hd % (64 / wd) || a->K != a->K / (a->Hd * a->Wd) * a->Hd * a->Wd) return -2;
+  const unsigned tiles = 5u * (unsigned)((a->Nc + bn - 1) / bn) * (unsigned)(a->Mc / mc);
   const unsigned blocks = tiles * (unsigned)a->splits;
   const bool sep = cfg >= 410 && a->splits > 1;  // (the binding allocates no counters for 41x)
   if ((cfg >= 410) != (a->counters == nullptr) && a->splits > 1) return -3;

@@ -277,15 +277,17 @@ WGRAD3_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64)}
 # wgrad5.hip (csrc/hip/wgrad5.hip, cfg 400 + id): (Mc, BN, Wd, LDS stages) -- a workgroup owns one
 # kernel row (5 taps) x all Mc x BN channels, a k-tile is 64 / Wd whole output rows of one image
 WGRAD5_CFGS = {400: (64, 64, 16, 2), 401: (64, 64, 16, 3), 402: (64, 64, 8, 2), 403: (64, 64, 32, 2),
-               404: (128, 64, 8, 2), 405: (128, 64, 16, 2), 406: (128, 32, 8, 2), 407: (128, 32, 16, 2)}
+               404: (128, 64, 8, 2), 405: (128, 64, 16, 2), 406: (128, 32, 8, 2), 407: (128, 32, 16, 2),
+               408: (64, 64, 64, 2)}
 # 410 + id: the same tiles with the split-K sum in a second, GPU-wide kernel (no last-arrival tail)
 WGRAD5_CFGS.update({c + 10: v for c, v in list(WGRAD5_CFGS.items())})
 
 
 def wgrad5_fits(cfg: int, Mc: int, Hd: int, Wd: int) -> bool:
-    """wgrad5 cfg usable for a layer: its channel count and output width, whole rows per k-tile."""
+    """wgrad5 cfg usable for a layer: whole channel blocks, its output width, whole output rows of
+    one image per 64-pixel k-tile."""
     ent = WGRAD5_CFGS.get(cfg)
-    return ent is not None and ent[0] == Mc and ent[2] == Wd and Hd % (64 // Wd) == 0
+    return ent is not None and Mc % ent[0] == 0 and ent[2] == Wd and Hd % (64 // Wd) == 0
 
 
 def pick_wgrad3(Mc: int, Nc: int, K: int, target_blocks: int = 2 * CU_COUNT) -> Optional[Tuple[int, int]]:
