@@ -83,7 +83,7 @@ def main():
                 p.wgrad3(name, G.data_ptr(), Hg, Wg, Mc, Dm.data_ptr(), Bn, Hd, Wd, Nc, pad, c3, sp, o.data_ptr(), 1.0, 0)
                 progs[(c3, sp)], outs[(c3, sp)] = p, o
         for c5 in sorted(H.WGRAD5_CFGS):  # wgrad5.hip: halo rows, one kernel row of taps per workgroup
-            if not H.wgrad5_fits(c5, Mc, Hd, Wd):
+            if not H.wgrad5_fits(c5, Mc, Hd, Wd, Bn):
                 continue
             for sp in (1, 2, 4, 8, 16, 24, 32, 48, 64):
                 if sp > 1 and kt // sp < 4:

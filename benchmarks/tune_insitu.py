@@ -104,14 +104,14 @@ def neighbours(key, cur, tiles=False, extra_tiles=(), extra_cfgs=()):
             out.append((cfg, s2))
     if key.startswith("w3,"):
         f = key.split(",")  # w3,Mc,Nc,Bn,Hd,Wd,Hg
-        Mc, Hd, Wd = int(f[1]), int(f[4]), int(f[5])
+        Mc, Bn, Hd, Wd = int(f[1]), int(f[3]), int(f[4]), int(f[5])
         fam = [300, 301, 302, 303, 310, 311, 312, 313] + ([320, 322, 330, 332] if Mc == 64 else [])
         if not tiles:
             fam = {310: (311, 313), 311: (310, 313), 313: (311, 312), 312: (313, 311)}.get(cfg, ())
             if 300 <= cfg < 320:  # the same tile with the other LDS stage count (NS 3 <-> 2)
                 fam = tuple(fam) + (cfg + 10 if cfg < 310 else cfg - 10,)
         # wgrad5 (halo rows) configurations that fit the layer
-        fam = tuple(fam) + tuple(c for c in H.WGRAD5_CFGS if H.wgrad5_fits(c, Mc, Hd, Wd))
+        fam = tuple(fam) + tuple(c for c in H.WGRAD5_CFGS if H.wgrad5_fits(c, Mc, Hd, Wd, Bn))
         out += [(c, sp) for c in fam]
     elif cfg >= 200:
         ns = (cfg - 200) // 10

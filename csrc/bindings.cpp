@@ -395,7 +395,7 @@ class Program {
     const bool w5 = cfg >= 400;  // wgrad5.hip: one kernel row (5 taps) x all Mc x bn per workgroup
     if (w5) {
       if (KF(dcg_wgrad5_tile)(cfg, &bm, &bn, &w5_wd, &ns)) throw std::runtime_error("bad wgrad5 cfg " + std::to_string(cfg));
-      if (Mc % bm || Wd != w5_wd || Hd % (64 / w5_wd))
+      if (Mc % bm || Wd != w5_wd || (Hd % (64 / w5_wd) && (64 / w5_wd) % Hd) || (Bn * Hd * Wd) % 64)
         throw std::runtime_error("wgrad5 cfg " + std::to_string(cfg) + " does not fit Mc=" + std::to_string(Mc) +
                                  " Hd=" + std::to_string(Hd) + " Wd=" + std::to_string(Wd));
       if (std::get<0>(adam)) throw std::runtime_error("wgrad5: no fused Adam");

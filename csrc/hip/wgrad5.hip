@@ -90,10 +90,9 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
   const int tile_id = (mt * ntn + nt) * 5 + ky;
   const int n0 = nt * BN, m0 = mt * MC;
 
-  const int KT = p.K / BK;                 // host: Hd % R == 0, so K is whole tiles of one image each
+  const int KT = p.K / BK;                 // host: whole output rows per k-tile, K a multiple of 64
   const int kt0 = split * p.kt_per_split;
   const int nk = max(0, min(KT, kt0 + p.kt_per_split) - kt0);
-  const int tiles_per_img = p.Hd / R;
 
   const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.G, p.g_bytes);
   const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.Dm, p.d_bytes);
@@ -123,10 +122,12 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
   auto issue = [&](int slot) {
     const uint32_t sa = lds_base + slot * STAGE;
     const uint32_t sb = sa + A_BYTES;
-    const int b = cur_kt / tiles_per_img, y0 = (cur_kt - b * tiles_per_img) * R;
 #pragma unroll
     for (int i = 0; i < PPW_A; ++i) {
-      const int iy = 2 * (y0 + a_ry[i]) + ky - p.pl;
+      // output row gy of the whole batch (a k-tile may span several small images: Hd < R)
+      const uint32_t gy = (uint32_t)(cur_kt * R + a_ry[i]);
+      const int b = (int)fdiv(gy * (uint32_t)WD, p.fd_hw), y = (int)gy - b * p.Hd;
+      const int iy = 2 * y + ky - p.pl;
       const bool ok = a_ok[i] && (unsigned)iy < (unsigned)p.Hg;
       dma16_asm_la(rg, sa + (wave + 4 * i) * 1024,
                    oob_unless(ok, (uint32_t)(((b * p.Hg + iy) * p.Wg + a_ix[i]) * p.Mc + a_m[i]) * 2u));
@@ -332,10 +333,10 @@ __global__ __launch_bounds__(256) void wgrad5_reduce_kernel(const float* __restr
 // GPU-wide kernel
 #define DCG_WGRAD5_CFGS(X) \
   X(0, 64, 64, 16, 2) X(1, 64, 64, 16, 3) X(2, 64, 64, 8, 2) X(3, 64, 64, 32, 2) X(4, 128, 64, 8, 2) \
-  X(5, 128, 64, 16, 2) X(6, 128, 32, 8, 2) X(7, 128, 32, 16, 2) X(8, 64, 64, 64, 2)
+  X(5, 128, 64, 16, 2) X(6, 128, 32, 8, 2) X(7, 128, 32, 16, 2) X(8, 64, 64, 64, 2) X(9, 64, 64, 4, 2)
 
 extern "C" int DCG_API(dcg_wgrad5_tile)(int cfg, int* mc, int* bn, int* wd, int* ns) {
-  if (cfg < 400 || cfg >= 419 || cfg % 10 >= 9) return -1;
+  if (cfg < 400 || cfg >= 420) return -1;
   const int id = cfg % 10;
 #define X(id_, MC_, BN_, WD_, NS_) if (id == id_) { *mc = MC_; *bn = BN_; *wd = WD_; *ns = NS_; return 0; }
   DCG_WGRAD5_CFGS(X)
@@ -370,7 +371,8 @@ extern "C" int DCG_API(dcg_wgrad5_launch)(const dcg::WGrad3Args* a, int cfg, hip
   int mc, bn, wd, ns;
   if (DCG_API(dcg_wgrad5_tile)(cfg, &mc, &bn, &wd, &ns)) return -1;
   // shapes the kernel assumes (the host binding checks them too)
-  if (a->Mc % mc || a->Wd != wd || a->Hd % (64 / wd) || a->K != a->K / (a->Hd * a->Wd) * a->Hd * a->Wd) return -2;
+  const int R = 64 / wd;  // output rows per k-tile: whole images or whole-image fractions, K in whole tiles
+  if (a->Mc % mc || a->Wd != wd || (a->Hd % R && R % a->Hd) || a->K % 64) return -2;
   const unsigned tiles = 5u * (unsigned)((a->Nc + bn - 1) / bn) * (unsigned)(a->Mc / mc);
   const unsigned blocks = tiles * (unsigned)a->splits;
   const bool sep = cfg >= 410 && a->splits > 1;  // (the binding allocates no counters for 41x)

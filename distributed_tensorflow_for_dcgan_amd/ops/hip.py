@@ -278,16 +278,19 @@ WGRAD3_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (64, 64)}
 # kernel row (5 taps) x all Mc x BN channels, a k-tile is 64 / Wd whole output rows of one image
 WGRAD5_CFGS = {400: (64, 64, 16, 2), 401: (64, 64, 16, 3), 402: (64, 64, 8, 2), 403: (64, 64, 32, 2),
                404: (128, 64, 8, 2), 405: (128, 64, 16, 2), 406: (128, 32, 8, 2), 407: (128, 32, 16, 2),
-               408: (64, 64, 64, 2)}
+               408: (64, 64, 64, 2), 409: (64, 64, 4, 2)}
 # 410 + id: the same tiles with the split-K sum in a second, GPU-wide kernel (no last-arrival tail)
 WGRAD5_CFGS.update({c + 10: v for c, v in list(WGRAD5_CFGS.items())})
 
 
-def wgrad5_fits(cfg: int, Mc: int, Hd: int, Wd: int) -> bool:
-    """wgrad5 cfg usable for a layer: whole channel blocks, its output width, whole output rows of
-    one image per 64-pixel k-tile."""
+def wgrad5_fits(cfg: int, Mc: int, Hd: int, Wd: int, Bn: int = 64) -> bool:
+    """wgrad5 cfg usable for a layer: whole channel blocks, its output width, whole output rows
+    per 64-pixel k-tile (a fraction of one image or whole images), whole k-tiles."""
     ent = WGRAD5_CFGS.get(cfg)
-    return ent is not None and Mc % ent[0] == 0 and ent[2] == Wd and Hd % (64 // Wd) == 0
+    if ent is None or Mc % ent[0] or ent[2] != Wd:
+        return False
+    R = 64 // Wd
+    return (Hd % R == 0 or R % Hd == 0) and (Bn * Hd * Wd) % 64 == 0
 
 
 def pick_wgrad3(Mc: int, Nc: int, K: int, target_blocks: int = 2 * CU_COUNT) -> Optional[Tuple[int, int]]:

@@ -315,7 +315,8 @@ def test_wgrad_conv_and_deconv():
                                             (403, 2, 64, 64, 64), (404, 2, 16, 128, 128), (405, 2, 32, 128, 64),
                                             (406, 2, 16, 128, 80), (407, 2, 32, 128, 32), (410, 4, 32, 64, 128),
                                             (414, 2, 16, 128, 128), (416, 2, 16, 128, 80),
-                                            (412, 2, 16, 128, 128), (410, 2, 32, 192, 64), (418, 2, 128, 64, 64)])
+                                            (412, 2, 16, 128, 128), (410, 2, 32, 192, 64), (418, 2, 128, 64, 64),
+                                            (419, 8, 8, 256, 128), (409, 4, 8, 64, 64)])
 def test_wgrad5_halo_rows_conv_and_deconv(cfg, B, Hs, Ci, Co):
     """wgrad5.hip (a kernel row of 5 taps per workgroup, the input rows staged once as a window)
     vs autograd: every configuration, split-K 1/3/5 (uneven and empty-tail splits), a partial last

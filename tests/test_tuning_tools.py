@@ -29,8 +29,8 @@ def test_shipped_table_entries_are_legal():
         cfg, sp = (int(x) for x in val.split(":"))
         assert sp >= 1, key
         if key.startswith("w3,") and cfg >= 400:
-            Mc, Hd, Wd = (int(v) for v in (key.split(",")[1], key.split(",")[4], key.split(",")[5]))
-            assert H.wgrad5_fits(cfg, Mc, Hd, Wd), (key, val)
+            f = key.split(",")
+            assert H.wgrad5_fits(cfg, int(f[1]), int(f[4]), int(f[5]), int(f[3])), (key, val)
         elif key.startswith("w3,"):
             assert 300 <= cfg < 340 and cfg % 10 in H.WGRAD3_TILES, (key, val)
         elif cfg >= 200:
