@@ -357,7 +357,10 @@ class HipEngine:
         second part."""
         self.progC = self._prog()
         sch = self._schedule()
-        if sch == "fused" and self.dt == 0:
+        self._adam_early = sch == "fused" and self.dt == 0 and self._adam_d_early()
+        if self._adam_early:
+            self._build_update_d_first(self.progC)  # Adam(D) on the D chain's stream, Adam(G) after the join
+        elif sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
             self._c_split = self._c_split_a = self.progC.size()
         elif sch in ("concurrent", "ddp") and not self.f16:
@@ -949,6 +952,7 @@ class HipEngine:
                     self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw,
                                 L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
         # ---------------- G backward (reads no D state)
+        self._a_gd_end = prog.size()  # the g_loss chain is done with D's weights / BN parameters
         n = len(self.gl)
         Lg = self.gl[-1]
         if not self._img_dact():  # (else fused into the image-gradient kernel above)
@@ -1279,12 +1283,25 @@ class HipEngine:
             ex.wait_mark(ex.alt[0], m)
             ex.run(self.progW, ex.alt, w, w_end)
             w = w_end
+        if self._adam_early:
+            # Adam(D) on the D chain's stream once the g_loss chain has left D (the first G-wgrad
+            # mark follows it), beside the G chain's tail; Adam(G) + the step counter after the join
+            assert self._g_w[0][0] >= self._a_gd_end
+            ex.wait_mark(ex.alt[0], marks[0])
+            ex.run(self.progC, ex.alt, 0, self._c_split)
         if n_main:
             # the last G weight gradients on cs after the G chain (their operands are produced
             # there): the D chain's stream no longer runs them serially after everything else
             ex.run(self.progW, [cs, ex.side], w, -1)
         ex.wait(cs, ex.alt[0])
-        ex.run(self.progC, [cs, ex.side])
+        ex.run(self.progC, [cs, ex.side], self._c_split if self._adam_early else 0, -1)
+
+    def _adam_d_early(self) -> bool:
+        """DCGAN_ADAM_D_EARLY=1 (fused single-process bf16 step, G weight gradients behind the D
+        chain): Adam(D) on the D chain's stream after that stream's last weight gradient, beside
+        the G chain's tail, instead of inside the one two-model Adam after the join."""
+        return (os.environ.get("DCGAN_ADAM_D_EARLY", "0") == "1" and self._sched_req in (None, "fused")
+                and not self.ddp and self._g_wgrad_on_d_stream() and not self._wgrad_adam_wanted())
 
     def _g_first(self) -> int:
         """DCGAN_G_FIRST=k: issue the G chain's first k ops before the D chain's (study switch)."""

@@ -487,3 +487,30 @@ def test_bn_fold_is_bit_identical_to_finalize_then_apply(monkeypatch, dtype, B):
     for a, b in pairs:
         assert torch.equal(a, b), (a.float() - b.float()).abs().max()
     assert e1.last_losses() == e2.last_losses()
+
+
+@pytest.mark.gpu
+def test_early_adam_d_is_bit_identical(monkeypatch):
+    """DCGAN_ADAM_D_EARLY=1 (Adam(D) on the D chain's stream beside the G chain's tail, Adam(G) +
+    step counter after the join) == the one two-model Adam after the join, bit for bit, 3 steps."""
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    dev = torch.device("cuda", 0)
+    cfg = DCGANConfig()
+    B = 32
+    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1).to(dev)
+    monkeypatch.setenv("DCGAN_ADAM_D_EARLY", "1")
+    e1 = HipEngine(cfg, B, dev, graph=False, seed=4)
+    monkeypatch.setenv("DCGAN_ADAM_D_EARLY", "0")
+    e2 = HipEngine(cfg, B, dev, graph=False, seed=4)
+    assert e1._adam_early and not e2._adam_early   # (decided when the update program is built)
+    e1.set_batch(real)
+    e2.set_batch(real)
+    for _ in range(3):
+        e1.train_step()
+        e2.train_step()
+    torch.cuda.synchronize()
+    for a, b in ((e1.model.g.flat, e2.model.g.flat), (e1.model.d.flat, e2.model.d.flat),
+                 (e1.wbf_d.flat, e2.wbf_d.flat), (e1.opt_d.m.flat, e2.opt_d.m.flat), (e1.opt_g.v.flat, e2.opt_g.v.flat),
+                 (e1.opt_g.powers, e2.opt_g.powers), (e1.opt_d.powers, e2.opt_d.powers)):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+    assert e1.last_losses() == e2.last_losses() and e1.global_step == e2.global_step == 3

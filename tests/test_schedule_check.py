@@ -195,6 +195,40 @@ def test_wgrad_adam_schedule_has_no_hazards(monkeypatch, wa):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
+def test_early_adam_d_has_no_hazards(monkeypatch):
+    """DCGAN_ADAM_D_EARLY=1: Adam(D) on the D chain's stream (after the g_loss chain has left D)
+    beside the G chain's tail -- no unordered overlap with the G chain's reads of D's weights."""
+    monkeypatch.setenv("DCGAN_ADAM_D_EARLY", "1")
+    eng = _dry()
+    assert eng._adam_early and eng._schedule() == "fused"
+    names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
+    assert names[:eng._c_split] == ["adam_d"]
+    hz, _ = SC.check_engine(eng)
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_adam_d_before_the_g_chain_left_d(monkeypatch):
+    """The same Adam(D) issued on the D chain's stream WITHOUT waiting for the g_loss chain to leave
+    D races the G chain's D data gradients (they read D's weights)."""
+    monkeypatch.setenv("DCGAN_ADAM_D_EARLY", "1")
+    eng = _dry()
+
+    def racy(ex):
+        cs, alt = ex.main(), ex.alt[0]
+        ex.run(eng.progA, [cs, ex.side], 0, eng._a_fwd)
+        ex.wait(alt, cs)
+        ex.run(eng.progB, ex.alt)
+        ex.run(eng.progC, ex.alt, 0, eng._c_split)    # Adam(D): no wait for the g_loss chain
+        ex.run(eng.progA, [cs, ex.side], eng._a_fwd, -1)
+        ex.run(eng.progW, [cs, ex.side])
+        ex.wait(cs, alt)
+        ex.run(eng.progC, [cs, ex.side], eng._c_split, -1)
+
+    eng._run_step = racy
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed Adam(D) racing the g_loss chain's reads of D"
+
+
 @pytest.mark.parametrize("fold", ["0", "64", "256"])
 def test_bn_fold_schedule_has_no_hazards(monkeypatch, fold):
     """BN finalize folded into the apply launches (DCGAN_BN_FOLD): same hazard-free step, one
