@@ -1299,7 +1299,8 @@ class HipEngine:
     def _adam_d_early(self) -> bool:
         """DCGAN_ADAM_D_EARLY=1 (fused single-process bf16 step, G weight gradients behind the D
         chain): Adam(D) on the D chain's stream after that stream's last weight gradient, beside
-        the G chain's tail, instead of inside the one two-model Adam after the join."""
+        the G chain's tail, instead of inside the one two-model Adam after the join. Bit-identical;
+        measured 0.1-1.0 % slower (4/4 pairs, profiles/r5/ab_adam_d_early_r5.txt), so off."""
         return (os.environ.get("DCGAN_ADAM_D_EARLY", "0") == "1" and self._sched_req in (None, "fused")
                 and not self.ddp and self._g_wgrad_on_d_stream() and not self._wgrad_adam_wanted())
 
