@@ -213,7 +213,7 @@ def test_bf16_wire_holds_the_50_step_envelope(tmp_path):
 
 
 def test_timed_concurrent_schedule_matches_fused():
-    """The per-phase timed step (7 concurrent graph segments incl. G_tail, the DDP schedule at W=1)
+    """The per-phase timed step (8 concurrent graph segments incl. G_tail and adam_G_a, the DDP schedule at W=1)
     is the same computation as the single fused graph, bit for bit; phase ends are reported."""
     a = _make(1, 0, True)
     b = _make(1, 0, True)
