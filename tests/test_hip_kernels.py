@@ -349,6 +349,22 @@ def test_wgrad5_halo_rows_conv_and_deconv(cfg, B, Hs, Ci, Co):
     assert torch.equal(first, o)
 
 
+@pytest.mark.parametrize("cfg,B,Hs,Ci,Co", [(410, 4, 32, 64, 128), (413, 2, 64, 64, 64), (418, 2, 128, 64, 64),
+                                            (412, 2, 16, 128, 128)])
+def test_wgrad5_fp16(cfg, B, Hs, Ci, Co):
+    """wgrad5.hip's fp16 build (the 256x256 fp16 step runs it) vs autograd, split-K 1 and 5."""
+    h = H()
+    Ho = Hs // 2
+    pad = (max((Ho - 1) * 2 + 5 - Hs, 0)) // 2
+    x = rnd(B, Hs, Hs, Ci, seed=190).to(torch.float16).contiguous()
+    w = rnd(5, 5, Ci, Co, scale=0.05, seed=191).requires_grad_(True)
+    dy = rnd(B, Ho, Ho, Co, seed=192).to(torch.float16).contiguous()
+    (gw,) = torch.autograd.grad(R.conv2d_same(x.float(), w), w, dy.float())
+    for sp in (1, 5):
+        out = h.conv_wgrad3(x, dy, pad, cfg=cfg, splits=sp)
+        close(out.reshape(5, 5, Ci, Co), gw, 2e-3, "fp16 conv wgrad5 cfg%d sp%d" % (cfg, sp))
+
+
 @pytest.mark.parametrize("B,Hs,Ci,Co", [(4, 16, 64, 128), (2, 8, 128, 256), (3, 7, 64, 64), (2, 14, 256, 128)])
 def test_wgrad3_conv_and_deconv_all_tiles(B, Hs, Ci, Co):
     """wgrad3.hip (LDS-DMA pipeline, in-kernel split-K) vs autograd: every tile x LDS-stage
