@@ -123,18 +123,34 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   const int ntn = (p.N + BN - 1) / BN;
   const int total = p.mtiles * ntn * p.nphases * S;
   int t = blockIdx.x;
-  {  // bijective XCD remap: workgroups b, b+8, b+16, ... (one XCD) get a contiguous run of t
-    const int q = total >> 3, rr = total & 7, xcd = t & 7;
-    t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+  int split, phase, nt, mt;
+  if (p.lpt && p.nphases > 1) {
+    // longest processing time first: the phases (host-sorted, most taps first) are dispatched one
+    // after the other, so the short phases fill in at the end; within a phase the same bijective
+    // XCD remap (the blocks of one XCD get a contiguous run of that phase's tiles)
+    const int T1 = p.mtiles * ntn * S;
+    phase = t / T1;
+    int u = t - phase * T1;
+    const int q = T1 >> 3, rr = T1 & 7, f = u & 7;
+    u = (f < rr ? f * (q + 1) : rr * (q + 1) + (f - rr) * q) + (u >> 3);
+    split = u % S;
+    const int r2 = u / S;
+    nt = r2 % ntn;
+    mt = r2 / ntn;
+  } else {
+    {  // bijective XCD remap: workgroups b, b+8, b+16, ... (one XCD) get a contiguous run of t
+      const int q = total >> 3, rr = total & 7, xcd = t & 7;
+      t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+    }
+    // split fastest (a tile's slabs on one XCD), then PHASE (deconv phases have 9/6/6/4 taps: a
+    // phase-slowest order would give whole XCDs the 9-tap phase), then n, then m
+    split = t % S;
+    int r_ = t / S;
+    phase = r_ % p.nphases;
+    r_ /= p.nphases;
+    nt = r_ % ntn;
+    mt = r_ / ntn;
   }
-  // split fastest (a tile's slabs on one XCD), then PHASE (deconv phases have 9/6/6/4 taps: a
-  // phase-slowest order would give whole XCDs the 9-tap phase), then n, then m
-  const int split = t % S;
-  int r_ = t / S;
-  const int phase = r_ % p.nphases;
-  r_ /= p.nphases;
-  const int nt = r_ % ntn;
-  const int mt = r_ / ntn;
   const int tile_id = (phase * p.mtiles + mt) * ntn + nt;
 
   const IGemmPhaseK& ph = p.phk[phase];  // kernarg segment: scalar loads

@@ -54,6 +54,9 @@ struct IGemmArgs {
   // activation-only backward (layer without BN): store g = dL/da * act'(y) instead of dL/da and
   // emit (sum g, 0) per channel -- the bias gradient partials. bnb_x aliases y, mean/rstd unused.
   int bnb_store_g;
+  // igemm3: longest phase first (mode 1: phases host-sorted by decreasing tap count, dispatched
+  // phase by phase, each phase's tiles XCD-contiguous) instead of the phases interleaved
+  int lpt;
 };
 
 
