@@ -1105,10 +1105,10 @@ class HipEngine:
 
     # ------------------------------------------------------------------ execution
     MAIN, ALT = 0, 1
-    # G's weight gradients behind the D chain (fused schedule): None = by image size. Measured
-    # (profiles/r2/ab_g_wgrad_after_d_chain_r2.txt): 64x64 1.105 vs 1.13 ms, 28x28 even, 128x128
-    # 5.84 vs 5.70 ms, 256x256 106.2 vs 104.6 ms -- at the larger sizes the D chain (2B rows of
-    # the bigger images) is the longer one already
+    # G's weight gradients off the G chain's stream (fused schedule; where: _gw_place): None = by
+    # image size. Round 2, behind the D chain (profiles/r2/ab_g_wgrad_after_d_chain_r2.txt): 64x64
+    # 1.105 vs 1.13 ms, 28x28 even, 128x128 5.84 vs 5.70 ms, 256x256 106.2 vs 104.6 ms -- at the
+    # larger sizes the D chain (2B rows of the bigger images) is the longer one already
     G_WGRAD_ON_D_STREAM: Optional[bool] = None
 
     def _g_wgrad_on_d_stream(self) -> bool:
@@ -1117,7 +1117,10 @@ class HipEngine:
         env = os.environ.get("DCGAN_G_WGRAD_ON_D")
         if env in ("0", "1"):
             return env == "1"
-        return self.cfg.output_size <= 64
+        # 128x128 bf16 with the G weight gradients beside the chains (alt1): 34.4k-34.5k vs
+        # 33.8k-33.9k img/s; 256x256 fp16 within the noise, kept on cs
+        # (profiles/r5/ab_gw_place_128_256_r5.txt)
+        return self.cfg.output_size <= 128
 
     def _schedule(self) -> str:
         req = self._sched_req
@@ -1254,8 +1257,8 @@ class HipEngine:
         D's backward starts right after the forward: holding it until the g_loss chain has left
         D (so it overlaps only G's backward) measured 1.314 vs 1.297 ms/step on MI355X, and
         holding it behind only the first 3-7 G-chain ops measured slower as well
-        (profiles/r4/ab_d_start_after_r4.txt). G's weight gradients run behind the D chain on its
-        stream, except the last _gw_tail_on_main() of them, which follow the G chain on cs."""
+        (profiles/r4/ab_d_start_after_r4.txt). G's weight gradients run on the streams _gw_place()
+        gives (default: the idle alt1 stream, each as soon as its operand exists)."""
         ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
         ex.wait(ex.alt[0], cs)
         # host issue order (eager replay): the first DCGAN_G_FIRST ops of the G chain go out before
@@ -1263,8 +1266,8 @@ class HipEngine:
         g_first = min(self._a_fwd + self._g_first(), self._g_w[0][0] if self._g_w else self.progA.size())
         ex.run(self.progA, [cs, ex.side], self._a_fwd, g_first)
         ex.run(self.progB, ex.alt)
-        # the G chain: data gradients on cs; each G weight gradient on the D chain's stream after
-        # that chain, once cs has produced its operand (a mark after that progA position)
+        # the G chain: data gradients on cs; each G weight gradient on its _gw_place() stream once
+        # cs has produced its operand (a mark after that progA position)
         if not self._g_wgrad_on_d_stream():  # every G gradient on cs
             ex.run(self.progA, [cs, ex.side], g_first, -1)
             ex.run(self.progW, [cs, ex.side])
@@ -1277,24 +1280,58 @@ class HipEngine:
             marks.append(ex.mark(cs))
             pos = a_end
         ex.run(self.progA, [cs, ex.side], pos, -1)
-        w = 0
-        n_main = min(self._gw_tail_on_main(), len(self._g_w))
-        for m, (_, w_end) in zip(marks[:len(marks) - n_main], self._g_w[:len(self._g_w) - n_main]):
-            ex.wait_mark(ex.alt[0], m)
-            ex.run(self.progW, ex.alt, w, w_end)
+        place = self._gw_place()
+        streams = {"d": ex.alt, "s": [ex.side], "a": [ex.alt[1]]}
+        w, segs = 0, []
+        for k, (m, (_, w_end)) in enumerate(zip(marks, self._g_w)):
+            segs.append((place[k], w, w_end))
+            if place[k] != "c":
+                st = streams[place[k]]
+                ex.wait_mark(st[0], m)
+                ex.run(self.progW, st, w, w_end)
             w = w_end
+        for q in sorted(set(place) & {"s", "a"}):
+            ex.wait(cs, streams[q][0])
         if self._adam_early:
             # Adam(D) on the D chain's stream once the g_loss chain has left D (the first G-wgrad
             # mark follows it), beside the G chain's tail; Adam(G) + the step counter after the join
             assert self._g_w[0][0] >= self._a_gd_end
             ex.wait_mark(ex.alt[0], marks[0])
             ex.run(self.progC, ex.alt, 0, self._c_split)
-        if n_main:
-            # the last G weight gradients on cs after the G chain (their operands are produced
-            # there): the D chain's stream no longer runs them serially after everything else
-            ex.run(self.progW, [cs, ex.side], w, -1)
+        # the G weight gradients placed on cs run after the G chain (their operands are produced
+        # there): the D chain's stream no longer runs them serially after everything else
+        for q, lo, hi in segs:
+            if q == "c":
+                ex.run(self.progW, [cs, ex.side], lo, hi)
         ex.wait(cs, ex.alt[0])
         ex.run(self.progC, [cs, ex.side], self._c_split if self._adam_early else 0, -1)
+
+    def _gw_place(self) -> str:
+        """Stream of each G weight-gradient segment (progW between consecutive _g_w ends) in the
+        fused step: "d" behind the D chain on its stream, "c" on the G chain's stream after that
+        chain, "s" / "a" on the idle side / alt1 stream as soon as its operand exists (beside both
+        chains). DCGAN_GW_PLACE gives the string (one letter per segment); otherwise
+        DCGAN_GW_STREAM (d / side / alt1, default alt1) for all but the last
+        DCGAN_GW_TAIL_ON_MAIN (default 0) segments, which are "c".
+
+        64x64 bf16, 3 interleaved rounds (profiles/r5/ab_gw_place_r5.txt): "aaaa" 123.7k-124.0k,
+        "ssss" 123.4k-123.8k, "sssc" 123.0k-123.3k, "sasa" 122.6k-123.0k, "ssdd" 121.7k-122.6k
+        img/s against 122.8k-122.9k for round 4's "ddcc" (the D chain now ends only ~15 us before
+        the G chain, so weight gradients queued behind it all land after both chains)."""
+        n = len(self._g_w)
+        v = os.environ.get("DCGAN_GW_PLACE")
+        if v is not None:
+            if len(v) != n or set(v) - set("dcsa"):
+                raise ValueError("DCGAN_GW_PLACE must be %d letters of d/c/s/a, got %r" % (n, v))
+        else:
+            g = os.environ.get("DCGAN_GW_STREAM", "d" if self._adam_early else "alt1")
+            if g not in ("d", "side", "alt1"):
+                raise ValueError("DCGAN_GW_STREAM must be d, side or alt1, got %r" % g)
+            n_main = min(self._gw_tail_on_main(), n)
+            v = {"d": "d", "side": "s", "alt1": "a"}[g] * (n - n_main) + "c" * n_main
+        if self._adam_early and ("s" in v or "a" in v):
+            raise ValueError("DCGAN_ADAM_D_EARLY needs the G weight gradients on the d / c streams")
+        return v
 
     def _adam_d_early(self) -> bool:
         """DCGAN_ADAM_D_EARLY=1 (fused single-process bf16 step, G weight gradients behind the D
@@ -1313,12 +1350,11 @@ class HipEngine:
 
     def _gw_tail_on_main(self) -> int:
         """Number of trailing G weight-gradient segments the fused step runs on the G chain's
-        stream after that chain instead of behind the D chain (DCGAN_GW_TAIL_ON_MAIN). Default 2:
-        at 64x64 the D chain's stream otherwise still runs g_h2's and g_h1's weight gradients
-        serially for ~70 us after the G chain has finished (profiles/r4/step_profile_r4.txt);
-        measured 0 / 1 / 2 / 3 / 4 -> 114.0k / 115.2k / 116.1k-118.1k / 116.6k / 115.2k img/s
-        (profiles/r4/ab_gw_tail_on_main_r4.txt)."""
-        v = os.environ.get("DCGAN_GW_TAIL_ON_MAIN", "2")
+        stream after that chain (DCGAN_GW_TAIL_ON_MAIN, default 0; see _gw_place). Round 4, with
+        the others behind the D chain: 0 / 1 / 2 / 3 / 4 -> 114.0k / 115.2k / 116.1k-118.1k /
+        116.6k / 115.2k img/s (profiles/r4/ab_gw_tail_on_main_r4.txt); round 5, with the others
+        on the idle alt1 stream, 0 is best (profiles/r5/ab_gw_stream_r5.txt)."""
+        v = os.environ.get("DCGAN_GW_TAIL_ON_MAIN", "0")
         if not v.isdigit():
             raise ValueError("DCGAN_GW_TAIL_ON_MAIN must be a non-negative integer, got %r" % v)
         return int(v)

@@ -255,6 +255,38 @@ def test_fused_g_wgrad_tail_on_main_has_no_hazards(monkeypatch, n):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
+@pytest.mark.parametrize("where", ["side", "alt1"])
+@pytest.mark.parametrize("n", ["0", "2"])
+def test_fused_g_wgrad_stream_has_no_hazards(monkeypatch, where, n):
+    """DCGAN_GW_STREAM=side/alt1: the G weight gradients on an otherwise idle stream beside both
+    chains (each after its operand's mark), joined into cs before Adam."""
+    monkeypatch.setenv("DCGAN_GW_STREAM", where)
+    monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", n)
+    eng = _dry()
+    assert eng._gw_place() == where[0] * (4 - int(n)) + "c" * int(n)
+    hz, n_ops = SC.check_engine(eng)
+    assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+@pytest.mark.parametrize("place", ["sasa", "ssac", "dsac", "sdcc", "aaaa"])
+def test_fused_g_wgrad_placements_have_no_hazards(monkeypatch, place):
+    """DCGAN_GW_PLACE: G weight-gradient segments spread over the D chain's stream, cs and both
+    idle streams (two weight gradients may run at once: no shared workspace between them)."""
+    monkeypatch.setenv("DCGAN_GW_PLACE", place)
+    eng = _dry()
+    assert eng._gw_place() == place
+    hz, _ = SC.check_engine(eng)
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_fused_g_wgrad_place_rejects_bad_values(monkeypatch):
+    for bad in ("ss", "sxsc"):
+        monkeypatch.setenv("DCGAN_GW_PLACE", bad)
+        with pytest.raises(ValueError):
+            _dry()._gw_place()
+
+
 def test_fused_g_wgrad_tail_on_main_rejects_bad_values(monkeypatch):
     monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", "two")
     eng = _dry()
