@@ -821,6 +821,21 @@ class Program {
                            P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
     }, acc.v);
   }
+  // the first part of a split adam2 update (same arithmetic, any flat sub-ranges): the beta
+  // powers are only read here; the last part (adam2) advances them and the step
+  int adam2_part(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA,
+                 uintptr_t pA, size_t nA, float lrA, float b1A, float b2A, float epsA, uintptr_t wD, uintptr_t wbfD,
+                 uintptr_t gD, uintptr_t mD, uintptr_t vD, uintptr_t pD, size_t nD, float lrD, float b1D, float b2D,
+                 float epsD, float gscale, int stream) {
+    AccList acc;
+    acc.w(wA, nA * 4).w(wbfA, nA * es_).r(gA, nA * 4).w(mA, nA * 4).w(vA, nA * 4).r(pA, 8)
+        .w(wD, nD * 4).w(wbfD, nD * es_).r(gD, nD * 4).w(mD, nD * 4).w(vD, nD * 4).r(pD, 8);
+    return add(name, stream, [=](hipStream_t s) {
+      return KF(dcg_adam2)(P<float>(wA), P<elem_t>(wbfA), P<const float>(gA), P<float>(mA), P<float>(vA), P<float>(pA),
+                           nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD), P<float>(mD),
+                           P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, gscale, nullptr, nullptr, s);
+    }, acc.v);
+  }
   // the end of the step when wgrad3 ran the big weights' Adam in its store pass: Adam over the
   // remaining ranges, mirror casts over the others, beta powers + step (misc.hip adam_rest_kernel).
   // ranges: [(set 0=A / 1=D, cast_only, offset, count)] in elements, offsets / counts % 4 == 0
@@ -1152,6 +1167,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("b2d"), py::arg("b1g"), py::arg("b2g"), py::arg("step"), py::arg("stream"), py::arg("ls") = 0,
            py::arg("growth_interval") = 2000)
       .def("adam2", &Program::adam2)
+      .def("adam2_part", &Program::adam2_part)
       .def("nonfinite_check", &Program::nonfinite_check)
       .def("narrow_deconv", &Program::narrow_deconv)
       .def("nconv", &Program::nconv)

@@ -605,6 +605,9 @@ __global__ __launch_bounds__(256) void adam2_kernel(Adam2Set A, Adam2Set D, floa
     const elem4 o = {(elem_t)wv[0], (elem_t)wv[1], (elem_t)wv[2], (elem_t)wv[3]};
     wbf[i] = o;
   }
+  // counter == nullptr: a first part of the update (the beta powers and the step are advanced
+  // by a later adam2 launch over the remaining ranges)
+  if (!counter) return;
   // last arrival: every block has read the powers above before it increments the counter
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -357,12 +357,15 @@ class HipEngine:
         second part."""
         self.progC = self._prog()
         sch = self._schedule()
+        self._adam_alt = False
         self._adam_early = sch == "fused" and self.dt == 0 and self._adam_d_early()
         if self._adam_early:
             self._build_update_d_first(self.progC)  # Adam(D) on the D chain's stream, Adam(G) after the join
         elif sch == "fused" and self.dt == 0:
+            self._adam_alt = self._adam_split_alt()
             self._build_update_fused(self.progC)
-            self._c_split = self._c_split_a = self.progC.size()
+            if not self._adam_alt:
+                self._c_split = self._c_split_a = self.progC.size()
         elif sch in ("concurrent", "ddp") and not self.f16:
             self._build_update_d_first(self.progC)
         else:
@@ -1093,10 +1096,41 @@ class HipEngine:
                            _p(od.powers), Dm.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, ranges, 1.0 / self.world,
                            _p(self.step_counter), 0)
             return
+        if self._adam_alt:
+            # part 1 (progC[:_c_split], on the G weight gradients' stream once the D chain is done):
+            # Adam over D and over G from g_h2's weights on -- nothing the G chain still reads after
+            # its last weight-gradient mark; part 2 (after the join): G's projection, g_bn0 and
+            # g_h1's slice + the beta powers and the step
+            hi = self.model.g.offsets[self.gl[1].name + "/w"][0]
+            es = self.wbf_g.flat.element_size()
+            prog.adam2_part("adam_gd_a", _p(G.flat) + 4 * hi, _p(self.wbf_g.flat) + es * hi,
+                            _p(self.grad_g.flat) + 4 * hi, _p(og.m.flat) + 4 * hi, _p(og.v.flat) + 4 * hi,
+                            _p(og.powers), G.flat.numel() - hi, og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat),
+                            _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers),
+                            Dm.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, 1.0 / self.world, 0)
+            self._c_split = self._c_split_a = prog.size()
+            prog.adam2("adam_g_b", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
+                       _p(og.v.flat), _p(og.powers), hi, og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat),
+                       _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers), 0,
+                       od.lr, od.beta1, od.beta2, od.eps, 1.0 / self.world, _p(self.step_counter), 0)
+            return
         prog.adam2("adam_gd", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
                    _p(og.powers), G.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat), _p(self.wbf_d.flat),
                    _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers), Dm.flat.numel(), od.lr,
                    od.beta1, od.beta2, od.eps, 1.0 / self.world, _p(self.step_counter), 0)
+
+    def _adam_split_alt(self) -> bool:
+        """DCGAN_ADAM_SPLIT_ALT=1 (fused single-process bf16 step whose G weight gradients all run
+        on one idle stream, _gw_place() "aaaa" / "ssss"): the part of the two-model Adam that the G
+        chain's tail cannot touch runs on that stream beside the tail (see _build_update_fused).
+        Bit-identical, but 1.1-2.0 % slower at 64x64 (3/3 rounds) and 0.5-0.8 % at 128x128: like
+        every Adam beside the chains before it (profiles/r5/ab_adam_split_alt_r5.txt). Off."""
+        if os.environ.get("DCGAN_ADAM_SPLIT_ALT", "0") != "1" or self._adam_fused or len(self.gl) < 2:
+            return False
+        if not self._g_wgrad_on_d_stream() or not self._g_w or self._g_w_layer[-1] != self.gl[0].name:
+            return False
+        place = self._gw_place()
+        return len(set(place)) == 1 and place[0] in "as"
 
     def _repack_weights_now(self):
         if self.progCast.size():
@@ -1290,6 +1324,15 @@ class HipEngine:
                 ex.wait_mark(st[0], m)
                 ex.run(self.progW, st, w, w_end)
             w = w_end
+        if self._adam_alt:
+            # Adam part 1 on the weight gradients' stream once the D chain is done (_adam_split_alt)
+            st = streams[place[-1]][0]
+            assert set(place) == {place[-1]}
+            ex.wait(st, ex.alt[0])
+            ex.run(self.progC, [st], 0, self._c_split)
+            ex.wait(cs, st)
+            ex.run(self.progC, [cs, ex.side], self._c_split, -1)
+            return
         for q in sorted(set(place) & {"s", "a"}):
             ex.wait(cs, streams[q][0])
         if self._adam_early:

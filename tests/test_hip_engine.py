@@ -491,19 +491,22 @@ def test_bn_fold_is_bit_identical_to_finalize_then_apply(monkeypatch, dtype, B):
 
 @pytest.mark.gpu
 def test_g_wgrad_placements_are_bit_identical(monkeypatch):
-    """The default G weight-gradient placement (idle alt1 stream, "aaaa") == round 4's (behind the
-    D chain, last two on cs: "ddcc") == two idle streams ("sasa"), bit for bit, 3 steps."""
+    """The default G weight-gradient placement (idle alt1 stream, "aaaa", with the first Adam part
+    on that stream) == round 4's (behind the D chain, last two on cs: "ddcc") == two idle streams
+    ("sasa") == "aaaa" with the one-launch Adam after the join, bit for bit, 3 steps."""
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     dev = torch.device("cuda", 0)
     B = 32
     real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     engs = []
-    for place in (None, "ddcc", "sasa"):
+    for place in (None, "ddcc", "sasa", "aaaa/one-adam"):
+        monkeypatch.setenv("DCGAN_ADAM_SPLIT_ALT", "0" if place and place.endswith("one-adam") else "1")
         if place is None:
             monkeypatch.delenv("DCGAN_GW_PLACE", raising=False)
         else:
-            monkeypatch.setenv("DCGAN_GW_PLACE", place)
+            monkeypatch.setenv("DCGAN_GW_PLACE", place[:4])
         e = HipEngine(DCGANConfig(), B, dev, graph=False, seed=5)
+        assert e._adam_alt == (place is None)
         e.set_batch(real)
         for _ in range(3):
             e.train_step()
@@ -511,10 +514,12 @@ def test_g_wgrad_placements_are_bit_identical(monkeypatch):
         engs.append(e)
     monkeypatch.delenv("DCGAN_GW_PLACE", raising=False)
     assert engs[0]._gw_place() == "aaaa"
+    assert all(e.global_step == 3 for e in engs)
     for e in engs[1:]:
         for a, b in ((engs[0].model.g.flat, e.model.g.flat), (engs[0].model.d.flat, e.model.d.flat),
                      (engs[0].opt_g.v.flat, e.opt_g.v.flat)):
             assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+        assert torch.equal(engs[0].wbf_g.flat, e.wbf_g.flat) and torch.equal(engs[0].opt_d.powers, e.opt_d.powers)
         assert engs[0].last_losses() == e.last_losses()
 
 

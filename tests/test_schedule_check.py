@@ -92,7 +92,8 @@ def test_op_accesses_are_recorded():
             if kind == eng.ext.OP_LAUNCH:
                 assert acc, "op %s records no accesses" % name
                 assert all(n > 0 for _, n, _ in acc)
-    assert ("adam_gd" in names or "adam_rest" in names or {"adam_g", "adam_d"} <= names)
+    assert ("adam_gd" in names or "adam_rest" in names or {"adam_g", "adam_d"} <= names
+            or {"adam_gd_a", "adam_g_b"} <= names)
     assert any(n.startswith("d_head") and n.endswith("+loss") for n in names)
     launches = sum(p.op_info(i)[2] == eng.ext.OP_LAUNCH for p in (eng.progA, eng.progB, eng.progW, eng.progC)
                    for i in range(p.size()))
@@ -280,6 +281,63 @@ def test_fused_g_wgrad_placements_have_no_hazards(monkeypatch, place):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
+def test_adam_split_alt_is_hazard_free(monkeypatch):
+    """DCGAN_ADAM_SPLIT_ALT=1, fused bf16 step: Adam over D and G from g_h2 on runs on the weight
+    gradients' stream beside the G chain's tail (progC[:_c_split]); the rest + the beta powers
+    after the join."""
+    monkeypatch.setenv("DCGAN_ADAM_SPLIT_ALT", "1")
+    eng = _dry()
+    assert eng._adam_alt and eng._c_split == 1
+    assert [eng.progC.op_info(i)[0] for i in range(eng.progC.size())] == ["adam_gd_a", "adam_g_b"]
+    hz, _ = SC.check_engine(eng)
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_adam_part_before_the_d_chain_ended(monkeypatch):
+    """The same first Adam part issued WITHOUT waiting for the D chain races D's weight
+    gradients (and the D chain's reads of D's weights)."""
+    monkeypatch.setenv("DCGAN_ADAM_SPLIT_ALT", "1")
+    eng = _dry()
+
+    def racy(ex):
+        cs, a1 = ex.main(), ex.alt[1]
+        ex.run(eng.progA, [cs, ex.side], 0, eng._a_fwd)
+        ex.wait(ex.alt[0], cs)
+        ex.run(eng.progB, ex.alt)
+        pos, w = eng._a_fwd, 0
+        for a_end, w_end in eng._g_w:
+            ex.run(eng.progA, [cs, ex.side], pos, a_end)
+            ex.wait(a1, cs)
+            ex.run(eng.progW, [a1], w, w_end)
+            pos, w = a_end, w_end
+        ex.run(eng.progA, [cs, ex.side], pos, -1)
+        ex.run(eng.progC, [a1], 0, eng._c_split)   # no wait for the D chain
+        ex.wait(cs, a1)
+        ex.wait(cs, ex.alt[0])
+        ex.run(eng.progC, [cs, ex.side], eng._c_split, -1)
+
+    eng._run_step = racy
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed Adam(D) racing the D chain"
+
+
+def test_checker_finds_adam_part_over_g_h1(monkeypatch):
+    """A first Adam part that also covers g_h1's weights races the G chain's g_h1 data gradient
+    (it reads g_h1's 16-bit mirror after the last weight-gradient mark)."""
+    monkeypatch.setenv("DCGAN_ADAM_SPLIT_ALT", "1")
+    eng = _dry()
+    lo = eng.model.g.offsets[eng.gl[0].name + "/w"][0]
+    G, og = eng.model.g, eng.opt_g
+    eng.progC = eng._prog()
+    eng.progC.adam2_part("bad", G.flat.data_ptr() + 4 * lo, eng.wbf_g.flat.data_ptr() + 2 * lo,
+                         eng.grad_g.flat.data_ptr() + 4 * lo, og.m.flat.data_ptr() + 4 * lo,
+                         og.v.flat.data_ptr() + 4 * lo, og.powers.data_ptr(), G.flat.numel() - lo, 1e-3, 0.5,
+                         0.999, 1e-8, 0, 0, 0, 0, 0, 0, 0, 1e-3, 0.5, 0.999, 1e-8, 1.0, 0)
+    eng._c_split = 1
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed Adam over g_h1 racing the g_h1 data gradient"
+
+
 def test_fused_g_wgrad_place_rejects_bad_values(monkeypatch):
     for bad in ("ss", "sxsc"):
         monkeypatch.setenv("DCGAN_GW_PLACE", bad)
@@ -289,9 +347,8 @@ def test_fused_g_wgrad_place_rejects_bad_values(monkeypatch):
 
 def test_fused_g_wgrad_tail_on_main_rejects_bad_values(monkeypatch):
     monkeypatch.setenv("DCGAN_GW_TAIL_ON_MAIN", "two")
-    eng = _dry()
     with pytest.raises(ValueError):
-        eng._gw_tail_on_main()
+        _dry()._gw_tail_on_main()
 
 
 @pytest.mark.parametrize("tail", ["0", "2", "4"])
@@ -373,4 +430,4 @@ def test_wgrad_adam_is_off_by_default():
     eng = _dry()
     assert not eng._wgrad_adam
     names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
-    assert names == ["adam_gd"]
+    assert names == (["adam_gd_a", "adam_g_b"] if eng._adam_alt else ["adam_gd"])
