@@ -106,12 +106,13 @@ def main():
                     help="rccl: CU + HBM-consuming copy kernel (comm_emu.hip); sleep: round-3 timer")
     ap.add_argument("--fake_nwg", type=int, default=32, help="workgroups (RCCL channels) of the rccl stand-in")
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--graph", type=int, default=1, help="1: segment hipGraphs (rounds 2-5 numbers), 0: eager replay")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig()
     ddp = a.schedule != "concurrent" or bool(a.fake_comm_us) or a.fake_busbw_gbs > 0
     eng = HipEngine(cfg, a.batch_size, dev, ddp=ddp, schedule=a.schedule if ddp else None,
-                    allreduce_dtype=a.allreduce_dtype)
+                    allreduce_dtype=a.allreduce_dtype, graph=bool(a.graph))
     if a.schedule in ("concurrent", "serial"):
         eng.enable_timing()  # the segmented schedules, Adam(G) / Adam(D) apart
     cpu = _cycles_per_us() if ddp and a.fake_kind == "sleep" else 0.0

@@ -1454,6 +1454,60 @@ class HipEngine:
         _, run, which = self._segments()[i]
         run(ex, stream, ex.side if which == self.MAIN else ex.alt[1])
 
+    def _ddp_gw_alt(self) -> int:
+        """DCGAN_DDP_GW_ALT (segmented DDP step, eager replay): 1 (default) = the G weight
+        gradients other than g_h1's run on the idle alt1 stream as soon as their operands exist
+        instead of after the G chain on cs, and G's slice above g_h1 goes on the wire from there;
+        2 = g_h1's as well (its collective then waits for alt1); 0 = round 4's segments.
+        Measured (profiles/r5/ab_ddp_gw_alt_b_r5.txt): W=1 one-rank RCCL 117.7k vs 111.9k-112.3k
+        img/s (2: 118.7k-120.0k); RCCL-like stand-in at W=8, 150 GB/s: 1.309-1.316 vs 1.336-1.341
+        ms (fp32 wire), 1.199-1.202 vs 1.242-1.245 (bf16), while 2 is slower there (1.359-1.361,
+        1.241-1.244). Graph-replayed segments keep round 4's layout."""
+        v = os.environ.get("DCGAN_DDP_GW_ALT", "1")
+        if v not in ("0", "1", "2"):
+            raise ValueError("DCGAN_DDP_GW_ALT must be 0, 1 or 2, got %r" % v)
+        if self.graph_enabled or self._g_split is None:
+            return 0
+        return int(v)
+
+    def _g_chain_gw_alt(self, ex, cs, mode: int):
+        """Segment "G_chain" with G's weight gradients on alt1 (_ddp_gw_alt), and the collective of
+        G's slice above g_h1 as soon as they are done. Returns the stream g_h1's gradient slice is
+        final on."""
+        A, W, a1 = self.progA, self.progW, ex.alt[1]
+        a_need, wb, we = self._g_split[:3]
+        pos, w = self._a_fwd, 0
+        for a_end, w_end in self._g_w:
+            if w_end > wb:
+                break
+            ex.run(A, [cs, ex.side], pos, a_end)
+            ex.wait(a1, cs)
+            ex.run(W, [a1], w, w_end)
+            pos, w = a_end, w_end
+        assert w == wb
+        # G's slice above g_h1 (g_h2's weights on: "gsplit_b") is final once these weight
+        # gradients are: its collective goes out now, into the comm stream's idle gap after D's top
+        # layer, instead of after the G chain
+        self._wire_cast(ex, "g_b", [a1])
+        self._ar_launch(ex, "gsplit_b", a1)
+        ex.run(A, [cs, ex.side], pos, a_need)
+        st = cs
+        if mode == 2:
+            ex.wait(a1, cs)
+            st = a1
+        ex.run(W, [st] if st is a1 else [st, ex.side], wb, we)
+        self._wire_cast(ex, "g_a", [st] if st is a1 else [st, ex.side])
+        return st
+
+    def _g_tail_gw_alt(self, ex, cs) -> None:
+        """Segment "G_tail" when G's weight gradients ran on alt1: the rest of the G chain, then
+        the join with alt1 before G's remaining slices are cast / reduced."""
+        we = self._g_split[2]
+        ex.run(self.progA, [cs, ex.side], self._g_split[0], -1)
+        ex.run(self.progW, [cs, ex.side], we, -1)
+        ex.wait(cs, ex.alt[1])
+        self._wire_cast(ex, "g_c", [cs, ex.side])
+
     def _ar_launch(self, ex, which: str, src) -> None:
         """All-reduce one gradient slice ("g", "dtop", "drest", "gsplit_a/b/c") on the comm stream
         once `src`'s queued work is done."""
@@ -1489,21 +1543,30 @@ class HipEngine:
             self._seg(ex, 1, alt)              # D chain: head + top layer gradients
             self._tick(2, alt)
             self._ar_launch(ex, "dtop", alt)
-            self._seg(ex, 2, cs)               # G chain: g_loss through D(fake), G backward to g_h1's wgrad
+            gw = self._ddp_gw_alt()
+            if gw:                             # the same segments with G's weight gradients on alt1
+                a_src = self._g_chain_gw_alt(ex, cs, gw)
+            else:
+                self._seg(ex, 2, cs)           # G chain: g_loss through D(fake), G backward to g_h1's wgrad
+                a_src = cs
             self._tick(3, cs)
             a_done = None
             if self._g_split is not None:
-                self._ar_launch(ex, "gsplit_a", cs)  # g_h1's slice, under the rest of both chains
+                self._ar_launch(ex, "gsplit_a", a_src)  # g_h1's slice, under the rest of both chains
                 a_done = ex.mark(ex.comm) if self.ddp else None
             self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
-            self._seg(ex, 4, cs)               # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
+            if gw:
+                self._g_tail_gw_alt(ex, cs)
+            else:
+                self._seg(ex, 4, cs)           # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
             self._tick(5, cs)
             # D's last bucket, then the rest of G's; Adam(D) runs while G's is in flight
             self._ar_launch(ex, "drest", alt)
             d_done = ex.mark(ex.comm) if self.ddp else None
             if self._g_split is not None:
-                self._ar_launch(ex, "gsplit_b", cs)
+                if not gw:                     # (else issued from alt1 inside the G chain)
+                    self._ar_launch(ex, "gsplit_b", cs)
                 self._ar_launch(ex, "gsplit_c", cs)
             else:
                 self._ar_launch(ex, "g", cs)

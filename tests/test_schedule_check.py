@@ -147,6 +147,36 @@ def test_checker_finds_adam_g_a_before_its_collective():
     assert hz, "the checker missed Adam(g_h1) racing its all-reduce"
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_ddp_gw_alt_has_no_hazards(monkeypatch, mode, wire):
+    """DCGAN_DDP_GW_ALT=1/2: the segmented DDP step with G's weight gradients (2: g_h1's too) on
+    the idle alt1 stream as soon as their operands exist; any wire."""
+    monkeypatch.setenv("DCGAN_DDP_GW_ALT", mode)
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False,
+                    allreduce_dtype=wire)
+    assert eng._schedule() == "concurrent" and eng._ddp_gw_alt() == int(mode)
+    hz, n_ops = SC.check_engine(eng)
+    assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_ddp_g_bucket_before_the_alt1_weight_gradients(monkeypatch):
+    """DCGAN_DDP_GW_ALT=1 with G's slice above g_h1 put on the wire from cs instead of from alt1
+    (i.e. without waiting for the weight gradients running there): the checker reports the race."""
+    monkeypatch.setenv("DCGAN_DDP_GW_ALT", "1")
+    eng = _dry(world=2)
+    orig = eng._ar_launch
+
+    def launch(ex, which, src):
+        orig(ex, which, ex.main() if which == "gsplit_b" else src)
+
+    eng._ar_launch = launch
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed G's collective racing the alt1 weight gradients"
+
+
 def test_checker_finds_an_early_g_bucket():
     """One-graph DDP: issuing G's first bucket one weight-gradient piece too early (before the
     piece that finalises it) is a race between the collective and that wgrad."""
