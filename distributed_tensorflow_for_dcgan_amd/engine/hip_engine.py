@@ -1458,14 +1458,15 @@ class HipEngine:
         """DCGAN_DDP_GW_ALT (segmented DDP step, eager replay): 1 (default) = the G weight
         gradients other than g_h1's run on the idle alt1 stream as soon as their operands exist
         instead of after the G chain on cs, and G's slice above g_h1 goes on the wire from there;
-        2 = g_h1's as well (its collective then waits for alt1); 0 = round 4's segments.
+        2 = g_h1's as well (its collective then waits for alt1); 3 = g_h1's on the idle side
+        stream at its operand's mark; 0 = round 4's segments.
         Measured (profiles/r5/ab_ddp_gw_alt_b_r5.txt): W=1 one-rank RCCL 117.7k vs 111.9k-112.3k
         img/s (2: 118.7k-120.0k); RCCL-like stand-in at W=8, 150 GB/s: 1.309-1.316 vs 1.336-1.341
         ms (fp32 wire), 1.199-1.202 vs 1.242-1.245 (bf16), while 2 is slower there (1.359-1.361,
         1.241-1.244). Graph-replayed segments keep round 4's layout."""
         v = os.environ.get("DCGAN_DDP_GW_ALT", "1")
-        if v not in ("0", "1", "2"):
-            raise ValueError("DCGAN_DDP_GW_ALT must be 0, 1 or 2, got %r" % v)
+        if v not in ("0", "1", "2", "3"):
+            raise ValueError("DCGAN_DDP_GW_ALT must be 0, 1, 2 or 3, got %r" % v)
         if self.graph_enabled or self._g_split is None:
             return 0
         return int(v)
@@ -1491,21 +1492,24 @@ class HipEngine:
         self._wire_cast(ex, "g_b", [a1])
         self._ar_launch(ex, "gsplit_b", a1)
         ex.run(A, [cs, ex.side], pos, a_need)
-        st = cs
-        if mode == 2:
-            ex.wait(a1, cs)
-            st = a1
-        ex.run(W, [st] if st is a1 else [st, ex.side], wb, we)
-        self._wire_cast(ex, "g_a", [st] if st is a1 else [st, ex.side])
+        st, sl = cs, [cs, ex.side]
+        if mode in (2, 3):
+            st = a1 if mode == 2 else ex.side
+            ex.wait(st, cs)
+            sl = [st]
+        ex.run(W, sl, wb, we)
+        self._wire_cast(ex, "g_a", sl)
         return st
 
-    def _g_tail_gw_alt(self, ex, cs) -> None:
+    def _g_tail_gw_alt(self, ex, cs, mode: int) -> None:
         """Segment "G_tail" when G's weight gradients ran on alt1: the rest of the G chain, then
-        the join with alt1 before G's remaining slices are cast / reduced."""
+        the join with alt1 (and side, mode 3) before G's remaining slices are cast / reduced."""
         we = self._g_split[2]
         ex.run(self.progA, [cs, ex.side], self._g_split[0], -1)
         ex.run(self.progW, [cs, ex.side], we, -1)
         ex.wait(cs, ex.alt[1])
+        if mode == 3:
+            ex.wait(cs, ex.side)
         self._wire_cast(ex, "g_c", [cs, ex.side])
 
     def _ar_launch(self, ex, which: str, src) -> None:
@@ -1557,7 +1561,7 @@ class HipEngine:
             self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
             if gw:
-                self._g_tail_gw_alt(ex, cs)
+                self._g_tail_gw_alt(ex, cs, gw)
             else:
                 self._seg(ex, 4, cs)           # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
             self._tick(5, cs)

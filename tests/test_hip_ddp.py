@@ -295,7 +295,7 @@ def _rccl_worker(out_dir, graph, port, schedule, gw_alt="0"):
 
 @pytest.mark.parametrize("graph,schedule,gw_alt", [(False, "ddp", "0"), (True, "ddp", "0"), (True, "concurrent", "0"),
                                                    (False, "concurrent", "0"), (False, "concurrent", "1"),
-                                                   (False, "concurrent", "2")])
+                                                   (False, "concurrent", "2"), (False, "concurrent", "3")])
 def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule, gw_alt):
     """The REAL collective path on a one-GPU box: a one-rank RCCL (backend "nccl") process group
     (DCGAN_FORCE_DDP=1). "ddp": the RCCL all-reduces captured INSIDE the step's single hipGraph

@@ -147,7 +147,7 @@ def test_checker_finds_adam_g_a_before_its_collective():
     assert hz, "the checker missed Adam(g_h1) racing its all-reduce"
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
 @pytest.mark.parametrize("wire", ["fp32", "bf16"])
 def test_ddp_gw_alt_has_no_hazards(monkeypatch, mode, wire):
     """DCGAN_DDP_GW_ALT=1/2: the segmented DDP step with G's weight gradients (2: g_h1's too) on
@@ -159,6 +159,17 @@ def test_ddp_gw_alt_has_no_hazards(monkeypatch, mode, wire):
     assert eng._schedule() == "concurrent" and eng._ddp_gw_alt() == int(mode)
     hz, n_ops = SC.check_engine(eng)
     assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
+def test_gw_alt_timed_single_process_has_no_hazards(monkeypatch, mode):
+    """W=1 with phase timers (the segmented step without collectives, so no comm-stream joins):
+    every DCGAN_DDP_GW_ALT mode still joins its streams into cs."""
+    monkeypatch.setenv("DCGAN_DDP_GW_ALT", mode)
+    eng = _dry(timing=True)
+    assert eng._schedule() == "concurrent" and not eng.ddp and eng._ddp_gw_alt() == int(mode)
+    hz, _ = SC.check_engine(eng)
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
