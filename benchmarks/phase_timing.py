@@ -91,6 +91,42 @@ def ring_us(numel: int, busbw_gbs: float, lat_us: float, world: int, esize: int 
     return lat_us + 2.0 * (world - 1) / world * numel * esize / (busbw_gbs * 1e3)
 
 
+def standin_engine(cfg, B, dev, schedule="concurrent", ddp=True, graph=False, wire="fp32", busbw_gbs=150.0,
+                   lat_us=10.0, world=8, kind="rccl", nwg=32, comm_us="", timing=False, dtype="bf16"):
+    """A one-GPU HipEngine running the DDP step with FakeReducer collectives at the real call
+    points (the RCCL-like stand-in). Returns (engine, {collective: modelled us})."""
+    eng = HipEngine(cfg, B, dev, ddp=ddp, schedule=schedule if ddp else None, allreduce_dtype=wire, graph=graph,
+                    dtype=dtype)
+    if timing:
+        eng.enable_timing()  # the segmented schedules, Adam(G) / Adam(D) apart
+    cpu = _cycles_per_us() if ddp and kind == "sleep" else 0.0
+    esize = 2 if wire == "bf16" else 4
+    comm = {}
+    if ddp:
+        # collective call points of DDP on a comm stream; the update program is rebuilt for W=2
+        # (Adam scales the un-reduced gradients by 1/2: only timing and stream order are emulated)
+        eng.world = 2
+        eng._build_updates()
+        eng._ensure_comm()
+
+        def fake(name, real, us=None):
+            flat = real.flat
+            if us is None:
+                us = ring_us(flat.numel(), busbw_gbs, lat_us, world, esize) if busbw_gbs > 0 else 0.0
+            comm[name] = round(us, 1)
+            return FakeReducer(us, flat, world, esize, nwg, kind, cpu, prefilled=real.wire if real.prefilled else None)
+
+        us3 = [float(x) for x in comm_us.split(",")] if comm_us else [None] * 3
+        eng._ar_dtop = fake("dtop", eng._ar_dtop, us3[1])
+        eng._ar_drest = fake("drest", eng._ar_drest, us3[2])
+        if schedule == "ddp":
+            eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), r) for (_, lo, hi), r in zip(eng._g_cuts, eng._ar_gparts)]
+        for name, r in list(vars(eng).items()):  # the G buckets of the segmented schedules
+            if (name == "_ar_g" or name.startswith("_ar_gsplit")) and isinstance(r, D.GradAllReducer):
+                setattr(eng, name, fake(name[4:], r, us3[0] if name == "_ar_g" else None))
+    return eng, comm
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch_size", type=int, default=128)
@@ -111,37 +147,10 @@ def main():
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig()
     ddp = a.schedule != "concurrent" or bool(a.fake_comm_us) or a.fake_busbw_gbs > 0
-    eng = HipEngine(cfg, a.batch_size, dev, ddp=ddp, schedule=a.schedule if ddp else None,
-                    allreduce_dtype=a.allreduce_dtype, graph=bool(a.graph))
-    if a.schedule in ("concurrent", "serial"):
-        eng.enable_timing()  # the segmented schedules, Adam(G) / Adam(D) apart
-    cpu = _cycles_per_us() if ddp and a.fake_kind == "sleep" else 0.0
-    esize = 2 if a.allreduce_dtype == "bf16" else 4
-    comm = {}
-    if ddp:
-        # collective call points of DDP on a comm stream; the update program is rebuilt for W=2
-        # (Adam scales the un-reduced gradients by 1/2: only timing and stream order are emulated)
-        eng.world = 2
-        eng._build_updates()
-        eng._ensure_comm()
-
-        def fake(name, real, us=None):
-            flat = real.flat
-            if us is None:
-                us = (ring_us(flat.numel(), a.fake_busbw_gbs, a.fake_lat_us, a.fake_world, esize)
-                      if a.fake_busbw_gbs > 0 else 0.0)
-            comm[name] = round(us, 1)
-            return FakeReducer(us, flat, a.fake_world, esize, a.fake_nwg, a.fake_kind, cpu,
-                               prefilled=real.wire if real.prefilled else None)
-
-        us3 = [float(x) for x in a.fake_comm_us.split(",")] if a.fake_comm_us else [None] * 3
-        eng._ar_dtop = fake("dtop", eng._ar_dtop, us3[1])
-        eng._ar_drest = fake("drest", eng._ar_drest, us3[2])
-        if a.schedule == "ddp":
-            eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), r) for (_, lo, hi), r in zip(eng._g_cuts, eng._ar_gparts)]
-        for name, r in list(vars(eng).items()):  # the G buckets of the segmented schedules
-            if (name == "_ar_g" or name.startswith("_ar_gsplit")) and isinstance(r, D.GradAllReducer):
-                setattr(eng, name, fake(name[4:], r, us3[0] if name == "_ar_g" else None))
+    eng, comm = standin_engine(cfg, a.batch_size, dev, schedule=a.schedule, ddp=ddp, graph=bool(a.graph),
+                               wire=a.allreduce_dtype, busbw_gbs=a.fake_busbw_gbs, lat_us=a.fake_lat_us,
+                               world=a.fake_world, kind=a.fake_kind, nwg=a.fake_nwg, comm_us=a.fake_comm_us,
+                               timing=a.schedule in ("concurrent", "serial"))
     eng.set_synthetic_batch(torch.rand(a.batch_size, 64, 64, 3, device=dev) * 2 - 1)
     for _ in range(a.warmup):
         eng.train_step()

@@ -8,6 +8,10 @@ try its neighbours (half / double split-K, one more / one fewer LDS stage, a few
 rebuild the engine, time ``--steps`` graph-replayed steps, keep a change only if it beats the
 incumbent by more than ``--min_gain``. One process, every candidate on the same GPU.
 
+``--standin_world 8``: tune the segmented DDP step (what N = 2..8 ranks run) with the RCCL-like
+stand-in collectives of ``benchmarks/phase_timing.py``; its table goes to ``--out`` (bench.py reads
+``ops/igemm_tuned_ddp.json`` for the DDP step when that file exists).
+
 ``python -m benchmarks.tune_insitu [--steps 150] [--passes 1] [--write]`` -- ``--write`` stores the
 result in ops/igemm_tuned.json (the table the engine reads). Other image sizes / dtypes
 (``--output_size 128``, ``--output_size 256 --batch 512 --dtype fp16``): the layers with no table
@@ -27,11 +31,16 @@ from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
 
 
 GRAPH = False  # --graph: time the hipGraph replay instead of the (default) C++ launch replay
+STANDIN = None  # --standin_world W: time the segmented DDP step with RCCL-like stand-in collectives
 
 
 def step_ms(cfg, B, steps, warmup, dtype="bf16"):
     dev = torch.device("cuda", 0)
-    eng = HipEngine(cfg, B, dev, seed=0, dtype=dtype, graph=GRAPH)
+    if STANDIN is not None:
+        from benchmarks.phase_timing import standin_engine
+        eng, _ = standin_engine(cfg, B, dev, graph=GRAPH, dtype=dtype, **STANDIN)
+    else:
+        eng = HipEngine(cfg, B, dev, seed=0, dtype=dtype, graph=GRAPH)
     real = torch.rand(B, cfg.output_size, cfg.output_size, cfg.c_dim, device=dev) * 2 - 1
     eng.set_synthetic_batch(real)
     for _ in range(warmup):
@@ -155,9 +164,15 @@ def main():
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--graph", type=int, default=0, help="1: tune under hipGraph replay (the pre-round-5 default)")
     ap.add_argument("--out", default="", help="also write the resulting table (JSON) here")
+    ap.add_argument("--standin_world", type=int, default=0,
+                    help="W > 0: tune the segmented DDP step (the N-GPU path) with the RCCL-like stand-in at W ranks")
+    ap.add_argument("--standin_busbw", type=float, default=150.0, help="stand-in ring bus bandwidth (GB/s)")
+    ap.add_argument("--standin_wire", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
-    global GRAPH
+    global GRAPH, STANDIN
     GRAPH = bool(a.graph)
+    if a.standin_world > 0:
+        STANDIN = dict(world=a.standin_world, busbw_gbs=a.standin_busbw, wire=a.standin_wire)
     cfg = DCGANConfig(output_size=a.output_size, c_dim=a.c_dim)
     table = H.tuned_table()
     keys = used_keys(cfg, a.batch, a.dtype, a.seed)
