@@ -9,8 +9,8 @@ rebuild the engine, time ``--steps`` graph-replayed steps, keep a change only if
 incumbent by more than ``--min_gain``. One process, every candidate on the same GPU.
 
 ``--standin_world 8``: tune the segmented DDP step (what N = 2..8 ranks run) with the RCCL-like
-stand-in collectives of ``benchmarks/phase_timing.py``; its table goes to ``--out`` (bench.py reads
-``ops/igemm_tuned_ddp.json`` for the DDP step when that file exists).
+stand-in collectives of ``benchmarks/phase_timing.py``; its table goes to ``--out`` only (a study:
+``profiles/r5/ab_ddp_table_r5.txt``; the engine has one table for every schedule).
 
 ``python -m benchmarks.tune_insitu [--steps 150] [--passes 1] [--write]`` -- ``--write`` stores the
 result in ops/igemm_tuned.json (the table the engine reads). Other image sizes / dtypes
