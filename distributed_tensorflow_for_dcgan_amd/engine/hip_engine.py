@@ -324,6 +324,7 @@ class HipEngine:
         # D-gradient slice final after the D chain's first segment: the top conv layer (+ its BN)
         # and the head, which the ParamSet lays out last
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
+        self._d_mid_off = self.model.d.offsets[self.dl[-2].name + "/w"][0] if len(self.dl) >= 3 else None
         self._g_cuts = self._g_bucket_cuts()
         self._g_split = self._g_split_plan()
         self._build_updates()  # (after the G split: Adam(G) follows its collectives)
@@ -332,7 +333,9 @@ class HipEngine:
             o = self._d_top_off
             nd, ng = self.grad_d.flat.numel(), self.grad_g.flat.numel()
             lo, hi = self._g_split[3:] if self._g_split is not None else (0, ng)
+            m = self._d_mid_off or 0
             for name, src, dst, a, b in (("dtop", self.grad_d, self.wire_d, o, nd), ("drest", self.grad_d, self.wire_d, 0, o),
+                                         ("dmid", self.grad_d, self.wire_d, m, o), ("drest2", self.grad_d, self.wire_d, 0, m),
                                          ("g", self.grad_g, self.wire_g, 0, ng), ("g_a", self.grad_g, self.wire_g, lo, hi),
                                          ("g_b", self.grad_g, self.wire_g, hi, ng), ("g_c", self.grad_g, self.wire_g, 0, lo)):
                 if b > a:
@@ -718,6 +721,8 @@ class HipEngine:
                     # head + top layer gradients final: DDP splits the segment here so their
                     # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
                     self._b_split = prog.size()
+                if i == len(self.dl) - 2:
+                    self._b_split2 = prog.size()  # the next layer down final too (_ddp_dmid)
 
             def emit_dgrad(i=i, L=L, dx=dx):
                 fused = None
@@ -1454,6 +1459,18 @@ class HipEngine:
         _, run, which = self._segments()[i]
         run(ex, stream, ex.side if which == self.MAIN else ex.alt[1])
 
+    def _ddp_dmid_wanted(self) -> bool:
+        """DCGAN_DDP_DMID=1 (segmented DDP step, eager replay): D's gradient in three collectives
+        -- top layer + head, the next layer down as soon as its weight gradient lands (issued
+        before G's on the comm stream), the rest at the D chain's end -- instead of two."""
+        return (os.environ.get("DCGAN_DDP_DMID", "0") == "1" and self._schedule() == "concurrent"
+                and self._d_mid_off is not None and getattr(self, "_b_split2", 0) > self._b_split)
+
+    def _ddp_dmid(self) -> bool:
+        if self.graph_enabled:
+            return False
+        return getattr(self, "_dmid", False) if self.ddp else self._ddp_dmid_wanted()
+
     def _ddp_gw_alt(self) -> int:
         """DCGAN_DDP_GW_ALT (segmented DDP step, eager replay): 1 (default) = the G weight
         gradients other than g_h1's run on the idle alt1 stream as soon as their operands exist
@@ -1547,6 +1564,13 @@ class HipEngine:
             self._seg(ex, 1, alt)              # D chain: head + top layer gradients
             self._tick(2, alt)
             self._ar_launch(ex, "dtop", alt)
+            dmid = self._ddp_dmid()
+            if dmid:
+                # D's next layer down: its slice goes out right after D's top layer on the comm
+                # stream (issue order = comm order), into the gap before G's first collective
+                ex.run(self.progB, ex.alt, self._b_split, self._b_split2)
+                self._wire_cast(ex, "dmid", ex.alt)
+                self._ar_launch(ex, "dmid", alt)
             gw = self._ddp_gw_alt()
             if gw:                             # the same segments with G's weight gradients on alt1
                 a_src = self._g_chain_gw_alt(ex, cs, gw)
@@ -1558,7 +1582,11 @@ class HipEngine:
             if self._g_split is not None:
                 self._ar_launch(ex, "gsplit_a", a_src)  # g_h1's slice, under the rest of both chains
                 a_done = ex.mark(ex.comm) if self.ddp else None
-            self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
+            if dmid:
+                ex.run(self.progB, ex.alt, self._b_split2, -1)
+                self._wire_cast(ex, "drest2", ex.alt)
+            else:
+                self._seg(ex, 3, alt)          # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
             if gw:
                 self._g_tail_gw_alt(ex, cs, gw)
@@ -1566,7 +1594,7 @@ class HipEngine:
                 self._seg(ex, 4, cs)           # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
             self._tick(5, cs)
             # D's last bucket, then the rest of G's; Adam(D) runs while G's is in flight
-            self._ar_launch(ex, "drest", alt)
+            self._ar_launch(ex, "drest2" if dmid else "drest", alt)
             d_done = ex.mark(ex.comm) if self.ddp else None
             if self._g_split is not None:
                 if not gw:                     # (else issued from alt1 inside the G chain)
@@ -1634,8 +1662,13 @@ class HipEngine:
                                         native=native)
 
             self._ar_dtop = mk(df[o:], wdf[o:] if direct else None)
-            self._ar_drest = mk(df[:o], wdf[:o] if direct else None)
             sch = self._schedule()
+            self._ar_drest = mk(df[:o], wdf[:o] if direct else None)  # (also for graph-replayed segments)
+            self._dmid = self._ddp_dmid_wanted()
+            if self._dmid:  # D's second-highest layer on the wire once its gradient is final
+                m = self._d_mid_off
+                self._ar_dmid = mk(df[m:o], wdf[m:o] if direct else None)
+                self._ar_drest2 = mk(df[:m], wdf[:m] if direct else None)
             if sch == "serial" or (sch == "concurrent" and self._g_split is None):
                 self._ar_g = mk(gf, wgf if direct else None)
             elif sch == "concurrent":  # g_h1's slice first, then the two others

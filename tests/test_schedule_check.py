@@ -173,6 +173,33 @@ def test_gw_alt_timed_single_process_has_no_hazards(monkeypatch, mode):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_ddp_dmid_has_no_hazards(monkeypatch, wire):
+    """DCGAN_DDP_DMID=1: D's gradient in three collectives (top layer + head; the next layer down
+    as soon as its weight gradient lands; the rest at the D chain's end)."""
+    monkeypatch.setenv("DCGAN_DDP_DMID", "1")
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False,
+                    allreduce_dtype=wire)
+    eng._ensure_comm()
+    assert eng._ddp_dmid() and eng._b_split < eng._b_split2
+    hz, n_ops = SC.check_engine(eng)
+    assert n_ops > 100
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_ddp_dmid_before_its_weight_gradient(monkeypatch):
+    """The D-mid collective issued one op too early (before the weight gradient that finalises
+    its slice) is a race the checker reports."""
+    monkeypatch.setenv("DCGAN_DDP_DMID", "1")
+    eng = _dry(world=2)
+    eng._ensure_comm()
+    assert eng._ddp_dmid()
+    eng._b_split2 -= 1
+    hz, _ = SC.check_engine(eng)
+    assert hz, "the checker missed D's middle collective racing its weight gradient"
+
+
 def test_checker_finds_ddp_g_bucket_before_the_alt1_weight_gradients(monkeypatch):
     """DCGAN_DDP_GW_ALT=1 with G's slice above g_h1 put on the wire from cs instead of from alt1
     (i.e. without waiting for the weight gradients running there): the checker reports the race."""
