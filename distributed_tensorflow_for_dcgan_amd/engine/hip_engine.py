@@ -685,6 +685,7 @@ class HipEngine:
         last = self.dl[-1]
         fused_next = self._head_bwd(prog, "d_head.bwd", self.d_a[last.name], self.dl_d, self.d_da[last.name],
                                     gD[lin + "/Matrix"], gD[lin + "/bias"], B2, last, 2, 0)
+        wside = self._dws = self._d_wgrad_side()
         # fused_next: BN-backward partials emitted by the layer above (head / dgrad GEMM store pass)
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
@@ -704,19 +705,25 @@ class HipEngine:
             def emit_wgrad(i=i, L=L, dx=dx):
                 src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
                 pad = same_pads(L.in_hw)[0]
+                ws = 0
+                if wside:  # (study) on the D chain's slot-1 stream once dx exists
+                    ev = prog.new_event()
+                    prog.record(ev, 0)
+                    prog.wait(ev, 1)
+                    ws = 1
                 if i == 0 and self._d0_direct() and prog.nwgrad_ok(L.in_hw, L.in_hw, L.out_hw, L.out_hw):
                     # image window staged per workgroup, no column matrix (narrow2.hip nwgrad)
                     prog.nwgrad(L.name + ".nwgrad", _p(self.d_in), B2, L.in_hw, L.in_hw, L.cin, _p(dx), L.out_hw,
-                                L.out_hw, pad, _p(gD[L.name + "/w"]), 0)
+                                L.out_hw, pad, _p(gD[L.name + "/w"]), ws)
                 elif i == 0 and L.cin % 8 != 0:
                     if self._d0_direct():  # the forward ran without a column matrix: build it here
                         prog.im2col_s2("d0.im2col", _p(self.d_in), _p(self.d0_col), B2, L.in_hw, L.in_hw, L.cin,
-                                       L.out_hw, L.out_hw, pad, pad, self.kp_d0, 0)
+                                       L.out_hw, L.out_hw, pad, pad, self.kp_d0, ws)
                     self._wgrad(prog, L.name, 2, self.d0_col, 1, 1, self.kp_d0, dx, B2 * L.out_hw ** 2, 1, 1, L.cout, 0,
-                                gD[L.name + "/w"])
+                                gD[L.name + "/w"], stream=ws)
                 else:
                     self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
-                                gD[L.name + "/w"], adam_of=("d", L.name + "/w"))
+                                gD[L.name + "/w"], stream=ws, adam_of=("d", L.name + "/w"))
                 if i == len(self.dl) - 1:
                     # head + top layer gradients final: DDP splits the segment here so their
                     # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
@@ -750,6 +757,10 @@ class HipEngine:
             # profiles/r2/ab_d_dgrad_first_r2.txt)
             emit_wgrad()
             fused_next = emit_dgrad()
+        if wside:  # join the weight gradients back into the D chain's stream
+            ev = prog.new_event()
+            prog.record(ev, 1)
+            prog.wait(ev, 0)
 
     def _g_bucket_cuts(self) -> List[Tuple[int, int, int]]:
         """G's gradient buckets for the "ddp" schedule: (progW piece index, lo, hi) -- after G's
@@ -1304,7 +1315,7 @@ class HipEngine:
         # the D chain's, so they sit first in the forward's queue
         g_first = min(self._a_fwd + self._g_first(), self._g_w[0][0] if self._g_w else self.progA.size())
         ex.run(self.progA, [cs, ex.side], self._a_fwd, g_first)
-        ex.run(self.progB, ex.alt)
+        ex.run(self.progB, [ex.alt[0], ex.side] if self._dws else ex.alt)
         # the G chain: data gradients on cs; each G weight gradient on its _gw_place() stream once
         # cs has produced its operand (a mark after that progA position)
         if not self._g_wgrad_on_d_stream():  # every G gradient on cs
@@ -1458,6 +1469,13 @@ class HipEngine:
             return
         _, run, which = self._segments()[i]
         run(ex, stream, ex.side if which == self.MAIN else ex.alt[1])
+
+    def _d_wgrad_side(self) -> bool:
+        """DCGAN_D_WGRAD_SIDE=1 (study; fused single-process step): D's weight gradients on a
+        stream of their own (progB slot 1 = the idle side stream), each after its dx exists,
+        joined back at the D chain's end; the D chain keeps only the data gradients."""
+        return (os.environ.get("DCGAN_D_WGRAD_SIDE", "0") == "1" and not self.ddp and not self._timing
+                and self._sched_req in (None, "fused"))
 
     def _ddp_dmid_wanted(self) -> bool:
         """DCGAN_DDP_DMID=1 (segmented DDP step, eager replay): D's gradient in three collectives

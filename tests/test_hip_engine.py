@@ -499,20 +499,23 @@ def test_g_wgrad_placements_are_bit_identical(monkeypatch):
     B = 32
     real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     engs = []
-    for place in (None, "ddcc", "sasa", "aaaa/one-adam"):
+    for place in (None, "ddcc", "sasa", "aaaa/one-adam", "aaaa/d-wgrad-side"):
         monkeypatch.setenv("DCGAN_ADAM_SPLIT_ALT", "0" if place and place.endswith("one-adam") else "1")
+        monkeypatch.setenv("DCGAN_D_WGRAD_SIDE", "1" if place and place.endswith("d-wgrad-side") else "0")
         if place is None:
             monkeypatch.delenv("DCGAN_GW_PLACE", raising=False)
         else:
             monkeypatch.setenv("DCGAN_GW_PLACE", place[:4])
         e = HipEngine(DCGANConfig(), B, dev, graph=False, seed=5)
-        assert e._adam_alt == (place is None)
+        assert e._adam_alt == (place is None or place.endswith("d-wgrad-side"))
+        assert e._dws == bool(place and place.endswith("d-wgrad-side"))
         e.set_batch(real)
         for _ in range(3):
             e.train_step()
         torch.cuda.synchronize()
         engs.append(e)
     monkeypatch.delenv("DCGAN_GW_PLACE", raising=False)
+    monkeypatch.delenv("DCGAN_D_WGRAD_SIDE", raising=False)
     assert engs[0]._gw_place() == "aaaa"
     assert all(e.global_step == 3 for e in engs)
     for e in engs[1:]:

@@ -406,6 +406,18 @@ def test_checker_finds_adam_part_over_g_h1(monkeypatch):
     assert hz, "the checker missed Adam over g_h1 racing the g_h1 data gradient"
 
 
+def test_d_wgrad_side_has_no_hazards(monkeypatch):
+    """DCGAN_D_WGRAD_SIDE=1 (study): D's weight gradients on progB's slot-1 stream (the side
+    stream in the fused step), each after its dx, joined back at the D chain's end."""
+    monkeypatch.setenv("DCGAN_D_WGRAD_SIDE", "1")
+    eng = _dry()
+    assert eng._dws
+    slots = {eng.progB.op_info(i)[1] for i in range(eng.progB.size())}
+    assert slots == {0, 1}
+    hz, _ = SC.check_engine(eng)
+    assert hz == [], "\n".join(map(str, hz[:10]))
+
+
 def test_fused_g_wgrad_place_rejects_bad_values(monkeypatch):
     for bad in ("ss", "sxsc"):
         monkeypatch.setenv("DCGAN_GW_PLACE", bad)
