@@ -119,9 +119,6 @@ def standin_engine(cfg, B, dev, schedule="concurrent", ddp=True, graph=False, wi
         us3 = [float(x) for x in comm_us.split(",")] if comm_us else [None] * 3
         eng._ar_dtop = fake("dtop", eng._ar_dtop, us3[1])
         eng._ar_drest = fake("drest", eng._ar_drest, us3[2])
-        for name in ("_ar_dmid", "_ar_drest2"):  # DCGAN_DDP_DMID: D's gradient in three pieces
-            if getattr(eng, name, None) is not None:
-                setattr(eng, name, fake(name[4:], getattr(eng, name)))
         if schedule == "ddp":
             eng._ar_gparts = [fake("g[%d:%d]" % (lo, hi), r) for (_, lo, hi), r in zip(eng._g_cuts, eng._ar_gparts)]
         for name, r in list(vars(eng).items()):  # the G buckets of the segmented schedules

@@ -397,10 +397,8 @@ class Program {
 
   // weight gradient v3 (wgrad3.hip): the 25-tap gather GEMM with the split-K reduction in-kernel,
   // written scaled straight into the fp32 gradient dst [25][Mc][Nc] -- one launch, no slabs pass
-  // adam = (w, m, v, powers, lr, b1, b2, eps) of this weight: TF-Adam in the store pass (or empty)
   int wgrad3(std::string name, uintptr_t G, int Hg, int Wg, int Mc, uintptr_t Dm, int Bn, int Hd, int Wd, int Nc,
-             int pad, int cfg, int splits, uintptr_t dst, float scale, int stream,
-             std::tuple<uintptr_t, uintptr_t, uintptr_t, uintptr_t, float, float, float, float> adam) {
+             int pad, int cfg, int splits, uintptr_t dst, float scale, int stream) {
     int bm = 0, bn = 0, ns = 0, w5_wd = 0;
     const bool w5 = cfg >= 400;  // wgrad5.hip: one kernel row (5 taps) x all Mc x bn per workgroup
     if (w5) {
@@ -408,7 +406,6 @@ class Program {
       if (Mc % bm || Wd != w5_wd || (Hd % (64 / w5_wd) && (64 / w5_wd) % Hd) || (Bn * Hd * Wd) % 64)
         throw std::runtime_error("wgrad5 cfg " + std::to_string(cfg) + " does not fit Mc=" + std::to_string(Mc) +
                                  " Hd=" + std::to_string(Hd) + " Wd=" + std::to_string(Wd));
-      if (std::get<0>(adam)) throw std::runtime_error("wgrad5: no fused Adam");
     } else if (KF(dcg_wgrad3_tile)(cfg, &bm, &bn, &ns)) {
       throw std::runtime_error("bad wgrad3 cfg " + std::to_string(cfg));
     }
@@ -432,13 +429,6 @@ class Program {
     a.out = P<float>(dst); a.scale = scale;
     AccList acc;
     acc.r(G, g_elems * es_).r(Dm, d_elems * es_).w(dst, (size_t)25 * Mc * Nc * 4);
-    if (std::get<0>(adam)) {
-      const size_t nw = (size_t)25 * Mc * Nc;
-      a.aw = P<float>(std::get<0>(adam)); a.am = P<float>(std::get<1>(adam)); a.av = P<float>(std::get<2>(adam));
-      a.apow = P<const float>(std::get<3>(adam));
-      a.alr = std::get<4>(adam); a.ab1 = std::get<5>(adam); a.ab2 = std::get<6>(adam); a.aeps = std::get<7>(adam);
-      acc.w(std::get<0>(adam), nw * 4).w(std::get<1>(adam), nw * 4).w(std::get<2>(adam), nw * 4).r(std::get<3>(adam), 8);
-    }
     const int tt = w5 ? 1 : KF(dcg_wgrad3_taps_per_tile)(cfg);
     if (tt == 2 && 2 * Mc != bm) throw std::runtime_error("wgrad3: two-tap tiles need BM = 2 Mc");
     // wgrad5: 5 * ceil(Nc / bn) tiles of 5 taps x Mc x bn; wgrad3: tap (group) x m x n tiles of bm x bn
@@ -568,44 +558,6 @@ class Program {
     return add(name, stream, [=](hipStream_t s) {
       return KF(dcg_bn_bwd_apply)(P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x), P<const float>(coef),
                               P<elem_t>(dx), R, C, rows_per_group, act, leak, s);
-    }, acc.v);
-  }
-  // BN finalize + apply in one launch (bnfold.hip): each workgroup reduces its own group's partial
-  // rows for its 64 channels; the same reads and writes as bn_finalize + bn_apply_act together
-  bool bn_fold_ok(int ppg, int groups, int C, int rows_per_group) const {
-    return KF(dcg_bnfold_ok)(ppg, groups, C, rows_per_group) != 0;
-  }
-  int bn_fold_fwd(std::string name, uintptr_t part, int ppg, int groups, int C, double count, uintptr_t gamma,
-                  uintptr_t beta, float eps, uintptr_t mean, uintptr_t rstd, uintptr_t scale, uintptr_t shift,
-                  uintptr_t ema_mean, uintptr_t ema_var, float decay, uintptr_t x, uintptr_t y, int R, int act,
-                  float leak, int stream) {
-    if (R % groups || !bn_fold_ok(ppg, groups, C, R / groups)) throw std::runtime_error(name + ": bn_fold_fwd shape");
-    const size_t gc = (size_t)groups * C * 4, t = (size_t)R * C * es_;
-    AccList acc;
-    acc.r(part, (size_t)groups * ppg * 2 * C * 4).r(gamma, (size_t)C * 4).r(beta, (size_t)C * 4)
-        .w(mean, gc).w(rstd, gc).w(scale, gc).w(shift, gc).w(ema_mean, gc).w(ema_var, gc).r(x, t).w(y, t);
-    const int rpg = R / groups;
-    return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_bnfold_fwd)(P<const float>(part), ppg, groups, C, rpg, count, P<const float>(gamma),
-                                P<const float>(beta), eps, P<float>(mean), P<float>(rstd), P<float>(scale),
-                                P<float>(shift), P<float>(ema_mean), P<float>(ema_var), decay, P<const elem_t>(x),
-                                P<elem_t>(y), act, leak, s);
-    }, acc.v);
-  }
-  int bn_fold_bwd(std::string name, uintptr_t part, int ppg, int groups, int C, float count, uintptr_t gamma,
-                  uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef, uintptr_t dy,
-                  uintptr_t y, uintptr_t x, uintptr_t dx, int R, int act, float leak, int stream) {
-    if (R % groups || !bn_fold_ok(ppg, groups, C, R / groups)) throw std::runtime_error(name + ": bn_fold_bwd shape");
-    const size_t gc = (size_t)groups * C * 4, t = (size_t)R * C * es_;
-    AccList acc;
-    acc.r(part, (size_t)groups * ppg * 2 * C * 4).r(gamma, (size_t)C * 4).r(mean, gc).r(rstd, gc)
-        .w(dgamma, (size_t)C * 4).w(dbeta, (size_t)C * 4).w(coef, 3 * gc).r(dy, t).r(x, t).r(y, t).w(dx, t);
-    const int rpg = R / groups;
-    return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_bnfold_bwd)(P<const float>(part), ppg, groups, C, rpg, count, P<const float>(gamma),
-                                P<const float>(mean), P<const float>(rstd), P<float>(dgamma), P<float>(dbeta),
-                                P<float>(coef), P<const elem_t>(dy), P<const elem_t>(y), P<const elem_t>(x),
-                                P<elem_t>(dx), act, leak, s);
     }, acc.v);
   }
   int act_bwd(std::string name, uintptr_t dy, uintptr_t y, uintptr_t dx, size_t n, int act, float leak, int stream) {
@@ -819,53 +771,6 @@ class Program {
                            nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD), P<float>(mD),
                            P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, gscale,
                            P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
-    }, acc.v);
-  }
-  // the first part of a split adam2 update (same arithmetic, any flat sub-ranges): the beta
-  // powers are only read here; the last part (adam2) advances them and the step
-  int adam2_part(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA,
-                 uintptr_t pA, size_t nA, float lrA, float b1A, float b2A, float epsA, uintptr_t wD, uintptr_t wbfD,
-                 uintptr_t gD, uintptr_t mD, uintptr_t vD, uintptr_t pD, size_t nD, float lrD, float b1D, float b2D,
-                 float epsD, float gscale, int stream) {
-    AccList acc;
-    acc.w(wA, nA * 4).w(wbfA, nA * es_).r(gA, nA * 4).w(mA, nA * 4).w(vA, nA * 4).r(pA, 8)
-        .w(wD, nD * 4).w(wbfD, nD * es_).r(gD, nD * 4).w(mD, nD * 4).w(vD, nD * 4).r(pD, 8);
-    return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_adam2)(P<float>(wA), P<elem_t>(wbfA), P<const float>(gA), P<float>(mA), P<float>(vA), P<float>(pA),
-                           nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD), P<float>(mD),
-                           P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, gscale, nullptr, nullptr, s);
-    }, acc.v);
-  }
-  // the end of the step when wgrad3 ran the big weights' Adam in its store pass: Adam over the
-  // remaining ranges, mirror casts over the others, beta powers + step (misc.hip adam_rest_kernel).
-  // ranges: [(set 0=A / 1=D, cast_only, offset, count)] in elements, offsets / counts % 4 == 0
-  int adam_rest(std::string name, uintptr_t wA, uintptr_t wbfA, uintptr_t gA, uintptr_t mA, uintptr_t vA, uintptr_t pA,
-                size_t nA, float lrA, float b1A, float b2A, float epsA, uintptr_t wD, uintptr_t wbfD, uintptr_t gD,
-                uintptr_t mD, uintptr_t vD, uintptr_t pD, size_t nD, float lrD, float b1D, float b2D, float epsD,
-                std::vector<std::tuple<int, int, size_t, size_t>> ranges, float gscale, uintptr_t step, int stream) {
-    struct Blk { unsigned long long off4; unsigned n4; int set; int cast; int pad; };
-    std::vector<Blk> blks;
-    constexpr size_t kChunk4 = 256 * 8;  // float4s per workgroup
-    for (auto& r : ranges) {
-      const int set = std::get<0>(r), cast = std::get<1>(r);
-      const size_t off = std::get<2>(r), n = std::get<3>(r);
-      if (off % 4 || n % 4 || off + n > (set == 0 ? nA : nD)) throw std::runtime_error("adam_rest: bad range");
-      for (size_t o4 = off / 4; o4 < (off + n) / 4; o4 += kChunk4)
-        blks.push_back({(unsigned long long)o4, (unsigned)std::min(kChunk4, (off + n) / 4 - o4), set, cast, 0});
-    }
-    if (blks.empty()) throw std::runtime_error("adam_rest: no ranges");
-    void* table = dev_alloc(blks.size() * sizeof(Blk), blks.data());
-    void* ctr = dev_alloc(sizeof(unsigned), nullptr, true);
-    const int nb = (int)blks.size();
-    AccList acc;
-    acc.w(wA, nA * 4).w(wbfA, nA * es_).r(gA, nA * 4).w(mA, nA * 4).w(vA, nA * 4).w(pA, 8)
-        .w(wD, nD * 4).w(wbfD, nD * es_).r(gD, nD * 4).w(mD, nD * 4).w(vD, nD * 4).w(pD, 8).w(step, 8)
-        .w((uintptr_t)ctr, 4);
-    return add(name, stream, [=](hipStream_t s) {
-      return KF(dcg_adam_rest)(P<float>(wA), P<elem_t>(wbfA), P<const float>(gA), P<float>(mA), P<float>(vA),
-                               P<float>(pA), nA, lrA, b1A, b2A, epsA, P<float>(wD), P<elem_t>(wbfD), P<const float>(gD),
-                               P<float>(mD), P<float>(vD), P<float>(pD), nD, lrD, b1D, b2D, epsD, table, nb, gscale,
-                               P<unsigned long long>(step), reinterpret_cast<unsigned*>(ctr), s);
     }, acc.v);
   }
   // narrow2.hip: TF-SAME stride-2 5x5 conv, 1..4 input -> 64 output channels, persistent `grid`
@@ -1127,9 +1032,7 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("wgrad", &Program::wgrad)
       .def("wgrad3", &Program::wgrad3, py::arg("name"), py::arg("G"), py::arg("Hg"), py::arg("Wg"), py::arg("Mc"),
            py::arg("Dm"), py::arg("Bn"), py::arg("Hd"), py::arg("Wd"), py::arg("Nc"), py::arg("pad"), py::arg("cfg"),
-           py::arg("splits"), py::arg("dst"), py::arg("scale"), py::arg("stream"),
-           py::arg("adam") = std::make_tuple((uintptr_t)0, (uintptr_t)0, (uintptr_t)0, (uintptr_t)0, 0.f, 0.f, 0.f, 0.f))
-      .def("adam_rest", &Program::adam_rest)
+           py::arg("splits"), py::arg("dst"), py::arg("scale"), py::arg("stream"))
       .def("colstats", &Program::colstats)
       .def("bn_finalize", &Program::bn_finalize)
       .def("bn_coef_eval", &Program::bn_coef_eval, py::arg("name"), py::arg("C"), py::arg("gamma"), py::arg("beta"),
@@ -1167,7 +1070,6 @@ PYBIND11_MODULE(_dcgan_hip, m) {
            py::arg("b2d"), py::arg("b1g"), py::arg("b2g"), py::arg("step"), py::arg("stream"), py::arg("ls") = 0,
            py::arg("growth_interval") = 2000)
       .def("adam2", &Program::adam2)
-      .def("adam2_part", &Program::adam2_part)
       .def("nonfinite_check", &Program::nonfinite_check)
       .def("narrow_deconv", &Program::narrow_deconv)
       .def("nconv", &Program::nconv)
@@ -1177,9 +1079,6 @@ PYBIND11_MODULE(_dcgan_hip, m) {
       .def("head_bwd_rs", &Program::head_bwd_rs)
       .def("narrow_deconv_bnin", &Program::narrow_deconv_bnin)
       .def("nwgrad_ok", &Program::nwgrad_ok)
-      .def("bn_fold_ok", &Program::bn_fold_ok)
-      .def("bn_fold_fwd", &Program::bn_fold_fwd)
-      .def("bn_fold_bwd", &Program::bn_fold_bwd)
       .def("nwgrad", &Program::nwgrad, py::arg("name"), py::arg("x"), py::arg("B"), py::arg("H"), py::arg("W"),
            py::arg("Cin"), py::arg("d"), py::arg("Hd"), py::arg("Wd"), py::arg("pad"), py::arg("dst"), py::arg("stream"),
            py::arg("chunks_per_wg") = 0)

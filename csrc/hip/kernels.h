@@ -83,10 +83,6 @@ struct WGrad3Args {                 // wgrad3.hip: 25-tap gather GEMM, in-kernel
   float* ws;                           // [tiles][splits][BM*BN] fp32 slabs (splits > 1)
   unsigned* counters;                  // [tiles] arrival counters, zero between launches
   int lhw, lw;                         // log2(Hd*Wd), log2(Wd) when both are powers of two, else -1
-  // optional TF-Adam of the finished gradient in the store pass (single-process bf16 step): the
-  // parameter / slot slices of this weight in the flat ParamSet layout, the device beta powers
-  float* aw; float* am; float* av; const float* apow;
-  float alr, ab1, ab2, aeps;
 };
 
 }  // namespace dcg

@@ -626,72 +626,6 @@ __global__ __launch_bounds__(256) void adam2_kernel(Adam2Set A, Adam2Set D, floa
   }
 }
 
-// The end of the single-process bf16 step when the big weights' TF-Adam already ran inside their
-// weight-gradient kernels (wgrad3 store pass): TF-Adam over the remaining ranges of both flat
-// buffers (biases, BN parameters, the linear / head / RGB-layer weights) and, for the ranges
-// updated earlier, only the 16-bit mirror the next step's GEMMs read (their fp32 masters changed
-// while this step's GEMMs still read the old mirror). Block b works on blk[b] (a range of one
-// set, in float4 units); the last block to finish advances both beta-power pairs and the step.
-struct AdamBlk {
-  unsigned long long off4;
-  unsigned n4;
-  int set;   // 0 = A, 1 = D
-  int cast;  // 1: mirror only
-  int pad;
-};
-
-__global__ __launch_bounds__(256) void adam_rest_kernel(Adam2Set A, Adam2Set D, const AdamBlk* __restrict__ blk,
-                                                        float gscale, unsigned long long* __restrict__ step,
-                                                        unsigned* __restrict__ counter) {
-  __shared__ int flag;
-  const AdamBlk b = blk[blockIdx.x];
-  const bool inA = b.set == 0;  // block-uniform
-  f32x4* __restrict__ w = reinterpret_cast<f32x4*>(inA ? A.w : D.w);
-  elem4* __restrict__ wbf = reinterpret_cast<elem4*>(inA ? A.wbf : D.wbf);
-  if (b.cast) {
-    for (size_t i = b.off4 + threadIdx.x; i < b.off4 + b.n4; i += 256) {
-      const f32x4 wv = w[i];
-      wbf[i] = (elem4){(elem_t)wv[0], (elem_t)wv[1], (elem_t)wv[2], (elem_t)wv[3]};
-    }
-  } else {
-    const f32x4* __restrict__ g = reinterpret_cast<const f32x4*>(inA ? A.g : D.g);
-    f32x4* __restrict__ m = reinterpret_cast<f32x4*>(inA ? A.m : D.m);
-    f32x4* __restrict__ v = reinterpret_cast<f32x4*>(inA ? A.v : D.v);
-    const float* pw = inA ? A.powers : D.powers;
-    const float b1 = inA ? A.b1 : D.b1, b2 = inA ? A.b2 : D.b2, eps = inA ? A.eps : D.eps;
-    const float lr_t = (inA ? A.lr : D.lr) * sqrtf(1.f - pw[1]) / (1.f - pw[0]);
-    for (size_t i = b.off4 + threadIdx.x; i < b.off4 + b.n4; i += 256) {
-      const f32x4 gv = g[i] * gscale;
-      f32x4 mv = m[i], vv = v[i], wv = w[i];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        mv[k] = __builtin_fmaf(b1, mv[k], (1.f - b1) * gv[k]);
-        vv[k] = __builtin_fmaf(b2, vv[k], (1.f - b2) * gv[k] * gv[k]);
-        wv[k] -= lr_t * mv[k] / (sqrtf(vv[k]) + eps);
-      }
-      m[i] = mv;
-      v[i] = vv;
-      w[i] = wv;
-      wbf[i] = (elem4){(elem_t)wv[0], (elem_t)wv[1], (elem_t)wv[2], (elem_t)wv[3]};
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = old == gridDim.x - 1;
-    if (flag) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (flag && threadIdx.x == 0) {
-    A.powers[0] *= A.b1;
-    A.powers[1] *= A.b2;
-    D.powers[0] *= D.b1;
-    D.powers[1] *= D.b2;
-    if (step) step[0] += 1ull;
-  }
-}
-
 // after both Adams: beta powers *= beta (TF variable update) and the global step counter
 __global__ void step_end_kernel(float* __restrict__ pd, float* __restrict__ pg, float b1d, float b2d, float b1g,
                                 float b2g, unsigned long long* __restrict__ step, float* __restrict__ ls,
@@ -1081,18 +1015,6 @@ extern "C" int DCG_API(dcg_adam2)(float* wA, elem_t* wbfA, const float* gA, floa
   unsigned blocksD = (unsigned)std::max<size_t>(1, 512 - std::min<size_t>(511, blocksA));
   hipLaunchKernelGGL(dcg::adam2_kernel, dim3(blocksA + blocksD), dim3(256), 0, s, A, D, gscale, step, counter,
                      blocksA);
-  return (int)hipGetLastError();
-}
-
-extern "C" int DCG_API(dcg_adam_rest)(float* wA, elem_t* wbfA, const float* gA, float* mA, float* vA, float* pA,
-                                      size_t nA, float lrA, float b1A, float b2A, float epsA, float* wD,
-                                      elem_t* wbfD, const float* gD, float* mD, float* vD, float* pD, size_t nD,
-                                      float lrD, float b1D, float b2D, float epsD, const void* blocks, int nblocks,
-                                      float gscale, unsigned long long* step, unsigned* counter, hipStream_t s) {
-  const Adam2Set A{wA, wbfA, gA, mA, vA, pA, nA, lrA, b1A, b2A, epsA};
-  const Adam2Set D{wD, wbfD, gD, mD, vD, pD, nD, lrD, b1D, b2D, epsD};
-  hipLaunchKernelGGL(adam_rest_kernel, dim3(nblocks), dim3(256), 0, s, A, D, static_cast<const AdamBlk*>(blocks),
-                     gscale, step, counter);
   return (int)hipGetLastError();
 }
 

@@ -263,35 +263,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGrad3Args p) {
       for (int j = 0; j < FN; ++j) acc[i][j] = tot[i][j];
   }
 
-  // ---- scaled store into the fp32 gradient (TF layout [tap][Mc][Nc]); with p.aw, also the TF-Adam
-  //      update of those parameters (adam2_kernel's arithmetic, element by element, gscale 1)
-  if (p.aw) {
-    const float b1 = p.ab1, b2 = p.ab2, eps = p.aeps;
-    const float lr_t = p.alr * sqrtf(1.f - p.apow[1]) / (1.f - p.apow[0]);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * TN + j * 16 + li;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ml = wm * TM + i * 16 + g4 * 4 + r;
-          const int tp = TT == 1 ? tap : TT * tap + ml / MCT;
-          const int m = TT == 1 ? m0 + ml : ml % MCT;
-          if (tp < 25 && m < p.Mc && n < p.Nc) {
-            const size_t o = ((size_t)tp * p.Mc + m) * p.Nc + n;
-            const float gv = acc[i][j][r] * p.scale;
-            p.out[o] = gv;
-            const float mv = __builtin_fmaf(b1, p.am[o], (1.f - b1) * gv);
-            const float vv = __builtin_fmaf(b2, p.av[o], (1.f - b2) * gv * gv);
-            p.am[o] = mv;
-            p.av[o] = vv;
-            p.aw[o] -= lr_t * mv / (sqrtf(vv) + eps);
-          }
-        }
-      }
-    return;
-  }
+  // ---- scaled store into the fp32 gradient (TF layout [tap][Mc][Nc])
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -11,12 +11,18 @@
 // * next_batch() waits until min_after_dequeue + batch examples are pooled (RandomShuffleQueue
 //   semantics), then draws `batch` uniformly random slots and copies them into the caller's
 //   buffer outside the lock.
-// With threads == 1 the order is a deterministic function of the seed.
+// Deterministic mode (threads == 1): the single reader pushes records in a
+// seed-determined order (epoch-shuffled files, records in file order) into an arrival FIFO, and
+// every draw is taken from a window of exactly min_after_dequeue + batch examples -- the window
+// is topped up from the FIFO's front before each draw -- however far the reader has run ahead.
+// The batch sequence is then a function of the seed and the files alone. With threads > 1 the
+// draw covers every pooled example (the readers' interleaving decides arrival order anyway).
 #pragma once
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <random>
 #include <stdexcept>
@@ -92,6 +98,7 @@ class Loader {
     free_.reserve(capacity_);
     for (int i = capacity_ - 1; i >= 0; --i) free_.push_back(i);
     threads = std::max(1, threads);
+    det_ = threads == 1;
     for (int t = 0; t < threads; ++t) workers_.emplace_back([this] { work(); });
   }
 
@@ -113,11 +120,15 @@ class Loader {
   int next_batch(uint8_t* dst) {
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [this] {
-      return stop_ || !error_.empty() || (int)filled_.size() >= min_after_ + batch_ ||
-             (done_workers_ == (int)workers_.size() && !filled_.empty()) ||
-             (done_workers_ == (int)workers_.size());
+      return stop_ || !error_.empty() || pooled() >= min_after_ + batch_ || done_workers_ == (int)workers_.size();
     });
     if (!error_.empty()) throw std::runtime_error(error_);
+    if (det_) {  // the draw window: exactly min_after + batch examples, in arrival order
+      while ((int)filled_.size() < min_after_ + batch_ && !arrived_.empty()) {
+        filled_.push_back(arrived_.front());
+        arrived_.pop_front();
+      }
+    }
     // draw the batch's slots under the lock (RandomShuffleQueue semantics), copy them out with
     // the lock released (the readers keep decoding meanwhile), then hand the slots back
     // the drawn slots live in a thread-local scratch vector (no allocation per batch, and two
@@ -147,7 +158,7 @@ class Loader {
     std::lock_guard<std::mutex> g(mu_);
     LoaderStats st;
     st.records = records_.load();
-    st.pooled = (int)filled_.size();
+    st.pooled = pooled();
     st.capacity = capacity_;
     st.dequeued = dequeued_;
     st.epochs = epochs_;
@@ -155,6 +166,8 @@ class Loader {
   }
 
  private:
+  int pooled() const { return (int)(filled_.size() + arrived_.size()); }
+
   bool take_file(std::string* f) {
     std::lock_guard<std::mutex> g(mu_);
     if (next_file_ >= order_.size()) {
@@ -238,7 +251,8 @@ class Loader {
           }
           {
             std::lock_guard<std::mutex> g(mu_);
-            filled_.push_back(slot);
+            if (det_) arrived_.push_back(slot);
+            else filled_.push_back(slot);
             ++records_;
           }
           cv_.notify_all();
@@ -269,7 +283,9 @@ class Loader {
   float u8_scale_, u8_shift_;
   size_t out_bytes_ = 4;
   std::vector<uint8_t> pool_;
-  std::vector<int> free_, filled_;
+  std::vector<int> free_, filled_;  // filled_: the draw pool (deterministic mode: the window)
+  std::deque<int> arrived_;          // deterministic mode: decoded examples not yet in the window
+  bool det_ = false;
   std::vector<size_t> order_;
   size_t next_file_ = 0;
   int epochs_ = 0;

@@ -296,22 +296,8 @@ class HipEngine:
         self._keep.append(buf)
         return buf
 
-    def _wgrad_adam_wanted(self) -> bool:
-        """TF-Adam of the big conv / deconv weights inside their weight-gradient kernels (wgrad3
-        store pass) instead of in the update pass after the join: single-process bf16 "fused"
-        step only (DDP must all-reduce the gradient first; fp16 must check for overflow first).
-        The update pass then runs Adam over the remaining ranges and only re-writes the 16-bit
-        mirrors of the others. Bit-identical to the update pass, but measured 17 % SLOWER
-        (1.26 vs 1.07 ms/step: the last-arriving split-K workgroups run the whole tile's Adam
-        serially on the chains' critical path; profiles/r5/ab_wgrad_adam_r5.txt), so off unless
-        DCGAN_WGRAD_ADAM=1."""
-        return (not self.ddp and self.dt == 0 and self._schedule() == "fused"
-                and os.environ.get("DCGAN_WGRAD_ADAM", "0") == "1")
-
     def _build(self):
         self._keep: List[torch.Tensor] = []
-        self._wgrad_adam = self._wgrad_adam_wanted()
-        self._adam_fused: List[Tuple[int, int, int]] = []  # (set 0 = G / 1 = D, offset, numel)
         self.progA = self._prog()
         self.progB = self._prog()
         self.progW = self._prog()  # G's weight gradients (see _build_gloss_and_g_backward)
@@ -324,7 +310,6 @@ class HipEngine:
         # D-gradient slice final after the D chain's first segment: the top conv layer (+ its BN)
         # and the head, which the ParamSet lays out last
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
-        self._d_mid_off = self.model.d.offsets[self.dl[-2].name + "/w"][0] if len(self.dl) >= 3 else None
         self._g_cuts = self._g_bucket_cuts()
         self._g_split = self._g_split_plan()
         self._build_updates()  # (after the G split: Adam(G) follows its collectives)
@@ -333,9 +318,7 @@ class HipEngine:
             o = self._d_top_off
             nd, ng = self.grad_d.flat.numel(), self.grad_g.flat.numel()
             lo, hi = self._g_split[3:] if self._g_split is not None else (0, ng)
-            m = self._d_mid_off or 0
             for name, src, dst, a, b in (("dtop", self.grad_d, self.wire_d, o, nd), ("drest", self.grad_d, self.wire_d, 0, o),
-                                         ("dmid", self.grad_d, self.wire_d, m, o), ("drest2", self.grad_d, self.wire_d, 0, m),
                                          ("g", self.grad_g, self.wire_g, 0, ng), ("g_a", self.grad_g, self.wire_g, lo, hi),
                                          ("g_b", self.grad_g, self.wire_g, hi, ng), ("g_c", self.grad_g, self.wire_g, 0, lo)):
                 if b > a:
@@ -360,15 +343,9 @@ class HipEngine:
         second part."""
         self.progC = self._prog()
         sch = self._schedule()
-        self._adam_alt = False
-        self._adam_early = sch == "fused" and self.dt == 0 and self._adam_d_early()
-        if self._adam_early:
-            self._build_update_d_first(self.progC)  # Adam(D) on the D chain's stream, Adam(G) after the join
-        elif sch == "fused" and self.dt == 0:
-            self._adam_alt = self._adam_split_alt()
+        if sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
-            if not self._adam_alt:
-                self._c_split = self._c_split_a = self.progC.size()
+            self._c_split = self._c_split_a = self.progC.size()
         elif sch in ("concurrent", "ddp") and not self.f16:
             self._build_update_d_first(self.progC)
         else:
@@ -511,32 +488,12 @@ class HipEngine:
         P = self.model.d if name.startswith("d_") else self.model.g
         ema_m = bnstate.mean[name] if update_ema else None
         ema_v = bnstate.var[name] if update_ema else None
-        if apply and self._bn_fold(prog, ppg, groups, C, rows):
-            prog.bn_fold_fwd(name + ".fin_apply", _p(part), ppg, groups, C, float(rows // groups),
-                             _p(P[name + "/gamma"]), _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]),
-                             _p(st["rstd"]), _p(st["scale"]), _p(st["shift"]), _p(ema_m), _p(ema_v),
-                             cfgm.bn_momentum, _p(x), _p(y), rows, act, cfgm.lrelu_leak, 0)
-            return
         prog.bn_finalize(name + ".fin", _p(part), ppg, groups, C, float(rows // groups), _p(P[name + "/gamma"]),
                          _p(P[name + "/beta"]), cfgm.bn_eps, _p(st["mean"]), _p(st["rstd"]), _p(st["scale"]),
                          _p(st["shift"]), _p(ema_m), _p(ema_v), cfgm.bn_momentum, 0)
         if apply:
             prog.bn_apply_act(name + ".apply", _p(x), _p(y), _p(st["scale"]), _p(st["shift"]), rows, C,
                               rows // groups, act, cfgm.lrelu_leak, 0)
-
-    def _bn_fold(self, prog, ppg: int, groups: int, C: int, rows: int) -> bool:
-        """BN finalize folded into the apply launch (bnfold.hip) when a group has at most
-        DCGAN_BN_FOLD partial rows (0 = never, the default): every apply workgroup then reduces its
-        own channels' partial rows. Bit-identical, but measured slower: 64x64 step 113.7k-114.8k
-        img/s with the 8 layers of <= 64 rows folded (61 launches), 96.1k-96.7k with all 13 of
-        <= 256 (55 launches), vs 120.0k-120.7k unfolded; with the cheaper 16-lane-group reduction
-        116.1k-116.8k / 113.0k-113.5k vs 118.7k-120.5k (profiles/r5/ab_bn_fold_r5.txt): each fused
-        launch still runs the whole dependent chain (partials -> fp64 sums -> coefficients ->
-        apply) in every workgroup, and the kernel boundary it removes costs ~1 us."""
-        v = os.environ.get("DCGAN_BN_FOLD", "0")
-        if not v.isdigit():
-            raise ValueError("DCGAN_BN_FOLD must be a non-negative integer, got %r" % v)
-        return 0 < ppg <= min(int(v), 256) and rows % groups == 0 and prog.bn_fold_ok(ppg, groups, C, rows // groups)
 
     @staticmethod
     def _rows_per_block(rows_per_group: int, C: int) -> int:
@@ -685,7 +642,6 @@ class HipEngine:
         last = self.dl[-1]
         fused_next = self._head_bwd(prog, "d_head.bwd", self.d_a[last.name], self.dl_d, self.d_da[last.name],
                                     gD[lin + "/Matrix"], gD[lin + "/bias"], B2, last, 2, 0)
-        wside = self._dws = self._d_wgrad_side()
         # fused_next: BN-backward partials emitted by the layer above (head / dgrad GEMM store pass)
         for i in range(len(self.dl) - 1, -1, -1):
             L = self.dl[i]
@@ -706,11 +662,6 @@ class HipEngine:
                 src = self.d_in if i == 0 else self.d_a[self.dl[i - 1].name]
                 pad = same_pads(L.in_hw)[0]
                 ws = 0
-                if wside:  # (study) on the D chain's slot-1 stream once dx exists
-                    ev = prog.new_event()
-                    prog.record(ev, 0)
-                    prog.wait(ev, 1)
-                    ws = 1
                 if i == 0 and self._d0_direct() and prog.nwgrad_ok(L.in_hw, L.in_hw, L.out_hw, L.out_hw):
                     # image window staged per workgroup, no column matrix (narrow2.hip nwgrad)
                     prog.nwgrad(L.name + ".nwgrad", _p(self.d_in), B2, L.in_hw, L.in_hw, L.cin, _p(dx), L.out_hw,
@@ -723,13 +674,11 @@ class HipEngine:
                                 gD[L.name + "/w"], stream=ws)
                 else:
                     self._wgrad(prog, L.name, 0, src, L.in_hw, L.in_hw, L.cin, dx, B2, L.out_hw, L.out_hw, L.cout, pad,
-                                gD[L.name + "/w"], stream=ws, adam_of=("d", L.name + "/w"))
+                                gD[L.name + "/w"], stream=ws)
                 if i == len(self.dl) - 1:
                     # head + top layer gradients final: DDP splits the segment here so their
                     # all-reduce (76 % of D's bytes at 64x64) overlaps the rest of D's backward
                     self._b_split = prog.size()
-                if i == len(self.dl) - 2:
-                    self._b_split2 = prog.size()  # the next layer down final too (_ddp_dmid)
 
             def emit_dgrad(i=i, L=L, dx=dx):
                 fused = None
@@ -757,10 +706,6 @@ class HipEngine:
             # profiles/r2/ab_d_dgrad_first_r2.txt)
             emit_wgrad()
             fused_next = emit_dgrad()
-        if wside:  # join the weight gradients back into the D chain's stream
-            ev = prog.new_event()
-            prog.record(ev, 1)
-            prog.wait(ev, 0)
 
     def _g_bucket_cuts(self) -> List[Tuple[int, int, int]]:
         """G's gradient buckets for the "ddp" schedule: (progW piece index, lo, hi) -- after G's
@@ -855,26 +800,16 @@ class HipEngine:
             prog.colsum_small(name, _p(x), rows, C, _p(sp), blocks, 0)
             prog.sum_partials(name + ".sum", _p(sp), blocks, C, C, _p(dst), 0)
 
-    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst, stream=0, adam_of=None):
-        """adam_of = ("g" | "d", tensor name): with _wgrad_adam, the wgrad3 store pass also runs
-        that weight's TF-Adam (see _wgrad_adam_wanted)."""
+    def _wgrad(self, prog, name, mode, G, Hg, Wg, Mc, Dm, Bn, Hd, Wd, Nc, pad, dst, stream=0):
+        """Weight gradient dst [25][Mc][Nc] (fp32): wgrad3 / wgrad5 (16-bit, 25-tap layers, split-K
+        reduced on the device, deterministic), else the first-generation slab kernel + reduce."""
         K = Bn * Hd * Wd
         taps = 1 if mode == 2 else 25
         if mode == 0 and not self.f32:  # 25-tap layers: LDS-DMA pipelined kernel, split-K reduced in-kernel
             plan = H.wgrad3_cfg_for(Mc, Nc, Bn, Hd, Wd, Hg)
             if plan is not None:
-                adam = (0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0)
-                if self._wgrad_adam and adam_of is not None and plan[0] < 400:  # (wgrad5: no fused Adam)
-                    which, tname = adam_of
-                    ps, opt = (self.model.g, self.opt_g) if which == "g" else (self.model.d, self.opt_d)
-                    off, shape = ps.offsets[tname]
-                    assert dst.data_ptr() == self.grad_g.flat.data_ptr() + 4 * off if which == "g" else \
-                        dst.data_ptr() == self.grad_d.flat.data_ptr() + 4 * off
-                    adam = (_p(ps.flat) + 4 * off, _p(opt.m.flat) + 4 * off, _p(opt.v.flat) + 4 * off, _p(opt.powers),
-                            opt.lr, opt.beta1, opt.beta2, opt.eps)
-                    self._adam_fused.append((0 if which == "g" else 1, off, dst.numel()))
                 prog.wgrad3(name + ".wgrad", _p(G), Hg, Wg, Mc, _p(Dm), Bn, Hd, Wd, Nc, pad, plan[0], plan[1],
-                            _p(dst), 1.0, stream, adam)
+                            _p(dst), 1.0, stream)
                 return
         cfg, splits = H.pick_wgrad(Mc, Nc, K, taps, dtype=self.dt)
         if mode == 0 and not self.f32:
@@ -905,11 +840,6 @@ class HipEngine:
                           self.cfg.lrelu_leak, rows, C, rpb, rpg, _p(part), 0)
         dg = grads[name + "/gamma"] if write_param_grads else None
         db = grads[name + "/beta"] if write_param_grads else None
-        if self._bn_fold(prog, Pn // groups, groups, C, rows):
-            prog.bn_fold_bwd(name + ".bwd_fin_apply", _p(part), Pn // groups, groups, C, float(rpg),
-                             _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), _p(dy), _p(y),
-                             _p(x), _p(dx), rows, act, self.cfg.lrelu_leak, 0)
-            return
         prog.bn_bwd_finalize(name + ".bwd_fin", _p(part), Pn // groups, groups, C, float(rpg),
                              _p(P[name + "/gamma"]), _p(mean), _p(rstd), _p(dg), _p(db), _p(coef), 0)
         prog.bn_bwd_apply(name + ".bwd_apply", _p(dy), _p(y), _p(x), _p(coef), _p(dx), rows, C, rpg, act,
@@ -1040,7 +970,7 @@ class HipEngine:
             pad = same_pads(L.out_hw)[0]
             w0 = progw.size()
             self._wgrad(progw, L.name, 0, dx, L.out_hw, L.out_hw, L.cout, src, B, L.in_hw, L.in_hw, L.cin, pad,
-                        gG[L.name + "/w"], adam_of=("g", L.name + "/w"))
+                        gG[L.name + "/w"])
             self._w_mark(prog, progw, w0, L.name)
             r = self._dgrad_bnb(prog, 0, B, L.out_hw, L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, True, bsrc, xsrc,
                                 src, 1, RELU)
@@ -1089,64 +1019,13 @@ class HipEngine:
 
     def _build_update_fused(self, prog):
         """Single-process bf16: both TF-Adams + the beta-power / global-step update in one launch
-        (adam2_kernel), G's buffer first -- the same arithmetic as the separate kernels. When the
-        big weights' Adam already ran in their wgrad3 kernels (_wgrad_adam): adam_rest_kernel --
-        Adam over the other ranges, the 16-bit mirror re-written for those weights."""
+        (adam2_kernel), G's buffer first -- the same arithmetic as the separate kernels."""
         od, og = self.opt_d, self.opt_g
         G, Dm = self.model.g, self.model.d
-        if self._adam_fused:
-            ranges = []
-            for st, ps in ((0, G), (1, Dm)):
-                done = sorted((off, -(-n // 4) * 4) for s_, off, n in self._adam_fused if s_ == st)
-                pos = 0
-                for off, n in done:
-                    if off > pos:
-                        ranges.append((st, 0, pos, off - pos))
-                    ranges.append((st, 1, off, n))
-                    pos = off + n
-                if ps.flat.numel() > pos:
-                    ranges.append((st, 0, pos, ps.flat.numel() - pos))
-            prog.adam_rest("adam_rest", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
-                           _p(og.v.flat), _p(og.powers), G.flat.numel(), og.lr, og.beta1, og.beta2, og.eps,
-                           _p(Dm.flat), _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat),
-                           _p(od.powers), Dm.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, ranges, 1.0 / self.world,
-                           _p(self.step_counter), 0)
-            return
-        if self._adam_alt:
-            # part 1 (progC[:_c_split], on the G weight gradients' stream once the D chain is done):
-            # Adam over D and over G from g_h2's weights on -- nothing the G chain still reads after
-            # its last weight-gradient mark; part 2 (after the join): G's projection, g_bn0 and
-            # g_h1's slice + the beta powers and the step
-            hi = self.model.g.offsets[self.gl[1].name + "/w"][0]
-            es = self.wbf_g.flat.element_size()
-            prog.adam2_part("adam_gd_a", _p(G.flat) + 4 * hi, _p(self.wbf_g.flat) + es * hi,
-                            _p(self.grad_g.flat) + 4 * hi, _p(og.m.flat) + 4 * hi, _p(og.v.flat) + 4 * hi,
-                            _p(og.powers), G.flat.numel() - hi, og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat),
-                            _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers),
-                            Dm.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, 1.0 / self.world, 0)
-            self._c_split = self._c_split_a = prog.size()
-            prog.adam2("adam_g_b", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
-                       _p(og.v.flat), _p(og.powers), hi, og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat),
-                       _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers), 0,
-                       od.lr, od.beta1, od.beta2, od.eps, 1.0 / self.world, _p(self.step_counter), 0)
-            return
         prog.adam2("adam_gd", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat), _p(og.v.flat),
                    _p(og.powers), G.flat.numel(), og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat), _p(self.wbf_d.flat),
                    _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers), Dm.flat.numel(), od.lr,
                    od.beta1, od.beta2, od.eps, 1.0 / self.world, _p(self.step_counter), 0)
-
-    def _adam_split_alt(self) -> bool:
-        """DCGAN_ADAM_SPLIT_ALT=1 (fused single-process bf16 step whose G weight gradients all run
-        on one idle stream, _gw_place() "aaaa" / "ssss"): the part of the two-model Adam that the G
-        chain's tail cannot touch runs on that stream beside the tail (see _build_update_fused).
-        Bit-identical, but 1.1-2.0 % slower at 64x64 (3/3 rounds) and 0.5-0.8 % at 128x128: like
-        every Adam beside the chains before it (profiles/r5/ab_adam_split_alt_r5.txt). Off."""
-        if os.environ.get("DCGAN_ADAM_SPLIT_ALT", "0") != "1" or self._adam_fused or len(self.gl) < 2:
-            return False
-        if not self._g_wgrad_on_d_stream() or not self._g_w or self._g_w_layer[-1] != self.gl[0].name:
-            return False
-        place = self._gw_place()
-        return len(set(place)) == 1 and place[0] in "as"
 
     def _repack_weights_now(self):
         if self.progCast.size():
@@ -1276,10 +1155,7 @@ class HipEngine:
         if self._graphs or self._step_host:
             raise RuntimeError("enable_timing() must precede the first train_step")
         self._timing = True
-        if self._wgrad_adam:  # the recorded wgrad kernels run Adam: re-record the step without it
-            self._build()
-        else:
-            self._build_updates()
+        self._build_updates()
         self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self._segments()) + 1)]
 
     def phase_times(self) -> Dict[str, float]:
@@ -1311,20 +1187,16 @@ class HipEngine:
         gives (default: the idle alt1 stream, each as soon as its operand exists)."""
         ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
         ex.wait(ex.alt[0], cs)
-        # host issue order (eager replay): the first DCGAN_G_FIRST ops of the G chain go out before
-        # the D chain's, so they sit first in the forward's queue
-        g_first = min(self._a_fwd + self._g_first(), self._g_w[0][0] if self._g_w else self.progA.size())
-        ex.run(self.progA, [cs, ex.side], self._a_fwd, g_first)
-        ex.run(self.progB, [ex.alt[0], ex.side] if self._dws else ex.alt)
+        ex.run(self.progB, ex.alt)
         # the G chain: data gradients on cs; each G weight gradient on its _gw_place() stream once
         # cs has produced its operand (a mark after that progA position)
         if not self._g_wgrad_on_d_stream():  # every G gradient on cs
-            ex.run(self.progA, [cs, ex.side], g_first, -1)
+            ex.run(self.progA, [cs, ex.side], self._a_fwd, -1)
             ex.run(self.progW, [cs, ex.side])
             ex.wait(cs, ex.alt[0])
             ex.run(self.progC, [cs, ex.side])
             return
-        pos, marks = g_first, []
+        pos, marks = self._a_fwd, []
         for a_end, _ in self._g_w:
             ex.run(self.progA, [cs, ex.side], pos, a_end)
             marks.append(ex.mark(cs))
@@ -1340,38 +1212,21 @@ class HipEngine:
                 ex.wait_mark(st[0], m)
                 ex.run(self.progW, st, w, w_end)
             w = w_end
-        if self._adam_alt:
-            # Adam part 1 on the weight gradients' stream once the D chain is done (_adam_split_alt)
-            st = streams[place[-1]][0]
-            assert set(place) == {place[-1]}
-            ex.wait(st, ex.alt[0])
-            ex.run(self.progC, [st], 0, self._c_split)
-            ex.wait(cs, st)
-            ex.run(self.progC, [cs, ex.side], self._c_split, -1)
-            return
         for q in sorted(set(place) & {"s", "a"}):
             ex.wait(cs, streams[q][0])
-        if self._adam_early:
-            # Adam(D) on the D chain's stream once the g_loss chain has left D (the first G-wgrad
-            # mark follows it), beside the G chain's tail; Adam(G) + the step counter after the join
-            assert self._g_w[0][0] >= self._a_gd_end
-            ex.wait_mark(ex.alt[0], marks[0])
-            ex.run(self.progC, ex.alt, 0, self._c_split)
         # the G weight gradients placed on cs run after the G chain (their operands are produced
-        # there): the D chain's stream no longer runs them serially after everything else
+        # there)
         for q, lo, hi in segs:
             if q == "c":
                 ex.run(self.progW, [cs, ex.side], lo, hi)
         ex.wait(cs, ex.alt[0])
-        ex.run(self.progC, [cs, ex.side], self._c_split if self._adam_early else 0, -1)
+        ex.run(self.progC, [cs, ex.side])
 
     def _gw_place(self) -> str:
         """Stream of each G weight-gradient segment (progW between consecutive _g_w ends) in the
-        fused step: "d" behind the D chain on its stream, "c" on the G chain's stream after that
-        chain, "s" / "a" on the idle side / alt1 stream as soon as its operand exists (beside both
-        chains). DCGAN_GW_PLACE gives the string (one letter per segment); otherwise
-        DCGAN_GW_STREAM (d / side / alt1, default alt1) for all but the last
-        DCGAN_GW_TAIL_ON_MAIN (default 0) segments, which are "c".
+        fused step: "a" (default) on the idle alt1 stream as soon as its operand exists (beside
+        both chains), "s" the idle side stream, "d" behind the D chain on its stream, "c" on the G
+        chain's stream after that chain. DCGAN_GW_PLACE gives the string (one letter per segment).
 
         64x64 bf16, 3 interleaved rounds (profiles/r5/ab_gw_place_r5.txt): "aaaa" 123.7k-124.0k,
         "ssss" 123.4k-123.8k, "sssc" 123.0k-123.3k, "sasa" 122.6k-123.0k, "ssdd" 121.7k-122.6k
@@ -1379,44 +1234,11 @@ class HipEngine:
         the G chain, so weight gradients queued behind it all land after both chains)."""
         n = len(self._g_w)
         v = os.environ.get("DCGAN_GW_PLACE")
-        if v is not None:
-            if len(v) != n or set(v) - set("dcsa"):
-                raise ValueError("DCGAN_GW_PLACE must be %d letters of d/c/s/a, got %r" % (n, v))
-        else:
-            g = os.environ.get("DCGAN_GW_STREAM", "d" if self._adam_early else "alt1")
-            if g not in ("d", "side", "alt1"):
-                raise ValueError("DCGAN_GW_STREAM must be d, side or alt1, got %r" % g)
-            n_main = min(self._gw_tail_on_main(), n)
-            v = {"d": "d", "side": "s", "alt1": "a"}[g] * (n - n_main) + "c" * n_main
-        if self._adam_early and ("s" in v or "a" in v):
-            raise ValueError("DCGAN_ADAM_D_EARLY needs the G weight gradients on the d / c streams")
+        if v is None:
+            return "a" * n
+        if len(v) != n or set(v) - set("dcsa"):
+            raise ValueError("DCGAN_GW_PLACE must be %d letters of d/c/s/a, got %r" % (n, v))
         return v
-
-    def _adam_d_early(self) -> bool:
-        """DCGAN_ADAM_D_EARLY=1 (fused single-process bf16 step, G weight gradients behind the D
-        chain): Adam(D) on the D chain's stream after that stream's last weight gradient, beside
-        the G chain's tail, instead of inside the one two-model Adam after the join. Bit-identical;
-        measured 0.1-1.0 % slower (4/4 pairs, profiles/r5/ab_adam_d_early_r5.txt), so off."""
-        return (os.environ.get("DCGAN_ADAM_D_EARLY", "0") == "1" and self._sched_req in (None, "fused")
-                and not self.ddp and self._g_wgrad_on_d_stream() and not self._wgrad_adam_wanted())
-
-    def _g_first(self) -> int:
-        """DCGAN_G_FIRST=k: issue the G chain's first k ops before the D chain's (study switch)."""
-        v = os.environ.get("DCGAN_G_FIRST", "0")
-        if not v.isdigit():
-            raise ValueError("DCGAN_G_FIRST must be a non-negative integer, got %r" % v)
-        return int(v)
-
-    def _gw_tail_on_main(self) -> int:
-        """Number of trailing G weight-gradient segments the fused step runs on the G chain's
-        stream after that chain (DCGAN_GW_TAIL_ON_MAIN, default 0; see _gw_place). Round 4, with
-        the others behind the D chain: 0 / 1 / 2 / 3 / 4 -> 114.0k / 115.2k / 116.1k-118.1k /
-        116.6k / 115.2k img/s (profiles/r4/ab_gw_tail_on_main_r4.txt); round 5, with the others
-        on the idle alt1 stream, 0 is best (profiles/r5/ab_gw_stream_r5.txt)."""
-        v = os.environ.get("DCGAN_GW_TAIL_ON_MAIN", "0")
-        if not v.isdigit():
-            raise ValueError("DCGAN_GW_TAIL_ON_MAIN must be a non-negative integer, got %r" % v)
-        return int(v)
 
     def _run_ddp(self, ex, cs):
         """The "ddp" schedule: the fused step with the gradient all-reduces on the comm stream,
@@ -1470,46 +1292,19 @@ class HipEngine:
         _, run, which = self._segments()[i]
         run(ex, stream, ex.side if which == self.MAIN else ex.alt[1])
 
-    def _d_wgrad_side(self) -> bool:
-        """DCGAN_D_WGRAD_SIDE=1 (study; fused single-process step): D's weight gradients on a
-        stream of their own (progB slot 1 = the idle side stream), each after its dx exists,
-        joined back at the D chain's end; the D chain keeps only the data gradients."""
-        return (os.environ.get("DCGAN_D_WGRAD_SIDE", "0") == "1" and not self.ddp and not self._timing
-                and self._sched_req in (None, "fused"))
+    def _ddp_gw_alt(self) -> bool:
+        """Segmented DDP step, eager replay: the G weight gradients other than g_h1's run on the idle
+        alt1 stream as soon as their operands exist (instead of after the G chain on cs), and G's
+        slice above g_h1 goes on the wire from there. Measured (profiles/r5/ab_ddp_gw_alt_b_r5.txt):
+        W=1 one-rank RCCL 117.7k vs 111.9k-112.3k img/s; RCCL-like stand-in at W=8, 150 GB/s:
+        1.309-1.316 vs 1.336-1.341 ms (fp32 wire), 1.199-1.202 vs 1.242-1.245 (bf16). Putting g_h1's
+        weight gradient there too was faster at W=1 but slower at W = 2, 4 and 8
+        (ab_ddp_gw_world_r5.txt). Graph-replayed segments keep round 4's layout."""
+        return not self.graph_enabled and self._g_split is not None
 
-    def _ddp_dmid_wanted(self) -> bool:
-        """DCGAN_DDP_DMID=1 (segmented DDP step, eager replay): D's gradient in three collectives
-        -- top layer + head, the next layer down as soon as its weight gradient lands (issued
-        before G's on the comm stream), the rest at the D chain's end -- instead of two."""
-        return (os.environ.get("DCGAN_DDP_DMID", "0") == "1" and self._schedule() == "concurrent"
-                and self._d_mid_off is not None and getattr(self, "_b_split2", 0) > self._b_split)
-
-    def _ddp_dmid(self) -> bool:
-        if self.graph_enabled:
-            return False
-        return getattr(self, "_dmid", False) if self.ddp else self._ddp_dmid_wanted()
-
-    def _ddp_gw_alt(self) -> int:
-        """DCGAN_DDP_GW_ALT (segmented DDP step, eager replay): 1 (default) = the G weight
-        gradients other than g_h1's run on the idle alt1 stream as soon as their operands exist
-        instead of after the G chain on cs, and G's slice above g_h1 goes on the wire from there;
-        2 = g_h1's as well (its collective then waits for alt1); 3 = g_h1's on the idle side
-        stream at its operand's mark; 0 = round 4's segments.
-        Measured (profiles/r5/ab_ddp_gw_alt_b_r5.txt): W=1 one-rank RCCL 117.7k vs 111.9k-112.3k
-        img/s (2: 118.7k-120.0k); RCCL-like stand-in at W=8, 150 GB/s: 1.309-1.316 vs 1.336-1.341
-        ms (fp32 wire), 1.199-1.202 vs 1.242-1.245 (bf16), while 2 is slower there (1.359-1.361,
-        1.241-1.244). Graph-replayed segments keep round 4's layout."""
-        v = os.environ.get("DCGAN_DDP_GW_ALT", "1")
-        if v not in ("0", "1", "2", "3"):
-            raise ValueError("DCGAN_DDP_GW_ALT must be 0, 1, 2 or 3, got %r" % v)
-        if self.graph_enabled or self._g_split is None:
-            return 0
-        return int(v)
-
-    def _g_chain_gw_alt(self, ex, cs, mode: int):
+    def _g_chain_gw_alt(self, ex, cs):
         """Segment "G_chain" with G's weight gradients on alt1 (_ddp_gw_alt), and the collective of
-        G's slice above g_h1 as soon as they are done. Returns the stream g_h1's gradient slice is
-        final on."""
+        G's slice above g_h1 as soon as they are done."""
         A, W, a1 = self.progA, self.progW, ex.alt[1]
         a_need, wb, we = self._g_split[:3]
         pos, w = self._a_fwd, 0
@@ -1527,32 +1322,24 @@ class HipEngine:
         self._wire_cast(ex, "g_b", [a1])
         self._ar_launch(ex, "gsplit_b", a1)
         ex.run(A, [cs, ex.side], pos, a_need)
-        st, sl = cs, [cs, ex.side]
-        if mode in (2, 3):
-            st = a1 if mode == 2 else ex.side
-            ex.wait(st, cs)
-            sl = [st]
-        ex.run(W, sl, wb, we)
-        self._wire_cast(ex, "g_a", sl)
-        return st
+        ex.run(W, [cs, ex.side], wb, we)
+        self._wire_cast(ex, "g_a", [cs, ex.side])
 
-    def _g_tail_gw_alt(self, ex, cs, mode: int) -> None:
+    def _g_tail_gw_alt(self, ex, cs) -> None:
         """Segment "G_tail" when G's weight gradients ran on alt1: the rest of the G chain, then
-        the join with alt1 (and side, mode 3) before G's remaining slices are cast / reduced."""
+        the join with alt1 before G's remaining slices are cast / reduced."""
         we = self._g_split[2]
         ex.run(self.progA, [cs, ex.side], self._g_split[0], -1)
         ex.run(self.progW, [cs, ex.side], we, -1)
         ex.wait(cs, ex.alt[1])
-        if mode == 3:
-            ex.wait(cs, ex.side)
         self._wire_cast(ex, "g_c", [cs, ex.side])
 
     def _ar_launch(self, ex, which: str, src) -> None:
         """All-reduce one gradient slice ("g", "dtop", "drest", "gsplit_a/b/c") on the comm stream
         once `src`'s queued work is done."""
         if self.ddp:
-            r = getattr(self, "_ar_" + which, None)
-            if r is None:
+            r = getattr(self, "_ar_" + which)  # AttributeError: a collective _ensure_comm never built
+            if r is None:                       # (an intentionally empty slice)
                 return
             ex.wait(ex.comm, src)
             ex.collective(r, ex.comm)
@@ -1582,37 +1369,25 @@ class HipEngine:
             self._seg(ex, 1, alt)              # D chain: head + top layer gradients
             self._tick(2, alt)
             self._ar_launch(ex, "dtop", alt)
-            dmid = self._ddp_dmid()
-            if dmid:
-                # D's next layer down: its slice goes out right after D's top layer on the comm
-                # stream (issue order = comm order), into the gap before G's first collective
-                ex.run(self.progB, ex.alt, self._b_split, self._b_split2)
-                self._wire_cast(ex, "dmid", ex.alt)
-                self._ar_launch(ex, "dmid", alt)
             gw = self._ddp_gw_alt()
             if gw:                             # the same segments with G's weight gradients on alt1
-                a_src = self._g_chain_gw_alt(ex, cs, gw)
+                self._g_chain_gw_alt(ex, cs)
             else:
                 self._seg(ex, 2, cs)           # G chain: g_loss through D(fake), G backward to g_h1's wgrad
-                a_src = cs
             self._tick(3, cs)
             a_done = None
             if self._g_split is not None:
-                self._ar_launch(ex, "gsplit_a", a_src)  # g_h1's slice, under the rest of both chains
+                self._ar_launch(ex, "gsplit_a", cs)  # g_h1's slice, under the rest of both chains
                 a_done = ex.mark(ex.comm) if self.ddp else None
-            if dmid:
-                ex.run(self.progB, ex.alt, self._b_split2, -1)
-                self._wire_cast(ex, "drest2", ex.alt)
-            else:
-                self._seg(ex, 3, alt)          # D chain: rest of D's backward -> grad_d final
+            self._seg(ex, 3, alt)              # D chain: rest of D's backward -> grad_d final
             self._tick(4, alt)
             if gw:
-                self._g_tail_gw_alt(ex, cs, gw)
+                self._g_tail_gw_alt(ex, cs)
             else:
                 self._seg(ex, 4, cs)           # G tail: g_h1 dgrad, g_bn0, projection, other G wgrads
             self._tick(5, cs)
             # D's last bucket, then the rest of G's; Adam(D) runs while G's is in flight
-            self._ar_launch(ex, "drest2" if dmid else "drest", alt)
+            self._ar_launch(ex, "drest", alt)
             d_done = ex.mark(ex.comm) if self.ddp else None
             if self._g_split is not None:
                 if not gw:                     # (else issued from alt1 inside the G chain)
@@ -1682,11 +1457,6 @@ class HipEngine:
             self._ar_dtop = mk(df[o:], wdf[o:] if direct else None)
             sch = self._schedule()
             self._ar_drest = mk(df[:o], wdf[:o] if direct else None)  # (also for graph-replayed segments)
-            self._dmid = self._ddp_dmid_wanted()
-            if self._dmid:  # D's second-highest layer on the wire once its gradient is final
-                m = self._d_mid_off
-                self._ar_dmid = mk(df[m:o], wdf[m:o] if direct else None)
-                self._ar_drest2 = mk(df[:m], wdf[:m] if direct else None)
             if sch == "serial" or (sch == "concurrent" and self._g_split is None):
                 self._ar_g = mk(gf, wgf if direct else None)
             elif sch == "concurrent":  # g_h1's slice first, then the two others

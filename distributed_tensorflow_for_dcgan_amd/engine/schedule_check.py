@@ -176,7 +176,7 @@ def check(cfg=None, batch_size: int = 8, dtype: str = "bf16", world: int = 1, sc
                     graph=False, allreduce_dtype=allreduce_dtype)
     if timing:  # (enable_timing without its CUDA events)
         eng._timing = True
-        eng._build() if eng._wgrad_adam else eng._build_updates()
+        eng._build_updates()
     hz, n = check_engine(eng, steps)
     return eng._schedule(), hz, n
 

@@ -115,14 +115,19 @@ def native_comm(device: torch.device):
 
 
 def shutdown() -> None:
+    """Tear down the native communicator and the process group this module created. Every
+    collective the engines issued (captured or eager) must have completed before the
+    communicator is freed: the device is synchronised first, and an engine built on it must not
+    be stepped afterwards (its recorded Programs / graphs still name the freed ncclComm)."""
     global _PG_INITIALISED_HERE, _NATIVE
     if _NATIVE is not None:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         _NATIVE.destroy()
         _NATIVE = None
     if is_initialized() and _PG_INITIALISED_HERE:
         dist.destroy_process_group()
         _PG_INITIALISED_HERE = False
-_NATIVE = None  # native RCCL communicator over the default group's ranks (native_comm)
 
 
 def barrier() -> None:

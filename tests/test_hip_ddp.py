@@ -272,10 +272,7 @@ def test_bench_direct_two_ranks_self_launch(tmp_path):
     assert res["config"]["backend"] == "gloo" and res["value"] > 0
 
 
-def _rccl_worker(out_dir, graph, port, schedule, gw_alt="0"):
-    gw_alt, _, dmid = gw_alt.partition("+")
-    os.environ["DCGAN_DDP_GW_ALT"] = gw_alt
-    os.environ["DCGAN_DDP_DMID"] = "1" if dmid == "dmid" else "0"
+def _rccl_worker(out_dir, graph, port, schedule):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["DCGAN_FORCE_DDP"] = "1"
@@ -287,27 +284,23 @@ def _rccl_worker(out_dir, graph, port, schedule, gw_alt="0"):
     D.init_distributed(1, 0, torch.device("cuda", 0))
     eng = _make(1, 0, graph)
     assert eng.ddp and eng._schedule() == schedule
-    assert eng._ddp_gw_alt() == (int(gw_alt) if schedule == "concurrent" and not graph else 0)
+    assert eng._ddp_gw_alt() == (schedule == "concurrent" and not graph)
     d, g, step = _run(eng)
-    assert eng._ddp_dmid() == (dmid == "dmid")
     torch.save({"d": d, "g": g, "step": step, "backend": tdist.get_backend(), "world": tdist.get_world_size(),
                 "graph": eng.graph_enabled, "graphs": len(eng._graphs)}, os.path.join(out_dir, "rccl.pt"))
     D.barrier()
     D.shutdown()
 
 
-@pytest.mark.parametrize("graph,schedule,gw_alt", [(False, "ddp", "0"), (True, "ddp", "0"), (True, "concurrent", "0"),
-                                                   (False, "concurrent", "0"), (False, "concurrent", "1"),
-                                                   (False, "concurrent", "2"), (False, "concurrent", "3"),
-                                                   (False, "concurrent", "1+dmid")])
-def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule, gw_alt):
+@pytest.mark.parametrize("graph,schedule", [(False, "ddp"), (True, "ddp"), (True, "concurrent"), (False, "concurrent")])
+def test_rccl_single_rank_ddp_matches_fused(tmp_path, graph, schedule):
     """The REAL collective path on a one-GPU box: a one-rank RCCL (backend "nccl") process group
     (DCGAN_FORCE_DDP=1). "ddp": the RCCL all-reduces captured INSIDE the step's single hipGraph
     (per-layer G buckets); "concurrent": issued on the comm stream between 8 segments (graphs or
-    eager replay; eager: G's weight gradients on alt1 with DCGAN_DDP_GW_ALT=1/2). All
+    eager replay; eager: G's weight gradients on alt1). All
     bit-identical to the fused single-graph step."""
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port(), schedule, gw_alt))
+    p = ctx.Process(target=_rccl_worker, args=(str(tmp_path), graph, _free_port(), schedule))
     p.start()
     p.join(timeout=600)
     assert p.exitcode == 0, "RCCL rank exited with %s" % p.exitcode

@@ -74,13 +74,11 @@ def _lrelu_d(a):
 def test_engine_stagewise(size, c_dim, B, dtype, monkeypatch):
     """fp16 runs with the dynamic loss scale in the gradient seeds: every stage is compared
     against a recomputation from the engine's own (scaled) inputs, so the scale cancels.
-    Programs A / B / W hold no optimiser op here (the wgrad-fused Adam is off: it would update the
-    weights the oracle reads; test_wgrad_fused_adam_matches_the_update_pass covers it): the G
-    stages are recomputed from the pre-update G weights. fp32 (the reference precision) is held
+    Programs A / B / W hold no optimiser op: the G stages are recomputed from the pre-update G
+    weights. fp32 (the reference precision) is held
     to 1e-4 per stage."""
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     from distributed_tensorflow_for_dcgan_amd.ops import hip as H
-    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
     dev = torch.device("cuda", 0)
     cfg = DCGANConfig(output_size=size, c_dim=c_dim)
     eng = HipEngine(cfg, B, dev, graph=False, seed=3, dtype=dtype)
@@ -430,92 +428,30 @@ def test_engine_sampler_zero_debias():
     assert rel(s, s_ref) < rel(s, ref_nodebias.sampler(z))
 
 
-def test_wgrad_fused_adam_matches_the_update_pass(monkeypatch):
-    """Single-process bf16: TF-Adam of the six conv / deconv weights inside their wgrad3 store pass
-    (+ adam_rest over the remaining ranges and the mirrors) gives bit for bit the weights, Adam
-    slots, beta powers and losses of the one-launch update pass after the join (DCGAN_WGRAD_ADAM=0),
-    over 5 steps (graph replay)."""
-    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
-    dev = torch.device("cuda", 0)
-    cfg = DCGANConfig()
-    B = 16
-    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(2)) * 2 - 1).to(dev)
-    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "1")
-    e1 = HipEngine(cfg, B, dev, graph=True, seed=2)
-    monkeypatch.setenv("DCGAN_WGRAD_ADAM", "0")
-    e2 = HipEngine(cfg, B, dev, graph=True, seed=2)
-    assert e1._wgrad_adam and not e2._wgrad_adam
-    e1.set_batch(real)
-    e2.set_batch(real)
-    for _ in range(5):
-        e1.train_step()
-        e2.train_step()
-    torch.cuda.synchronize()
-    for a, b in ((e1.model.g.flat, e2.model.g.flat), (e1.model.d.flat, e2.model.d.flat),
-                 (e1.wbf_g.flat, e2.wbf_g.flat), (e1.opt_g.m.flat, e2.opt_g.m.flat), (e1.opt_d.v.flat, e2.opt_d.v.flat),
-                 (e1.opt_g.powers, e2.opt_g.powers), (e1.opt_d.powers, e2.opt_d.powers)):
-        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
-    assert e1.last_losses() == e2.last_losses() and e1.global_step == e2.global_step == 5
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("dtype,B", [("bf16", 128), ("bf16", 16), ("fp32", 32)])
-def test_bn_fold_is_bit_identical_to_finalize_then_apply(monkeypatch, dtype, B):
-    """BN finalize folded into the apply launch (bnfold.hip, DCGAN_BN_FOLD=256: every layer with
-    <= 256 partial rows per group) gives bit for bit the weights, Adam slots, BN moving averages
-    and losses of the two-launch path (DCGAN_BN_FOLD=0) over 3 steps, with fewer launches."""
-    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
-    dev = torch.device("cuda", 0)
-    cfg = DCGANConfig()
-    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(3)) * 2 - 1).to(dev)
-    monkeypatch.setenv("DCGAN_BN_FOLD", "256")
-    e1 = HipEngine(cfg, B, dev, dtype=dtype, graph=False, seed=3)
-    monkeypatch.setenv("DCGAN_BN_FOLD", "0")
-    e2 = HipEngine(cfg, B, dev, dtype=dtype, graph=False, seed=3)
-    assert e1.kernel_count() < e2.kernel_count()
-    e1.set_batch(real)
-    e2.set_batch(real)
-    for _ in range(3):
-        e1.train_step()
-        e2.train_step()
-    torch.cuda.synchronize()
-    pairs = [(e1.model.g.flat, e2.model.g.flat), (e1.model.d.flat, e2.model.d.flat),
-             (e1.opt_g.m.flat, e2.opt_g.m.flat), (e1.opt_d.v.flat, e2.opt_d.v.flat)]
-    for bs1, bs2 in ((e1.model.g_bn, e2.model.g_bn), (e1.model.d_bn, e2.model.d_bn)):
-        for k in bs1.mean:
-            pairs += [(bs1.mean[k], bs2.mean[k]), (bs1.var[k], bs2.var[k])]
-    for a, b in pairs:
-        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
-    assert e1.last_losses() == e2.last_losses()
 
 
 @pytest.mark.gpu
 def test_g_wgrad_placements_are_bit_identical(monkeypatch):
-    """The default G weight-gradient placement (idle alt1 stream, "aaaa", with the first Adam part
-    on that stream) == round 4's (behind the D chain, last two on cs: "ddcc") == two idle streams
-    ("sasa") == "aaaa" with the one-launch Adam after the join, bit for bit, 3 steps."""
+    """The default G weight-gradient placement (idle alt1 stream, "aaaa") == round 4's (behind the
+    D chain, last two on cs: "ddcc") == two idle streams ("sasa") == all on cs ("cccc"), bit for
+    bit, 3 steps."""
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     dev = torch.device("cuda", 0)
     B = 32
     real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(dev)
     engs = []
-    for place in (None, "ddcc", "sasa", "aaaa/one-adam", "aaaa/d-wgrad-side"):
-        monkeypatch.setenv("DCGAN_ADAM_SPLIT_ALT", "0" if place and place.endswith("one-adam") else "1")
-        monkeypatch.setenv("DCGAN_D_WGRAD_SIDE", "1" if place and place.endswith("d-wgrad-side") else "0")
+    for place in (None, "ddcc", "sasa", "cccc"):
         if place is None:
             monkeypatch.delenv("DCGAN_GW_PLACE", raising=False)
         else:
-            monkeypatch.setenv("DCGAN_GW_PLACE", place[:4])
+            monkeypatch.setenv("DCGAN_GW_PLACE", place)
         e = HipEngine(DCGANConfig(), B, dev, graph=False, seed=5)
-        assert e._adam_alt == (place is None or place.endswith("d-wgrad-side"))
-        assert e._dws == bool(place and place.endswith("d-wgrad-side"))
         e.set_batch(real)
         for _ in range(3):
             e.train_step()
         torch.cuda.synchronize()
         engs.append(e)
     monkeypatch.delenv("DCGAN_GW_PLACE", raising=False)
-    monkeypatch.delenv("DCGAN_D_WGRAD_SIDE", raising=False)
     assert engs[0]._gw_place() == "aaaa"
     assert all(e.global_step == 3 for e in engs)
     for e in engs[1:]:
@@ -526,28 +462,3 @@ def test_g_wgrad_placements_are_bit_identical(monkeypatch):
         assert engs[0].last_losses() == e.last_losses()
 
 
-@pytest.mark.gpu
-def test_early_adam_d_is_bit_identical(monkeypatch):
-    """DCGAN_ADAM_D_EARLY=1 (Adam(D) on the D chain's stream beside the G chain's tail, Adam(G) +
-    step counter after the join) == the one two-model Adam after the join, bit for bit, 3 steps."""
-    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
-    dev = torch.device("cuda", 0)
-    cfg = DCGANConfig()
-    B = 32
-    real = (torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1).to(dev)
-    monkeypatch.setenv("DCGAN_ADAM_D_EARLY", "1")
-    e1 = HipEngine(cfg, B, dev, graph=False, seed=4)
-    monkeypatch.setenv("DCGAN_ADAM_D_EARLY", "0")
-    e2 = HipEngine(cfg, B, dev, graph=False, seed=4)
-    assert e1._adam_early and not e2._adam_early   # (decided when the update program is built)
-    e1.set_batch(real)
-    e2.set_batch(real)
-    for _ in range(3):
-        e1.train_step()
-        e2.train_step()
-    torch.cuda.synchronize()
-    for a, b in ((e1.model.g.flat, e2.model.g.flat), (e1.model.d.flat, e2.model.d.flat),
-                 (e1.wbf_d.flat, e2.wbf_d.flat), (e1.opt_d.m.flat, e2.opt_d.m.flat), (e1.opt_g.v.flat, e2.opt_g.v.flat),
-                 (e1.opt_g.powers, e2.opt_g.powers), (e1.opt_d.powers, e2.opt_d.powers)):
-        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
-    assert e1.last_losses() == e2.last_losses() and e1.global_step == e2.global_step == 3

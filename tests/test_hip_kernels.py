@@ -424,67 +424,6 @@ def _p(t):
     return 0 if t is None else t.data_ptr()
 
 
-@pytest.mark.parametrize("groups,Bg,Hs,C,rows_pb", [(2, 4, 8, 128, 64), (1, 8, 8, 256, 32), (2, 16, 4, 512, 16),
-                                                    (1, 64, 8, 64, 16)])
-def test_bn_fold_matches_finalize_then_apply(groups, Bg, Hs, C, rows_pb):
-    """bnfold.hip (finalize inside the apply launch) == bn_finalize + bn_apply_act and
-    bn_bwd_finalize + bn_bwd_apply, bit for bit, output by output (partial rows per group:
-    16..256)."""
-    h = H()
-    R_ = groups * Bg * Hs * Hs
-    P = R_ // rows_pb
-    assert P // groups <= 256
-    x = bf(rnd(groups * Bg, Hs, Hs, C, scale=2.0, seed=126) + 0.3)
-    dy = bf(rnd(groups * Bg, Hs, Hs, C, seed=129))
-    gamma = (1 + 0.1 * rnd(C, seed=127)).contiguous()
-    beta = (0.1 * rnd(C, seed=128)).contiguous()
-    part = torch.empty(P, 2, C, device=dev)
-    pr = _prog()
-    pr.colstats("st", 0, _p(x), 0, 0, 0, 0, 0, 0.2, R_, C, rows_pb, R_ // groups, _p(part), 0)
-    h.run(pr)
-    outs = []
-    for fold in (False, True):
-        o = {k: torch.zeros(groups, C, device=dev) for k in ("mean", "rstd", "scale", "shift")}
-        o["ema_m"] = torch.full((groups, C), 0.5, device=dev)
-        o["ema_v"] = torch.full((groups, C), 2.0, device=dev)
-        o["y"] = torch.zeros_like(x)
-        pr = _prog()
-        args = (_p(part), P // groups, groups, C, float(R_ // groups), _p(gamma), _p(beta), 1e-5, _p(o["mean"]),
-                _p(o["rstd"]), _p(o["scale"]), _p(o["shift"]), _p(o["ema_m"]), _p(o["ema_v"]), 0.9)
-        if fold:
-            assert pr.bn_fold_ok(P // groups, groups, C, R_ // groups)
-            pr.bn_fold_fwd("fold", *args, _p(x), _p(o["y"]), R_, 2, 0.2, 0)
-        else:
-            pr.bn_finalize("fin", *args, 0)
-            pr.bn_apply_act("apply", _p(x), _p(o["y"]), _p(o["scale"]), _p(o["shift"]), R_, C, R_ // groups, 2, 0.2, 0)
-        h.run(pr)
-        # backward (statistics of the two-launch forward for both, so only the backward differs)
-        y = outs[0]["y"] if fold else o["y"]
-        mean, rstd = (outs[0]["mean"], outs[0]["rstd"]) if fold else (o["mean"], o["rstd"])
-        part2 = torch.empty(P, 2, C, device=dev)
-        pr = _prog()
-        pr.colstats("bst", 1, _p(x), _p(dy), _p(y), _p(mean), _p(rstd), 2, 0.2, R_, C, rows_pb, R_ // groups,
-                    _p(part2), 0)
-        h.run(pr)
-        o["coef"] = torch.zeros(groups, 3, C, device=dev)
-        o["dgam"] = torch.zeros(C, device=dev)
-        o["dbet"] = torch.zeros(C, device=dev)
-        o["dx"] = torch.zeros_like(x)
-        pr = _prog()
-        args = (_p(part2), P // groups, groups, C, float(R_ // groups), _p(gamma), _p(mean), _p(rstd),
-                _p(o["dgam"]), _p(o["dbet"]), _p(o["coef"]))
-        if fold:
-            pr.bn_fold_bwd("bfold", *args, _p(dy), _p(y), _p(x), _p(o["dx"]), R_, 2, 0.2, 0)
-        else:
-            pr.bn_bwd_finalize("bfin", *args, 0)
-            pr.bn_bwd_apply("bapp", _p(dy), _p(y), _p(x), _p(o["coef"]), _p(o["dx"]), R_, C, R_ // groups, 2, 0.2, 0)
-        h.run(pr)
-        outs.append(o)
-    torch.cuda.synchronize()
-    bad = [k for k in outs[0] if not torch.equal(outs[0][k], outs[1][k])]
-    assert not bad, {k: float((outs[0][k].float() - outs[1][k].float()).abs().max()) for k in bad}
-
-
 def test_bn_forward_backward_groups():
     """colstats -> finalize (+EMA) -> apply(act) and the backward chain vs autograd (2 groups)."""
     h = H()
