@@ -140,17 +140,36 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
   const bool nok = n < N;
   const int g = m0 / p.bnb_rpg;
   const float slope = p.bnb_act == ACT_LRELU ? p.bnb_leak : 0.f;
+  // Every x / y row this thread needs is loaded BEFORE the first store: interleaved with the C
+  // stores, each row's loads waited a full memory round trip (the compiler cannot move a load of
+  // bnb_x / bnb_y above a store to C, they may alias), IT of them back to back per thread.
+  constexpr int IT = (BM + RL - 1) / RL;
+  int offs[IT];
+  elem8 yv_[IT], xv_[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int r = rl + it * RL;
+    const int off = (r < BM && nok) ? rowoff[r] : -1;
+    offs[it] = off;
+    const size_t o = off >= 0 ? (size_t)off + p.cofs + n : 0;
+    if (off >= 0) {
+      yv_[it] = *reinterpret_cast<const elem8*>(p.bnb_y + o);
+      if (!p.bnb_store_g) xv_[it] = *reinterpret_cast<const elem8*>(p.bnb_x + o);
+    }
+  }
   if (p.bnb_store_g) {  // activation backward only: store g, partial sums of the stored g
     float s[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] = 0.f;
     elem_t* C = reinterpret_cast<elem_t*>(p.C);
-    for (int r = rl; r < BM; r += RL) {
-      const int off = rowoff[r];
-      if (off < 0 || !nok) continue;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int r = rl + it * RL;
+      const int off = offs[it];
+      if (off < 0) continue;
       const size_t o = (size_t)off + p.cofs + n;
       const elem8 dv = __builtin_bit_cast(elem8, *reinterpret_cast<const u32x4*>(ctile + r * CPAD + 8 * c));
-      const elem8 yv = *reinterpret_cast<const elem8*>(p.bnb_y + o);
+      const elem8 yv = yv_[it];
       elem8 gv;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -182,15 +201,16 @@ __device__ __forceinline__ void vec_store_bnb(const IGemmArgs& p, const int* row
     s2[i] = 0.f;
   }
   elem_t* C = reinterpret_cast<elem_t*>(p.C);
-  for (int r = rl; r < BM; r += RL) {
-    const int off = rowoff[r];
-    if (off < 0 || !nok) continue;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int r = rl + it * RL;
+    const int off = offs[it];
+    if (off < 0) continue;
     const size_t o = (size_t)off + p.cofs + n;
     const u32x4 v = *reinterpret_cast<const u32x4*>(ctile + r * CPAD + 8 * c);
     *reinterpret_cast<u32x4*>(C + o) = v;
     const elem8 dv = __builtin_bit_cast(elem8, v);
-    const elem8 yv = *reinterpret_cast<const elem8*>(p.bnb_y + o);
-    const elem8 xv = *reinterpret_cast<const elem8*>(p.bnb_x + o);
+    const elem8 yv = yv_[it], xv = xv_[it];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float gv = (float)dv[i] * ((float)yv[i] > 0.f ? 1.f : slope);

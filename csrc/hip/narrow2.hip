@@ -21,7 +21,11 @@
 // one image; wave w owns output row w (two 16-pixel blocks). The 11 x 67 input window is held in
 // LDS as 4-channel (8 B) pixels; the next tile's window is loaded into registers while the current
 // one is computed. Swapped operands (C^T = W^T X^T): each lane ends with 4 consecutive channels of
-// one pixel -> 8-byte stores, no LDS staging of the output.
+// one pixel; the 4x32-pixel C tile goes through LDS so the store pass writes whole 16-byte chunks
+// of contiguous 4 KiB rows, with the BN-backward operands (x, y) of its pixels loaded before any
+// store (round 6: the fused-statistics variant went from 39.7 to 27.9 us, the forward from 19.0
+// to 16.9 us; round 5's 8-byte stores interleaved with dependent loads waited a memory round
+// trip per 16 pixels).
 //
 // nwgrad: one workgroup = a band of output rows of one image, processed in chunks of <= 256
 // pixels; both MFMA operands are "k = pixel" fragments read with the gfx950 transposing read
@@ -59,6 +63,8 @@ constexpr int NC_WP = NC_WC + 1;            // window pixel pitch per row
 constexpr int NC_WPIX = NC_WR * NC_WC;      // 737 staged pixels
 constexpr int NC_PPT = (NC_WPIX + 255) / 256;
 constexpr int NC_KS = 136;                  // transposed-weight row stride (elements; 272 B = 17 x 16 B)
+constexpr int NC_CS = 72;                   // C-tile pixel stride (elements; 144 B = 9 x 16 B)
+constexpr int NC_SP = NC_TY * NC_TX * 8 / 256;  // 16-byte chunks per thread in the store pass
 
 struct NConvArgs {
   const elem_t* x; const elem_t* w; const float* bias; elem_t* y;
@@ -82,6 +88,7 @@ __global__ __launch_bounds__(256) void nconv_kernel(NConvArgs p) {
   __shared__ __attribute__((aligned(16))) elem_t wt[64 * NC_KS];
   __shared__ __attribute__((aligned(16))) elem_t xs[NC_WR * NC_WP * 4];
   __shared__ float red[4][2][64];
+  __shared__ __attribute__((aligned(16))) elem_t ct[NC_TY * NC_TX * NC_CS];  // C tile (store pass)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
   int t = blockIdx.x;
@@ -101,18 +108,21 @@ __global__ __launch_bounds__(256) void nconv_kernel(NConvArgs p) {
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
       wf[nb][kb] = *reinterpret_cast<const elem8*>(wt + (16 * nb + li) * NC_KS + 32 * kb + 8 * g);
-  float bias_r[4][4], mu[4][4], rs[4][4], s1[4][4], s2[4][4];
+  float bias_r[4][4];
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = 16 * nb + 4 * g + e;
-      bias_r[nb][e] = p.bias ? p.bias[n] : 0.f;
-      mu[nb][e] = BNB ? p.mean[n] : 0.f;
-      rs[nb][e] = BNB ? p.rstd[n] : 0.f;
-      s1[nb][e] = 0.f;
-      s2[nb][e] = 0.f;
-    }
+    for (int e = 0; e < 4; ++e) bias_r[nb][e] = p.bias ? p.bias[16 * nb + 4 * g + e] : 0.f;
+  // store pass: this thread's fixed 8-channel chunk
+  const int c8 = tid & 7;
+  float mu[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = BNB ? p.mean[8 * c8 + e] : 0.f;
+    rs[e] = BNB ? p.rstd[8 * c8 + e] : 0.f;
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+  }
   const float bslope = p.bact == ACT_LRELU ? p.bleak : 0.f;
 
   // ---- window staging: registers (next tile) -> LDS
@@ -150,7 +160,6 @@ __global__ __launch_bounds__(256) void nconv_kernel(NConvArgs p) {
   __syncthreads();
   for (; t < p.ntiles; t += gridDim.x) {
     const int tn = t + gridDim.x;
-    if (tn < p.ntiles) fetch(tn);  // in flight while this tile computes
     const int b = t / p.tiles_per_img, rem = t - b * p.tiles_per_img;
     const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
     f32x4 acc[2][4];
@@ -173,57 +182,79 @@ __global__ __launch_bounds__(256) void nconv_kernel(NConvArgs p) {
         for (int nb = 0; nb < 4; ++nb) acc[h][nb] = DCG_MFMA_16x16x32(wf[nb][kb], xf, acc[h][nb], 0, 0, 0);
       }
     }
-    // ---- epilogue: lane = pixel 16 h + li of output row `wave`, channels 16 nb + 4 g + e
-    const int oy = ty * NC_TY + wave;
+    // next window in flight under this tile's store pass (issued after the MFMAs: issued before
+    // them, the compiler's register reuse drained it at the first LDS read)
+    if (tn < p.ntiles) fetch(tn);
+    // ---- C tile -> LDS: lane = pixel 16 h + li of output row `wave`, channels 16 nb + 4 g + e
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int ox = tx * NC_TX + 16 * h + li;
-      const bool valid = oy < p.Ho && ox < p.Wo;
-      const size_t o = (((size_t)b * p.Ho + (valid ? oy : 0)) * p.Wo + (valid ? ox : 0)) * 64;
+      const int px = wave * NC_TX + 16 * h + li;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
-        const int n0 = 16 * nb + 4 * g;
         elem4 ov;
 #pragma unroll
         for (int e = 0; e < 4; ++e) ov[e] = f2bf(nc_act<ACT>(acc[h][nb][e] + bias_r[nb][e], p.leak));
-        if (valid) {
-          *reinterpret_cast<elem4*>(p.y + o + n0) = ov;
-          if constexpr (BNB) {  // statistics of exactly the stored (rounded) gradient
-            const elem4 xv = *reinterpret_cast<const elem4*>(p.bx + o + n0);
-            const elem4 yv = *reinterpret_cast<const elem4*>(p.by + o + n0);
+        *reinterpret_cast<elem4*>(ct + px * NC_CS + 16 * nb + 4 * g) = ov;
+      }
+    }
+    __syncthreads();  // the C tile is complete; every wave is done with this window
+    // ---- store pass: thread = one 8-channel chunk (c8) of 4 pixels, 16-byte coalesced rows
+    //      (a tile row is 32 contiguous pixels = 4 KiB); BN operands loaded before the stores
+    size_t o[NC_SP];
+    bool ok[NC_SP];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float gv = (float)ov[e] * ((float)yv[e] > 0.f ? 1.f : bslope);
-              s1[nb][e] += gv;
-              s2[nb][e] += gv * ((float)xv[e] - mu[nb][e]) * rs[nb][e];
-            }
+    for (int i = 0; i < NC_SP; ++i) {
+      const int px = (tid >> 3) + 32 * i;  // pixel of the tile: row px / 32, column px % 32
+      const int oy = ty * NC_TY + (px >> 5), ox = tx * NC_TX + (px & 31);
+      ok[i] = oy < p.Ho && ox < p.Wo;
+      o[i] = ok[i] ? (((size_t)b * p.Ho + oy) * p.Wo + ox) * 64 + 8 * c8 : 0;
+    }
+    elem8 bxv[NC_SP], byv[NC_SP];
+    if constexpr (BNB) {
+#pragma unroll
+      for (int i = 0; i < NC_SP; ++i) {
+        bxv[i] = *reinterpret_cast<const elem8*>(p.bx + o[i]);
+        byv[i] = *reinterpret_cast<const elem8*>(p.by + o[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NC_SP; ++i) {
+      const int px = (tid >> 3) + 32 * i;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ct + px * NC_CS + 8 * c8);
+      if (ok[i]) {
+        *reinterpret_cast<u32x4*>(p.y + o[i]) = v;
+        if constexpr (BNB) {  // statistics of exactly the stored (rounded) gradient
+          const elem8 dv = __builtin_bit_cast(elem8, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gv = (float)dv[e] * ((float)byv[i][e] > 0.f ? 1.f : bslope);
+            s1[e] += gv;
+            s2[e] += gv * ((float)bxv[i][e] - mu[e]) * rs[e];
           }
         }
       }
     }
-    __syncthreads();  // every wave is done with this window
     if (tn < p.ntiles) {
-      commit();
-      __syncthreads();
+      commit();         // (every wave finished its window reads before the barrier above)
+      __syncthreads();  // the window is staged; every wave is done with this C tile
     }
   }
   if constexpr (BNB) {
-    // fixed-order reduction: the 16 pixel lanes of a group (butterfly), then the 4 waves in order
+    // fixed-order reduction: the 8 lanes of a wave with the same chunk (xor 8, 16, 32), then
+    // the 4 waves in order
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
+    for (int e = 0; e < 8; ++e) {
+      float a = s1[e], c = s2[e];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = s1[nb][e], c = s2[nb][e];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          c += __shfl_xor(c, o, 64);
-        }
-        if (li == 0) {
-          red[wave][0][16 * nb + 4 * g + e] = a;
-          red[wave][1][16 * nb + 4 * g + e] = c;
-        }
+      for (int sh = 8; sh < 64; sh <<= 1) {
+        a += __shfl_xor(a, sh, 64);
+        c += __shfl_xor(c, sh, 64);
       }
+      if (lane < 8) {
+        red[wave][0][8 * c8 + e] = a;
+        red[wave][1][8 * c8 + e] = c;
+      }
+    }
     __syncthreads();
     if (tid < 128) {
       const int st = tid >> 6, n = tid & 63;

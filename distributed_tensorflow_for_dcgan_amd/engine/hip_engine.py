@@ -1300,7 +1300,8 @@ class HipEngine:
         1.309-1.316 vs 1.336-1.341 ms (fp32 wire), 1.199-1.202 vs 1.242-1.245 (bf16). Putting g_h1's
         weight gradient there too was faster at W=1 but slower at W = 2, 4 and 8
         (ab_ddp_gw_world_r5.txt). Graph-replayed segments keep round 4's layout."""
-        return not self.graph_enabled and self._g_split is not None
+        return (self._schedule() == "concurrent" and not (self.graph_enabled or self.graph_requested)
+                and self._g_split is not None)
 
     def _g_chain_gw_alt(self, ex, cs):
         """Segment "G_chain" with G's weight gradients on alt1 (_ddp_gw_alt), and the collective of
