@@ -1,60 +1,33 @@
 """Fused HIP training engine: the whole reference DCGAN step on hand-written gfx950 kernels.
 
 The step (``image_train.py:151-158`` semantics) is recorded ONCE into
-native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buffers, then
-replayed every step -- captured into hipGraphs so a step is one (single process) or seven
-(DDP) graph launches:
+native ``Program`` objects (``csrc/bindings.cpp``) over statically allocated buffers and replayed
+every step from C++ (eager, the default) or as hipGraphs:
 
-  progA[:a_fwd]  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the
-                 2B batch [real | fake] with per-half BN statistics (= the reference's two
-                 D calls) -> fused 3-loss BCE
-  progA[a_fwd:]  the g_loss chain back through D(fake) (pre-update D weights) and G's
-                 backward (G grads final)                          -- the "G chain"
-  progW          G's weight gradients, each tied to the progA position that produces its operand;
-                 under "fused" they run on the D chain's stream after that chain, beside G's
-                 data-gradient chain
-  progB          D's backward of d_loss, both halves (D grads final) -- the "D chain";
-                 runs on its own stream concurrently with the G chain (disjoint buffers,
-                 both only READ D's forward state and weights)
-  progC          TF-Adam(G), TF-Adam(D), beta powers, global step (device-resident); each
-                 Adam also writes the 16-bit weight mirror the next step's GEMMs read
+  progA[:a_fwd]  z ~ U(-1,1) (Philox, device step counter) -> G forward -> D forward on the 2B
+                 batch [real | fake] with per-half BN statistics -> fused 3-loss BCE
+  progA[a_fwd:]  the g_loss chain back through D(fake) and G's data gradients  -- "G chain"
+  progW          G's weight gradients, each tied to the progA position that produces its operand
+  progB          D's backward of d_loss, both halves (D grads final)            -- "D chain"
+  progC          TF-Adam(G), TF-Adam(D), beta powers, global step (+ 16-bit weight mirrors)
 
-Schedules (``_schedule``), all covered by the stream-hazard checker
-(``engine/schedule_check.py``) and by GPU bit-exactness tests:
-  "fused"       single process: ONE hipGraph; the two backward chains on two streams; ONE
-                Adam launch for both models after the join (16-bit dtypes)
-  "concurrent"  DDP (default) and the per-phase timed step: the two chains cut into 7 graph
-                segments, the collectives issued between them from the host on a comm stream --
-                D's top layer + head (76 % of D's gradient bytes at 64x64) as soon as the D chain
-                has produced it; G's lowest deconv (64 % of G's bytes) as soon as its weight
-                gradient exists (``_g_split_plan``: the G chain computes it right after its input
-                gradient, the rest of G's backward follows as "G_tail"); the rest of D's when the
-                D chain ends, the rest of G's when the G tail ends; Adam(D) runs under G's last
-                all-reduce. With a bf16 wire (bf16 engine) each segment ends with the cast of its
-                finished gradient slice into a flat bf16 image that RCCL reduces in place and
-                Adam reads (``_wire_direct``): no copies around the collectives
-  "ddp"         DCGAN_DDP_SCHEDULE=ddp (RCCL): the fused schedule with the gradient all-reduces on
-                the comm stream INSIDE the same single hipGraph (RCCL collectives are captured);
-                G's gradients go out in per-layer buckets as G's weight gradients land
-                (``_g_cuts``). W=1 overhead vs "fused" is ~1.5 % (vs ~7 % segmented), but ROCm's
-                graph executor does not overlap the collectives with the compute branches, so
-                with real communication the segmented step is faster (ab_ddp_one_graph_r3.txt)
-  "serial"      ``schedule="serial"`` / DCGAN_SERIAL_DBWD=1: fwd + G chain, then the D chain, as
-                5 segments (the G all-reduce overlaps D's backward)
+Schedules (``_schedule``), all proven free of cross-stream overlaps by ``schedule_check.py``:
+  "fused"       one process: both chains on two streams, G weight gradients on a third, one
+                Adam launch after the join
+  "concurrent"  DDP default: the chains cut into segments with the gradient collectives issued
+                between them on the comm stream (D's top layer first, g_h1's slice as soon as its
+                weight gradient exists, the rest as each chain ends; bf16 wire without copies)
+  "ddp"         the fused schedule with the collectives inside one hipGraph (native RCCL)
+  "serial"      forward + G chain, then the D chain (the G all-reduce under D's backward)
 
-Every schedule is issued through an executor (``_TorchExec``; the checker substitutes a
-recording one), so the stream order the checker proves is the order the GPU runs.
-
-Layouts: activations NHWC in the compute dtype (bf16 / fp16 / fp32); master weights fp32 in
-TF layout inside the flat ``ParamSet`` buffers (what the checkpoint writes and DDP reduces);
-16-bit runs keep one mirror of every weight in the same flat layout, which every GEMM reads
-in whichever orientation it needs (fp32 runs read the masters directly).
+Layouts: activations NHWC in the compute dtype; fp32 master weights in TF layout inside the flat
+``ParamSet`` buffers (what checkpoints write and DDP reduces); 16-bit runs keep one mirror of every
+weight in the same flat layout, which the GEMMs read in either orientation.
 """
 from __future__ import annotations
 
 import math
 import os
-from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -64,6 +37,7 @@ from ..models.dcgan import DCGAN
 from ..optim.adam import TFAdam
 from ..ops import hip as H
 from ..parallel import dist as D
+from .hip_aux import HipEngineAux
 
 RELU, LRELU, TANH, NONE = 1, 2, 3, 0
 DTYPES = {"bf16": (0, torch.bfloat16), "fp16": (1, torch.float16), "fp32": (2, torch.float32)}
@@ -139,7 +113,7 @@ class _TorchExec:
             graph.replay()
 
 
-class HipEngine:
+class HipEngine(HipEngineAux):
     name = "hip"
     dtype_name = "bf16"
     INIT_LOSS_SCALE = 32768.0   # fp16 dynamic loss scaling (TF/Keras LossScaleOptimizer defaults)
@@ -900,7 +874,13 @@ class HipEngine:
                 else:
                     self._igemm(prog, "g." + L.name + ".dgrad_img", 1, dx, nat, self.img_grad, B, L.out_hw,
                                 L.out_hw, L.cout, L.in_hw, L.in_hw, L.cin, pad)
-        # ---------------- G backward (reads no D state)
+        self._build_g_backward(prog, progw)
+
+    def _build_g_backward(self, prog, progw):
+        """G's backward from the image gradient img_g (G's tanh backward already applied when the
+        image-gradient kernel fused it): data gradients into prog, weight gradients into progw."""
+        cfg, B = self.cfg, self.B
+        Pg, gG = self.model.g, self.grad_g
         self._a_gd_end = prog.size()  # the g_loss chain is done with D's weights / BN parameters
         n = len(self.gl)
         Lg = self.gl[-1]
@@ -1121,12 +1101,9 @@ class HipEngine:
         return run
 
     def _adam_g_split(self) -> bool:
-        """Segmented DDP step: Adam over g_h1's gradient slice runs as soon as that slice's
-        collective (the first G one, the largest) has landed, beside the remaining collectives;
-        Adam over the rest of G after the last one (DCGAN_ADAM_G_SPLIT=0: one Adam(G) at the end).
-        Under the RCCL-like stand-in at W=8: 1.383 vs 1.394-1.399 ms (fp32 wire, 150 GB/s), 1.305 vs
-        1.317-1.319 (bf16), 1.310 vs 1.320 (fp32, 300 GB/s); at W=1 within the spread
-        (profiles/r5/ab_adam_g_split_r5.txt)."""
+        """Segmented DDP step: Adam over g_h1's slice as soon as its collective has landed, Adam over
+        the rest of G after the last one (DCGAN_ADAM_G_SPLIT=0: one Adam(G) at the end;
+        profiles/r5/ab_adam_g_split_r5.txt)."""
         return (self._schedule() == "concurrent" and self._g_split is not None and not self.f16
                 and os.environ.get("DCGAN_ADAM_G_SPLIT", "1") != "0")
 
@@ -1179,12 +1156,9 @@ class HipEngine:
         return self._exec
 
     def _run_fused(self, ex, cs):
-        """The "fused" schedule issued onto cs (+ the alt streams); also what gets captured.
-        D's backward starts right after the forward: holding it until the g_loss chain has left
-        D (so it overlaps only G's backward) measured 1.314 vs 1.297 ms/step on MI355X, and
-        holding it behind only the first 3-7 G-chain ops measured slower as well
-        (profiles/r4/ab_d_start_after_r4.txt). G's weight gradients run on the streams _gw_place()
-        gives (default: the idle alt1 stream, each as soon as its operand exists)."""
+        """The "fused" schedule issued onto cs (+ the alt streams); also what gets captured. D's
+        backward starts right after the forward (profiles/r4/ab_d_start_after_r4.txt); G's weight
+        gradients run on the streams _gw_place() gives."""
         ex.run(self.progA, [cs, ex.side], 0, self._a_fwd)
         ex.wait(ex.alt[0], cs)
         ex.run(self.progB, ex.alt)
@@ -1223,15 +1197,10 @@ class HipEngine:
         ex.run(self.progC, [cs, ex.side])
 
     def _gw_place(self) -> str:
-        """Stream of each G weight-gradient segment (progW between consecutive _g_w ends) in the
-        fused step: "a" (default) on the idle alt1 stream as soon as its operand exists (beside
-        both chains), "s" the idle side stream, "d" behind the D chain on its stream, "c" on the G
-        chain's stream after that chain. DCGAN_GW_PLACE gives the string (one letter per segment).
-
-        64x64 bf16, 3 interleaved rounds (profiles/r5/ab_gw_place_r5.txt): "aaaa" 123.7k-124.0k,
-        "ssss" 123.4k-123.8k, "sssc" 123.0k-123.3k, "sasa" 122.6k-123.0k, "ssdd" 121.7k-122.6k
-        img/s against 122.8k-122.9k for round 4's "ddcc" (the D chain now ends only ~15 us before
-        the G chain, so weight gradients queued behind it all land after both chains)."""
+        """Stream of each G weight-gradient segment in the fused step: "a" (default) the idle alt1
+        stream as soon as its operand exists, "s" the side stream, "d" behind the D chain, "c" on
+        cs after the G chain; DCGAN_GW_PLACE gives one letter per segment ("aaaa" measured best,
+        profiles/r5/ab_gw_place_r5.txt)."""
         n = len(self._g_w)
         v = os.environ.get("DCGAN_GW_PLACE")
         if v is None:
@@ -1293,13 +1262,9 @@ class HipEngine:
         run(ex, stream, ex.side if which == self.MAIN else ex.alt[1])
 
     def _ddp_gw_alt(self) -> bool:
-        """Segmented DDP step, eager replay: the G weight gradients other than g_h1's run on the idle
-        alt1 stream as soon as their operands exist (instead of after the G chain on cs), and G's
-        slice above g_h1 goes on the wire from there. Measured (profiles/r5/ab_ddp_gw_alt_b_r5.txt):
-        W=1 one-rank RCCL 117.7k vs 111.9k-112.3k img/s; RCCL-like stand-in at W=8, 150 GB/s:
-        1.309-1.316 vs 1.336-1.341 ms (fp32 wire), 1.199-1.202 vs 1.242-1.245 (bf16). Putting g_h1's
-        weight gradient there too was faster at W=1 but slower at W = 2, 4 and 8
-        (ab_ddp_gw_world_r5.txt). Graph-replayed segments keep round 4's layout."""
+        """Segmented DDP step, eager replay: G's weight gradients other than g_h1's on the idle alt1
+        stream as soon as their operands exist, G's slice above g_h1 reduced from there
+        (profiles/r5/ab_ddp_gw_alt_b_r5.txt, ab_ddp_gw_world_r5.txt)."""
         return (self._schedule() == "concurrent" and not (self.graph_enabled or self.graph_requested)
                 and self._g_split is not None)
 
@@ -1540,127 +1505,6 @@ class HipEngine:
     def losses_tensor(self) -> torch.Tensor:
         return self.losses
 
-    def activations(self) -> "Dict[str, torch.Tensor]":
-        """Views of the last step's tensors for summaries (no extra compute)."""
-        B = self.B
-        a = OrderedDict()
-        a["z"] = self.z
-        a["d"] = self.prob[:B]
-        a["d_"] = self.prob[B:]
-        a["G"] = self.fake
-        a["g_h0_relu"] = self.g_h0
-        for L in self.gl[:-1]:
-            a[L.name + "_relu"] = self.g_a[L.name]
-        a[self.gl[-1].name] = self.fake
-        for L in self.dl:
-            a[L.name] = self.d_a[L.name][:B]
-        a[self.cfg.d_lin_name] = self.logits[:B]
-        return a
-
-    # ------------------------------------------------------------------ device-side summaries
-    def device_summaries(self) -> "OrderedDict[str, object]":
-        """Zero fraction + TF-bucket histogram statistics of every summarised tensor, computed on
-        the device (summary.hip) in ONE program; only the per-tensor statistics rows (a few KB
-        each) are copied to the host. Returns name -> numpy row [min, max, n, sum, sumsq, zeros,
-        counts...] (obs.summaries turns them into TensorBoard protos)."""
-        from ..obs.events import BUCKET_EDGES
-        if self.progSum is None:
-            names, tensors = [], []
-            for name, t in self.activations().items():
-                if name != "G":
-                    names.append(name + ("/activations" if name not in ("z", "d", "d_") else ""))
-                    tensors.append(t)
-            for name, t in self.model.all_named_variables().items():
-                names.append(name)
-                tensors.append(t)
-            nb = len(BUCKET_EDGES) + 1
-            self._sum_edges = torch.tensor(BUCKET_EDGES, dtype=torch.float64, device=self.device)
-            self._sum_out = torch.zeros(len(tensors), nb + 6, dtype=torch.float64, device=self.device)
-            prog = self._prog()
-            for i, t in enumerate(tensors):
-                xd = 0 if t.dtype == torch.float32 else 1
-                if xd == 1 and t.dtype != self.edt:
-                    raise TypeError("summary of %s: dtype %s" % (names[i], t.dtype))
-                prog.tensor_summary("sum." + names[i], _p(t), xd, t.numel(), _p(self._sum_edges), nb,
-                                    _p(self._sum_out[i]), 0)
-            self.progSum, self._sum_names = prog, names
-        H.run(self.progSum)
-        rows = self._sum_out.cpu().numpy()
-        return OrderedDict(zip(self._sum_names, rows))
-
-    # ------------------------------------------------------------------ sampling / eval
-    def sampler(self, z: torch.Tensor) -> torch.Tensor:
-        """G with inference-mode BN (moving averages) -- distriubted_model.py:131-153. With
-        --bn_zero_debias the moving averages are divided by 1 - decay^t (t = EMA updates so far,
-        as in the reference engine's BNState.averages)."""
-        if self.progS is None:
-            self._build_sampler()
-        bn = self.model.g_bn
-        t = float(bn.steps[0])
-        corr = 1.0 - bn.decay ** t if (bn.zero_debias and t > 0) else 1.0
-        self._debias.fill_(1.0 / corr)
-        self.sample_z.copy_(z.to(self.device, torch.float32))
-        H.run(self.progS)
-        return self._s_out.float().clone()
-
-    def _build_sampler(self):
-        cfg, B = self.cfg, self.B
-        prog = self._prog()
-        Pg = self.model.g
-        t = self._t
-        h0p, h0 = t(B, cfg.g_lin_out), t(B, cfg.g_lin_out)
-        self._s_out = t(B, cfg.output_size, cfg.output_size, cfg.c_dim)
-        sc = {name: (t(C, dtype=torch.float32), t(C, dtype=torch.float32)) for name, C in cfg.g_bn_layers()}
-        self._s_keep = [h0p, h0, sc]
-        bnst = self.model.g_bn
-        prog.linear_fwd("s.lin", _p(self.sample_z), _p(Pg["g_h0_lin/Matrix"]), _p(Pg["g_h0_lin/bias"]), _p(h0p), B,
-                        cfg.z_dim, cfg.g_lin_out, 0)
-
-        def coef(name, C):  # BN state and the debias factor are read live (device pointers)
-            prog.bn_coef_eval("s." + name, C, _p(Pg[name + "/gamma"]), _p(Pg[name + "/beta"]), cfg.bn_eps,
-                              _p(bnst.mean[name]), _p(bnst.var[name]), 1.0, _p(sc[name][0]), _p(sc[name][1]), 0,
-                              _p(self._debias))
-
-        C0 = cfg.g_base_ch
-        coef("g_bn0", C0)
-        prog.bn_apply_act("s.g_bn0", _p(h0p), _p(h0), _p(sc["g_bn0"][0]), _p(sc["g_bn0"][1]),
-                          B * cfg.g_base_hw ** 2, C0, B * cfg.g_base_hw ** 2, RELU, 0.0, 0)
-        prev = h0
-        for L in self.gl:
-            nat = self.wbf_g[L.name + "/w"]
-            pad = same_pads(L.out_hw)[0]
-            if L.bn:
-                xb, ab = t(B, L.out_hw, L.out_hw, L.cout), t(B, L.out_hw, L.out_hw, L.cout)
-                self._s_keep += [xb, ab]
-                self._igemm(prog, "s." + L.name, 1, prev, nat, xb, B, L.in_hw, L.in_hw, L.cin, L.out_hw, L.out_hw,
-                            L.cout, pad, bias=Pg[L.name + "/biases"])
-                coef(L.bn, L.cout)
-                rows = B * L.out_hw ** 2
-                prog.bn_apply_act("s." + L.bn, _p(xb), _p(ab), _p(sc[L.bn][0]), _p(sc[L.bn][1]), rows, L.cout, rows,
-                                  RELU, 0.0, 0)
-                prev = ab
-            else:
-                self._deconv_out(prog, "s." + L.name, prev, nat, self._s_out, B, L, pad, Pg[L.name + "/biases"], TANH)
-        self.progS = prog
-
-    def eval_losses(self, real: torch.Tensor, z: torch.Tensor) -> Dict[str, float]:
-        """Sample-time d_loss / g_loss (image_train.py:181-184) in train-mode BN but WITHOUT
-        mutating the moving averages (documented deviation)."""
-        if self.progEval is None:
-            prog = self._prog()
-            self._ev_z = self._t(self.B, self.cfg.z_dim, dtype=torch.float32)
-            self._build_forward(prog, update_ema=False, z=self._ev_z, train_z=False)
-            self.progEval = prog
-        saved_real = self.d_in[:self.B].clone()
-        saved_losses = self.losses.clone()
-        self.set_batch(real)
-        self._ev_z.copy_(z.to(self.device, torch.float32))
-        H.run(self.progEval)
-        l = self.losses.tolist()
-        self.d_in[:self.B].copy_(saved_real)
-        self.losses.copy_(saved_losses)
-        return {"d_loss": l[3], "g_loss": l[2]}
-
     def sync_state_for_checkpoint(self) -> None:
         torch.cuda.synchronize(self.device)
 
@@ -1672,32 +1516,3 @@ class HipEngine:
     def after_state_load(self) -> None:
         """Call after loading weights/slots from a checkpoint: refresh the 16-bit weight mirrors."""
         self._repack_weights_now()
-
-    def placement(self) -> List[str]:
-        """--log_device_placement lines: every recorded op of the step runs on this rank's HIP
-        device; which stream slots / graphs carry it."""
-        progs = [("forward+G backward", self.progA), ("D backward", self.progB), ("G weight grads", self.progW),
-                 ("optimisers", self.progC)]
-        out = ["HIP engine (%s): %d kernels per step, schedule %s, hipGraph %s%s" % (
-            self.dtype_name, self.kernel_count(), self._schedule(), "captured" if self.graph_enabled else
-            ("requested" if self.graph_requested else "off"),
-            ", comm stream for all-reduces" if self.ddp else "")]
-        for label, p in progs:
-            if p is None:
-                continue
-            slots = sorted({p.op_info(i)[1] for i in range(p.size())})
-            out.append("  %-20s %3d ops on %s, stream slots %s" % (label, p.size(), self.device, slots))
-        return out
-
-    def op_names(self) -> List[str]:
-        out = []
-        for p in (self.progA, self.progB, self.progW, self.progC):
-            out += [p.name(i) for i in range(p.size())]
-        return out
-
-    def kernel_count(self) -> int:
-        """Kernel launches per training step (events excluded)."""
-        n = 0
-        for p in (self.progA, self.progB, self.progW, self.progC):
-            n += sum(1 for i in range(p.size()) if p.op_info(i)[2] == self.ext.OP_LAUNCH)
-        return n

@@ -70,11 +70,20 @@ class ParamSet:
                  device: torch.device | str = "cpu", dtype: torch.dtype = torch.float32):
         self.specs = list(specs)
         self.offsets: "OrderedDict[str, Tuple[int, Tuple[int, ...]]]" = OrderedDict()
+        # storage order: every tensor the step reads in fp32 (biases, BN scale / offset, linear
+        # layers) first, then the conv / deconv kernels ("/w") in layer order -- the tensors the
+        # GEMMs only read through the 16-bit mirror. Each layer's kernel is then one contiguous
+        # slice (DDP collectives per layer; the sharded update shards exactly those). Names, TF
+        # shapes and the initialisation order stay the spec order.
+        order = sorted(range(len(self.specs)), key=lambda i: (self.specs[i][0].endswith("/w"), i))
+        offs = {}
         off = 0
+        for i in order:
+            name, shape, _ = self.specs[i]
+            offs[name] = off
+            off += -(-math.prod(shape) // self.ALIGN) * self.ALIGN
         for name, shape, _ in self.specs:
-            self.offsets[name] = (off, tuple(shape))
-            n = math.prod(shape)
-            off += -(-n // self.ALIGN) * self.ALIGN
+            self.offsets[name] = (offs[name], tuple(shape))
         self.numel_padded = off
         self.flat = torch.zeros(off, device=device, dtype=dtype)
         self._build_views()
