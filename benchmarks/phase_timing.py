@@ -29,7 +29,8 @@ class FakeReducer:
     (fp32 gradient -> bf16 wire buffer before the collective, back after it:
     parallel/dist.py GradAllReducer.issue), so the bf16 rows carry their full cost."""
 
-    def __init__(self, us, flat=None, world=8, esize=4, nwg=32, kind="rccl", cycles_per_us=0.0, prefilled=None):
+    def __init__(self, us, flat=None, world=8, esize=4, nwg=32, kind="rccl", cycles_per_us=0.0, prefilled=None,
+                 wire_copies=True):
         self.us = float(us)
         self.flat = flat
         self.numel = 0 if flat is None else flat.numel()
@@ -42,7 +43,7 @@ class FakeReducer:
         # the step graphs, so the stand-in only streams the image, no copies)
         self.prefilled = prefilled
         self.wire = (torch.empty(self.numel, device=flat.device, dtype=torch.bfloat16)
-                     if esize == 2 and flat is not None and prefilled is None else None)
+                     if esize == 2 and flat is not None and prefilled is None and wire_copies else None)
         if kind == "rccl" and self.bytes > 0 and flat is not None:
             from distributed_tensorflow_for_dcgan_amd.ops import hip as H
             payload = prefilled if prefilled is not None else (flat if self.wire is None else self.wire)
@@ -106,6 +107,9 @@ def standin_engine(cfg, B, dev, schedule="concurrent", ddp=True, graph=False, wi
         # collective call points of DDP on a comm stream; the update program is rebuilt for W=2
         # (Adam scales the un-reduced gradients by 1/2: only timing and stream order are emulated)
         eng.world = 2
+        if getattr(eng, "_shards", None) is not None:  # sharded update: shards of 1/W, as at W ranks
+            eng.shard_world = world
+            eng._build_shards()
         eng._build_updates()
         eng._ensure_comm()
 
@@ -115,6 +119,18 @@ def standin_engine(cfg, B, dev, schedule="concurrent", ddp=True, graph=False, wi
                 us = ring_us(flat.numel(), busbw_gbs, lat_us, world, esize) if busbw_gbs > 0 else 0.0
             comm[name] = round(us, 1)
             return FakeReducer(us, flat, world, esize, nwg, kind, cpu, prefilled=real.wire if real.prefilled else None)
+
+        if eng._sharded():
+            # reduce-scatter: (W-1)/W x 4 B per element, all-gather of the bf16 mirror: (W-1)/W x 2 B
+            # (FakeReducer moves 2 (W-1)/W x esize bytes: esize 2 and 1)
+            for name, (sr, _, _, _) in eng._shards.items():
+                for op, es in (("rs", 2), ("ag", 1)):
+                    us = ring_us(sr.grad.numel(), busbw_gbs, lat_us, world, es) if busbw_gbs > 0 else 0.0
+                    comm[op + "." + name] = round(us, 1)
+                    setattr(sr, op + "_op", FakeReducer(us, sr.grad, world, es, nwg, kind, cpu, wire_copies=False))
+            for name, _, _, _ in eng._small:
+                setattr(eng, "_ar_" + name, fake(name, getattr(eng, "_ar_" + name)))
+            return eng, comm
 
         us3 = [float(x) for x in comm_us.split(",")] if comm_us else [None] * 3
         eng._ar_dtop = fake("dtop", eng._ar_dtop, us3[1])

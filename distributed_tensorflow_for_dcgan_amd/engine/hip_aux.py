@@ -51,7 +51,11 @@ class HipEngineAux:
                 if name != "G":
                     names.append(name + ("/activations" if name not in ("z", "d", "d_") else ""))
                     tensors.append(t)
+            sharded = getattr(self, "_shards", None) is not None and self._sharded()
             for name, t in self.model.all_named_variables().items():
+                if sharded and name.endswith("/w"):  # masters current only on this rank's shard:
+                    mir = self.wbf_g if name in self.wbf_g.tensors else self.wbf_d  # the bf16 mirror
+                    t = mir[name]
                 names.append(name)
                 tensors.append(t)
             nb = len(BUCKET_EDGES) + 1
@@ -158,15 +162,19 @@ class HipEngineAux:
             out.append("  %-20s %3d ops on %s, stream slots %s" % (label, p.size(), self.device, slots))
         return out
 
+    def _step_progs(self):
+        return [p for p in (self.progA, self.progB, self.progW, self.progC, getattr(self, "progSh", None))
+                if p is not None]
+
     def op_names(self) -> List[str]:
         out = []
-        for p in (self.progA, self.progB, self.progW, self.progC):
+        for p in self._step_progs():
             out += [p.name(i) for i in range(p.size())]
         return out
 
     def kernel_count(self) -> int:
         """Kernel launches per training step (events excluded)."""
         n = 0
-        for p in (self.progA, self.progB, self.progW, self.progC):
+        for p in self._step_progs():
             n += sum(1 for i in range(p.size()) if p.op_info(i)[2] == self.ext.OP_LAUNCH)
         return n

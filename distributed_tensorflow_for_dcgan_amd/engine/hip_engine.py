@@ -286,6 +286,7 @@ class HipEngine(HipEngineAux):
         self._d_top_off = self.model.d.offsets[self.dl[-1].name + "/w"][0]
         self._g_cuts = self._g_bucket_cuts()
         self._g_split = self._g_split_plan()
+        self._build_shards()
         self._build_updates()  # (after the G split: Adam(G) follows its collectives)
         self.progX, self._wire_ops = self._prog(), {}
         if self.wire_d is not None:  # fp32 gradient slice -> its bf16 wire image, one op per collective
@@ -317,7 +318,10 @@ class HipEngine(HipEngineAux):
         second part."""
         self.progC = self._prog()
         sch = self._schedule()
-        if sch == "fused" and self.dt == 0:
+        if self._sharded():
+            self._build_update_sharded(self.progC)
+            self._c_split = self._c_split_a = self.progC.size()
+        elif sch == "fused" and self.dt == 0:
             self._build_update_fused(self.progC)
             self._c_split = self._c_split_a = self.progC.size()
         elif sch in ("concurrent", "ddp") and not self.f16:
@@ -326,6 +330,145 @@ class HipEngine(HipEngineAux):
             self._build_update(self.progC, first=True)
             self._c_split = self._c_split_a = self.progC.size()
             self._build_update(self.progC, first=False)
+
+    # ---- sharded update (segmented DDP step, bf16): reduce-scatter -> Adam on 1/W -> all-gather
+    def _shard_plan(self):
+        """(name, model, a, b) of the sharded slices -- the conv kernels, which the step reads only
+        through the 16-bit mirror (ParamSet stores them last, in layer order) -- and the
+        (name, model, a, b) all-reduced slices of everything it reads in fp32 (biases, BN
+        scale / offset, linear layers), or None where the sharded update does not apply."""
+        if not (self.ddp and self.dt == 0 and not self.graph_requested and self._g_split is not None
+                and os.environ.get("DCGAN_DDP_SHARD", "1") != "0"):
+            return None
+        Dm, G = self.model.d, self.model.g
+        first_w = lambda ps: min(off for k, (off, _) in ps.offsets.items() if k.endswith("/w"))  # noqa: E731
+        sdw, o, nd = first_w(Dm), self._d_top_off, Dm.flat.numel()
+        lo, hi = self._g_split[3:]
+        W = self.shard_world or self.world
+        if lo != first_w(G) or not (sdw < o < nd) or any((b - a) % W for a, b in ((sdw, o), (o, nd), (lo, hi))):
+            return None
+        shard = [("dw_top", "d", o, nd), ("g_b", "g", hi, G.flat.numel()), ("g_a", "g", lo, hi), ("dw_rest", "d", sdw, o)]
+        return shard, [("d_small", "d", 0, sdw), ("g_c", "g", 0, lo)]
+
+    shard_world: Optional[int] = None  # shard count override (the one-GPU RCCL-like stand-in)
+
+    def _sharded(self) -> bool:
+        return getattr(self, "_shards", None) is not None and self._schedule() == "concurrent"
+
+    def _build_shards(self):
+        """ShardReducers (their reduced-gradient / 16-bit shard buffers) and progSh: one Adam per
+        shard, run on the comm stream between its reduce-scatter and its all-gather."""
+        plan = self._shard_plan()
+        self._shards, self._sh_ops, self.progSh = None, {}, None
+        if plan is None:
+            return
+        W = self.shard_world or self.world
+        r = self.rank % W
+        self._shards, self._small = {}, plan[1]
+        self.progSh = self._prog()
+        for name, m, a, b in plan[0]:
+            ps, grad, mir = ((self.model.d, self.grad_d, self.wbf_d) if m == "d" else (self.model.g, self.grad_g, self.wbf_g))
+            opt = self.opt_d if m == "d" else self.opt_g
+            sr = D.ShardReducer(grad.flat[a:b], mir.flat[a:b], W, r)
+            self._shards[name] = (sr, m, a, b)
+            k = a + sr.lo
+            i0 = self.progSh.size()
+            self.progSh.adam_bf("adam_shard." + name, _p(ps.flat) + 4 * k, _p(sr.agin), _p(sr.gs),
+                                _p(opt.m.flat) + 4 * k, _p(opt.v.flat) + 4 * k, _p(opt.powers), sr.n, opt.lr,
+                                opt.beta1, opt.beta2, opt.eps, 1.0 / self.world, 0, 0, 0)
+            self._sh_ops[name] = (i0, self.progSh.size())
+
+    def _build_update_sharded(self, prog):
+        """Adam over the all-reduced fp32-read slices (full, every rank) + both beta powers + the
+        step counter, after every shard's Adam has read the powers (the step's final join)."""
+        gs = 1.0 / self.world
+        for name, m, a, b in self._small:
+            ps, grad, mir, opt = ((self.model.d, self.grad_d, self.wbf_d, self.opt_d) if m == "d" else
+                                  (self.model.g, self.grad_g, self.wbf_g, self.opt_g))
+            es = mir.flat.element_size()
+            prog.adam_bf("adam." + name, _p(ps.flat) + 4 * a, _p(mir.flat) + es * a, _p(grad.flat) + 4 * a,
+                         _p(opt.m.flat) + 4 * a, _p(opt.v.flat) + 4 * a, _p(opt.powers), b - a, opt.lr, opt.beta1,
+                         opt.beta2, opt.eps, gs, 0, 0, 0)
+        od, og = self.opt_d, self.opt_g
+        prog.step_end("step_end", _p(od.powers), _p(og.powers), od.beta1, od.beta2, og.beta1, og.beta2,
+                      _p(self.step_counter), 0, 0, self.LOSS_SCALE_GROWTH)
+
+    def _sh_rs(self, ex, name, src) -> None:
+        if self.ddp:
+            ex.wait(ex.comm, src)
+            ex.collective(self._shards[name][0].rs_op, ex.comm)
+
+    def _sh_update(self, ex, name) -> None:
+        """Adam over this rank's shard (on the comm stream, after its reduce-scatter), then the
+        all-gather of the 16-bit shards into the mirror slice."""
+        if self.ddp:
+            b, e = self._sh_ops[name]
+            ex.run(self.progSh, [ex.comm], b, e)
+            ex.collective(self._shards[name][0].ag_op, ex.comm)
+
+    def _run_sharded(self, ex, cs) -> None:
+        """The segmented DDP step with the sharded update. Comm-stream order: RS(d_h3) as soon as
+        D's top layer is done; Adam + AG of it once the g_loss pass has left D (mark inside the G
+        chain); RS(g_h2..g_h4 kernels) from alt1; RS(g_h1 kernel) after the G chain, Adam + AG of
+        g_h2..g_h4 (their last reader, the G chain, is done); RS / Adam / AG of D's lower kernels
+        and the all-reduce of D's fp32-read tensors after the D chain; the all-reduce of G's after
+        the G tail, then Adam + AG of g_h1 (its data gradient, in the tail, read the old mirror).
+        The main stream joins the comm stream and runs Adam over the all-reduced slices."""
+        alt = ex.alt[0]
+        self._tick(0, cs)
+        self._seg(ex, 0, cs)                   # z, G fwd, D fwd (real | fake), losses
+        self._tick(1, cs)
+        ex.wait(alt, cs)
+        self._seg(ex, 1, alt)                  # D chain: head + top layer gradients
+        self._tick(2, alt)
+        self._sh_rs(ex, "dw_top", alt)
+        gd = []                                # mark: the g_loss pass is done with D's weights
+        self._g_chain_gw_alt(ex, cs, on_gd=gd.append, sharded=True)
+        self._tick(3, cs)
+        self._sh_rs(ex, "g_a", cs)
+        self._sh_update(ex, "g_b")
+        B, bt = self.progB, self._b_top_dgrad
+        ex.run(B, ex.alt, self._b_split, bt)   # D chain: the top layer's data gradient
+        if self.ddp:                           # Adam + AG of the top kernel after its last readers
+            ex.wait_mark(ex.comm, gd[0])
+            ex.wait(ex.comm, alt)
+        self._sh_update(ex, "dw_top")
+        ex.run(B, ex.alt, bt, -1)              # D chain: the rest -> grad_d final
+        self._tick(4, alt)
+        self._sh_rs(ex, "dw_rest", alt)
+        self._sh_update(ex, "dw_rest")
+        self._ar_launch(ex, "d_small", alt)
+        self._g_tail_gw_alt(ex, cs)
+        self._tick(5, cs)
+        self._ar_launch(ex, "g_c", cs)
+        self._sh_update(ex, "g_a")
+        self._ar_join(ex, cs)
+        ex.wait(cs, alt)                       # (W = 1 timing: the D chain itself)
+        self._seg(ex, 5, cs)                   # Adam over the all-reduced slices, powers, step
+        self._tick(6, cs)
+
+    def sync_check_tensors(self):
+        """What the cross-rank divergence check compares: the fp32 masters, or -- after sharded
+        updates, where each rank's conv-kernel masters are current only on its shard -- the 16-bit
+        mirrors plus the masters of the all-reduced slices."""
+        if self._shards is None or not self._sharded():
+            return [self.model.g.flat, self.model.d.flat]
+        out = [self.wbf_g.flat, self.wbf_d.flat]
+        for name, m, a, b in self._small:
+            out.append((self.model.d if m == "d" else self.model.g).flat[a:b])
+        return out
+
+    def gather_sharded_state(self) -> None:
+        """Collective (every rank): after sharded updates each rank holds only its shard of the
+        conv kernels' fp32 masters and Adam slots current; gather them (checkpoints, summaries
+        of the masters, the divergence check)."""
+        if self._shards is None or not self.ddp or self.dry:
+            return
+        torch.cuda.synchronize(self.device)
+        for sr, m, a, b in self._shards.values():
+            ps, opt = (self.model.d, self.opt_d) if m == "d" else (self.model.g, self.opt_g)
+            for flat in (ps.flat, opt.m.flat, opt.v.flat):
+                D.gather_shards(flat, [(a, b)])
 
     def _build_update_d_first(self, prog):
         """Adam(D) (progC[:_c_split]), then Adam(G) + beta powers / global step: the step counter
@@ -680,6 +823,8 @@ class HipEngine(HipEngineAux):
             # profiles/r2/ab_d_dgrad_first_r2.txt)
             emit_wgrad()
             fused_next = emit_dgrad()
+            if i == len(self.dl) - 1:
+                self._b_top_dgrad = prog.size()  # the D chain's last read of the top layer's kernel
 
     def _g_bucket_cuts(self) -> List[Tuple[int, int, int]]:
         """G's gradient buckets for the "ddp" schedule: (progW piece index, lo, hi) -- after G's
@@ -1064,6 +1209,10 @@ class HipEngine(HipEngineAux):
                 (lambda ex, cs, sec: self._run_ddp(ex, cs))
             run.empty = False
             return [("step", run, M)]
+        if sch == "concurrent" and self._sharded():
+            return [("fwd", lin([(A, 0, self._a_fwd)]), M), ("D_bwd_top", lin([(B, 0, self._b_split)]), self.ALT),
+                    ("G_chain", lin([]), M), ("D_bwd_rest", lin([(B, self._b_split, -1)]), self.ALT),
+                    ("G_tail", lin([]), M), ("update", lin([(C, 0, -1)]), M)]
         if sch == "serial":
             return [("fwd+G_bwd", lin([(A, 0, -1), (W, 0, -1)]), M), ("D_bwd_top", lin([(B, 0, self._b_split)]), M),
                     ("D_bwd_rest", lin([(B, self._b_split, -1)]), M), ("adam_G", lin([(C, 0, self._c_split)]), M),
@@ -1112,7 +1261,7 @@ class HipEngine(HipEngineAux):
         step graphs write each gradient slice's bf16 image when the slice is final, RCCL reduces
         the image in place, Adam reads it (``adam_bf(gbf=...)``). Other schedules / dtypes use the
         reducer's own fp32 <-> bf16 copies around each collective."""
-        return (self.wire_d is not None and self._schedule() == "concurrent"
+        return (self.wire_d is not None and self._schedule() == "concurrent" and not self._sharded()
                 and os.environ.get("DCGAN_WIRE_DIRECT", "1") != "0")  # =0: the copying reducer (A/B)
 
     def _wire_cast(self, ex, name: str, streams) -> None:
@@ -1268,12 +1417,17 @@ class HipEngine(HipEngineAux):
         return (self._schedule() == "concurrent" and not (self.graph_enabled or self.graph_requested)
                 and self._g_split is not None)
 
-    def _g_chain_gw_alt(self, ex, cs):
+    def _g_chain_gw_alt(self, ex, cs, on_gd=None, sharded=False):
         """Segment "G_chain" with G's weight gradients on alt1 (_ddp_gw_alt), and the collective of
-        G's slice above g_h1 as soon as they are done."""
+        G's slice above g_h1 as soon as they are done. on_gd(mark): called with a mark on cs once
+        the g_loss pass is done with D's weights (progA[:_a_gd_end])."""
         A, W, a1 = self.progA, self.progW, ex.alt[1]
         a_need, wb, we = self._g_split[:3]
         pos, w = self._a_fwd, 0
+        if on_gd is not None:
+            ex.run(A, [cs, ex.side], pos, self._a_gd_end)
+            on_gd(ex.mark(cs))
+            pos = self._a_gd_end
         for a_end, w_end in self._g_w:
             if w_end > wb:
                 break
@@ -1285,8 +1439,11 @@ class HipEngine(HipEngineAux):
         # G's slice above g_h1 (g_h2's weights on: "gsplit_b") is final once these weight
         # gradients are: its collective goes out now, into the comm stream's idle gap after D's top
         # layer, instead of after the G chain
-        self._wire_cast(ex, "g_b", [a1])
-        self._ar_launch(ex, "gsplit_b", a1)
+        if sharded:
+            self._sh_rs(ex, "g_b", a1)
+        else:
+            self._wire_cast(ex, "g_b", [a1])
+            self._ar_launch(ex, "gsplit_b", a1)
         ex.run(A, [cs, ex.side], pos, a_need)
         ex.run(W, [cs, ex.side], wb, we)
         self._wire_cast(ex, "g_a", [cs, ex.side])
@@ -1325,6 +1482,9 @@ class HipEngine(HipEngineAux):
                 self._run_fused(ex, cs)
             else:
                 self._run_ddp(ex, cs)
+            return
+        if sch == "concurrent" and self._sharded():
+            self._run_sharded(ex, cs)
             return
         if sch == "concurrent":
             alt = ex.alt[0]
@@ -1420,6 +1580,10 @@ class HipEngine(HipEngineAux):
                 return D.GradAllReducer(t, mb, wd, stream=cs, force=True, wire=wire, prefilled=wire is not None,
                                         native=native)
 
+            if self._sharded():  # the conv kernels go through ShardReducers; the fp32-read slices:
+                for name, m, a, b in self._small:
+                    setattr(self, "_ar_" + name, mk((df if m == "d" else gf)[a:b]) if b > a else None)
+                return
             self._ar_dtop = mk(df[o:], wdf[o:] if direct else None)
             sch = self._schedule()
             self._ar_drest = mk(df[:o], wdf[:o] if direct else None)  # (also for graph-replayed segments)
@@ -1509,7 +1673,9 @@ class HipEngine(HipEngineAux):
         torch.cuda.synchronize(self.device)
 
     def sync_bn_state(self) -> None:
-        """Average BN moving averages over ranks (collective; see ReferenceEngine)."""
+        """Average BN moving averages over ranks (collective; see ReferenceEngine) -- and, after
+        sharded updates, gather the conv kernels' fp32 masters and Adam slots (checkpoints)."""
+        self.gather_sharded_state()
         D.all_reduce_mean_(self.model.g_bn.flat)
         D.all_reduce_mean_(self.model.d_bn.flat)
 

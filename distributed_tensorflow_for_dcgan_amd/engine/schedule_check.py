@@ -109,7 +109,8 @@ class RecordingExec:
         self._merge(self.vc[dst.name], token)
 
     def collective(self, reducer, stream: _S) -> None:
-        self._op(stream, "allreduce[%d elems]" % reducer.flat.numel(), reducer.accesses())
+        label = getattr(reducer, "label", None) or "allreduce[%d elems]" % reducer.flat.numel()
+        self._op(stream, label, reducer.accesses())
 
     def replay(self, graph, stream) -> None:  # graphs are never enabled in a dry run
         raise RuntimeError("graph replay in a recording executor")

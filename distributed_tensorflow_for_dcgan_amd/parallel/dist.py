@@ -299,6 +299,74 @@ class GradAllReducer:
             self.flat.mul_(1.0 / self.world)
 
 
+class ShardReducer:
+    """One gradient slice of the sharded update (ZeRO-1 style): ``rs()``
+    reduce-scatters the fp32 gradient slice (SUM) into this rank's shard ``gs`` (1/W of it); the
+    caller's Adam updates that shard of the fp32 masters / slots and writes its 16-bit weights into
+    ``agin``; ``ag()`` all-gathers ``agin`` from every rank into the mirror slice the GEMMs read.
+    Per rank that is (W-1)/W x (4 + 2) bytes per element on the wire instead of the all-reduce's
+    2 (W-1)/W x 4, at unchanged gradient precision, and 1/W of the Adam work. The slice length
+    must be a multiple of W (ParamSet's 64-element alignment covers W | 64)."""
+
+    def __init__(self, grad_slice: torch.Tensor, mirror_slice: torch.Tensor, world: Optional[int] = None,
+                 rank_: Optional[int] = None):
+        self.world = int(world or world_size())
+        self.rank = rank() if rank_ is None else int(rank_)
+        n = grad_slice.numel()
+        if n % self.world or mirror_slice.numel() != n:
+            raise ValueError("sharded slice of %d elements for %d ranks" % (n, self.world))
+        self.grad, self.mirror = grad_slice, mirror_slice
+        self.n = n // self.world
+        self.lo = self.rank * self.n  # this rank's shard inside the slice
+        self.gs = torch.empty(self.n, dtype=torch.float32, device=grad_slice.device)
+        self.agin = torch.empty(self.n, dtype=mirror_slice.dtype, device=grad_slice.device)
+        self.active = is_initialized()
+        self.rs_op, self.ag_op = _ShardOp(self, True), _ShardOp(self, False)
+
+    def rs(self) -> None:
+        if self.active:
+            dist.reduce_scatter_tensor(self.gs, self.grad, op=dist.ReduceOp.SUM)
+        else:  # no process group (dry runs / one process): the shard is the slice itself
+            self.gs.copy_(self.grad[self.lo:self.lo + self.n])
+
+    def ag(self) -> None:
+        if self.active:
+            dist.all_gather_into_tensor(self.mirror, self.agin)
+        else:
+            self.mirror[self.lo:self.lo + self.n].copy_(self.agin)
+
+
+class _ShardOp:
+    """The reduce-scatter or the all-gather half of a ShardReducer, as an executor collective
+    (``issue()`` on the current stream, ``accesses()`` for the schedule checker)."""
+
+    def __init__(self, r: ShardReducer, is_rs: bool):
+        self.r, self.is_rs = r, is_rs
+        self.label = "%s[%d elems]" % ("reduce_scatter" if is_rs else "all_gather", r.grad.numel())
+
+    def issue(self) -> None:
+        self.r.rs() if self.is_rs else self.r.ag()
+
+    def accesses(self):
+        r = self.r
+        if self.is_rs:
+            return [(r.grad.data_ptr(), r.grad.numel() * 4, False), (r.gs.data_ptr(), r.n * 4, True)]
+        es = r.mirror.element_size()
+        return [(r.agin.data_ptr(), r.n * es, False), (r.mirror.data_ptr(), r.mirror.numel() * es, True)]
+
+
+def gather_shards(flat: torch.Tensor, slices: Sequence[Tuple[int, int]]) -> None:
+    """All-gather every rank's shard of each [a, b) slice of a flat fp32 buffer (masters / Adam
+    slots after sharded updates) so that every rank holds the whole buffer again."""
+    if not is_initialized():
+        return
+    W, r = dist.get_world_size(), dist.get_rank()
+    for a, b in slices:
+        n = (b - a) // W
+        shard = flat[a + r * n:a + (r + 1) * n].clone()
+        dist.all_gather_into_tensor(flat[a:b], shard)
+
+
 class _nullctx:
     def __enter__(self):
         return self

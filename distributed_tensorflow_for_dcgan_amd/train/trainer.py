@@ -267,7 +267,9 @@ def run(flags: Flags, out=None) -> int:
             if chief and save_now:
                 ckpt.save(engine)
             if int(flags.check_sync_every) > 0 and world > 1 and step % int(flags.check_sync_every) == 0:
-                if not D.params_in_sync([engine.model.g.flat, engine.model.d.flat], device):
+                tens = (engine.sync_check_tensors() if hasattr(engine, "sync_check_tensors")
+                        else [engine.model.g.flat, engine.model.d.flat])
+                if not D.params_in_sync(tens, device):
                     raise RuntimeError("DDP divergence: parameters differ across ranks at step %d" % step)
             if fault_at >= 0 and step == fault_at:
                 emit(losslog.ready(flush=True))  # the last step lines before a crash are the useful ones

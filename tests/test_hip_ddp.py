@@ -41,6 +41,7 @@ def _run(eng):
     for _ in range(STEPS):
         eng.train_step()
     torch.cuda.synchronize()
+    eng.gather_sharded_state()  # (collective; sharded update: every rank's conv-kernel shards)
     return eng.model.d.flat.cpu(), eng.model.g.flat.cpu(), eng.global_step
 
 
@@ -86,6 +87,57 @@ def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
     d, g, _ = _run(eng)
     assert torch.equal(r0["d"], d), (r0["d"] - d).abs().max()
     assert torch.equal(r0["g"], g), (r0["g"] - g).abs().max()
+
+
+def _shard_worker(rank, world, port, out_dir, shard):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DCGAN_DIST_BACKEND"] = "gloo"
+    os.environ["DCGAN_DDP_SHARD"] = shard
+    torch.cuda.set_device(0)
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    from distributed_tensorflow_for_dcgan_amd.models.config import DCGANConfig
+    from distributed_tensorflow_for_dcgan_amd.parallel import dist as D
+    D.init_distributed(world, rank, torch.device("cuda", 0))
+    dev = torch.device("cuda", 0)
+    eng = HipEngine(DCGANConfig(output_size=64, c_dim=3), B, dev, seed=3, rank=rank, world=world, graph=False)
+    assert eng._sharded() == (shard == "1") and eng._schedule() == "concurrent"
+    for s in range(STEPS):  # rank-specific batches and z
+        eng.set_batch((torch.rand(B, 64, 64, 3, generator=torch.Generator().manual_seed(100 + 7 * s + rank)) * 2
+                       - 1).to(dev))
+        eng.train_step()
+    torch.cuda.synchronize()
+    mirrors = (eng.wbf_d.flat.cpu().clone(), eng.wbf_g.flat.cpu().clone())
+    eng.sync_bn_state()  # what the trainer runs before a checkpoint: gathers the sharded state
+    torch.save({"d": eng.model.d.flat.cpu(), "g": eng.model.g.flat.cpu(), "md": eng.opt_d.m.flat.cpu(),
+                "vg": eng.opt_g.v.flat.cpu(), "wd": mirrors[0], "wg": mirrors[1], "pd": eng.opt_d.powers.cpu(),
+                "step": eng.global_step, "L": eng.last_losses()}, os.path.join(out_dir, "s%s_%d.pt" % (shard, rank)))
+    D.barrier()
+    D.shutdown()
+
+
+def test_sharded_update_matches_allreduce_two_ranks(tmp_path):
+    """DDP default (eager segmented step, bf16): reduce-scatter the conv kernels' gradients, Adam
+    on this rank's half, all-gather the bf16 mirror. With DIFFERENT batches per rank, after 3 steps
+    and the pre-checkpoint gather, masters / Adam slots / mirrors / powers / losses equal the
+    all-reduce step's bit for bit (a two-rank fp32 sum is exact in either order), on both ranks;
+    before the gather the mirrors already agree."""
+    ctx = mp.get_context("spawn")
+    res = {}
+    for shard in ("1", "0"):
+        port = _free_port()
+        procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, str(tmp_path), shard)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=600)
+            assert p.exitcode == 0, "rank exited with %s" % p.exitcode
+        res[shard] = [torch.load(tmp_path / ("s%s_%d.pt" % (shard, r)), weights_only=True) for r in range(2)]
+    ref = res["0"][0]
+    for r in res["1"] + res["0"][1:]:
+        for k in ("d", "g", "md", "vg", "wd", "wg", "pd"):
+            assert torch.equal(r[k], ref[k]), (k, (r[k].float() - ref[k].float()).abs().max())
+        assert r["step"] == STEPS and r["L"] == ref["L"]
 
 
 def _real(rank):

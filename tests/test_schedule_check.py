@@ -104,6 +104,7 @@ def test_op_accesses_are_recorded():
 def test_adam_g_split_has_no_hazards(monkeypatch, split, wire):
     """Segmented DDP step with Adam over g_h1's slice right after its collective (and the rest of
     Adam(G) after the last one) -- and without the split: no unordered overlaps, any wire."""
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "0")  # the all-reduce segmented step
     monkeypatch.setenv("DCGAN_ADAM_G_SPLIT", split)
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False,
@@ -115,9 +116,10 @@ def test_adam_g_split_has_no_hazards(monkeypatch, split, wire):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
-def test_checker_finds_adam_g_a_before_its_collective():
+def test_checker_finds_adam_g_a_before_its_collective(monkeypatch):
     """Adam over g_h1's slice issued without waiting for that slice's collective: the checker
     reports the race on the gradient slice."""
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "0")  # the all-reduce segmented step
     eng = _dry(world=2)
     names = [n for n, _, _ in eng._segments()]
     assert names.index("adam_G_a") == 5
@@ -147,9 +149,10 @@ def test_checker_finds_adam_g_a_before_its_collective():
 
 
 @pytest.mark.parametrize("wire", ["fp32", "bf16"])
-def test_ddp_gw_alt_has_no_hazards(wire):
+def test_ddp_gw_alt_has_no_hazards(monkeypatch, wire):
     """The segmented DDP step with G's weight gradients (but g_h1's) on the idle alt1 stream as
     soon as their operands exist; any wire."""
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "0")  # the all-reduce segmented step
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False,
                     allreduce_dtype=wire)
@@ -163,6 +166,7 @@ def test_ddp_gw_alt_has_no_hazards(wire):
 def test_checker_finds_ddp_g_bucket_before_the_alt1_weight_gradients(monkeypatch):
     """G's slice above g_h1 put on the wire from cs instead of from alt1 (i.e. without waiting
     for the weight gradients running there): the checker reports the race."""
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "0")  # the all-reduce segmented step
     eng = _dry(world=2)
     orig = eng._ar_launch
 
@@ -245,9 +249,10 @@ def test_fused_g_wgrad_place_rejects_bad_values(monkeypatch):
 
 
 
-def test_checker_finds_an_early_g_bucket():
+def test_checker_finds_an_early_g_bucket(monkeypatch):
     """Segmented DDP: issuing the all-reduce of g_h1's slice before the G chain segment that
     computes its weight gradient is a race the checker reports."""
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "0")  # the all-reduce segmented step
     eng = _dry(world=2)
 
     def early(ex):
@@ -278,7 +283,8 @@ def test_bf16_wire_schedules_have_no_hazards(dtype, schedule):
     assert hz == [], "\n".join(map(str, hz[:10]))
 
 
-def test_bf16_wire_direct_path_is_used():
+def test_bf16_wire_direct_path_is_used(monkeypatch):
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "0")  # the all-reduce segmented step
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
     eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=2, dry_run=True, graph=False, allreduce_dtype="bf16")
     assert eng._schedule() == "concurrent" and eng._wire_direct()
@@ -292,3 +298,49 @@ def test_bf16_wire_direct_path_is_used():
 
 
 
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_update_is_the_bf16_ddp_default_and_hazard_free(world):
+    """Segmented DDP step, bf16, eager: the conv kernels go reduce-scatter -> Adam on 1/W ->
+    all-gather of the bf16 mirror (4 slices), the fp32-read tensors through two all-reduces."""
+    from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=world, dry_run=True, graph=False)
+    assert eng._sharded() and sorted(eng._shards) == ["dw_rest", "dw_top", "g_a", "g_b"]
+    assert [n for n, _, _, _ in eng._small] == ["d_small", "g_c"]
+    for name, (sr, m, a, b) in eng._shards.items():
+        assert sr.n * world == b - a and sr.lo == 0
+    hz, n = SC.check_engine(eng)
+    assert n > 100 and hz == [], "\n".join(map(str, hz[:10]))
+
+
+def test_checker_finds_the_top_kernel_gather_before_its_last_reader():
+    """The top D kernel's Adam + all-gather must follow the D chain's top-layer data gradient
+    (it reads the old bf16 mirror): issued right after its reduce-scatter, the checker reports it."""
+    eng = _dry(world=2)
+    assert eng._sharded()
+
+    def early(ex):
+        cs, alt = ex.main(), ex.alt[0]
+        eng._seg(ex, 0, cs)
+        ex.wait(alt, cs)
+        eng._seg(ex, 1, alt)
+        eng._sh_rs(ex, "dw_top", alt)
+        eng._sh_update(ex, "dw_top")          # too early: the top-layer dgrad has not run
+        eng._g_chain_gw_alt(ex, cs, sharded=True)
+        eng._sh_rs(ex, "g_a", cs)
+        eng._sh_update(ex, "g_b")
+        ex.run(eng.progB, ex.alt, eng._b_split, -1)
+        eng._sh_rs(ex, "dw_rest", alt)
+        eng._sh_update(ex, "dw_rest")
+        eng._ar_launch(ex, "d_small", alt)
+        eng._g_tail_gw_alt(ex, cs)
+        eng._ar_launch(ex, "g_c", cs)
+        eng._sh_update(ex, "g_a")
+        eng._ar_join(ex, cs)
+        ex.wait(cs, alt)
+        eng._seg(ex, 5, cs)
+
+    eng._run_step = early
+    hz, _ = SC.check_engine(eng)
+    assert any("all_gather" in h.a or "all_gather" in h.b for h in hz), "\n".join(map(str, hz[:10]))
