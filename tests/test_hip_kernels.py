@@ -240,8 +240,54 @@ def test_igemm3_deconv_and_dgrad_layouts(B, Hi, Ho, Ci, Co):
             close(out, gx, 2e-3, "G dgrad cfg%d s%d" % (cfg, splits))
 
 
+HALO = [300, 303, 304, 305, 310, 313, 314, 315]
+
+
+@pytest.mark.parametrize("B,Hi,Ci,Co", [(8, 4, 512, 256), (4, 8, 256, 128), (2, 16, 128, 64), (1, 32, 64, 64),
+                                        (2, 32, 128, 128)])
+def test_igemm3_halo_deconv(B, Hi, Ci, Co):
+    """Halo K loop (input window of a phase tile staged once per 64-channel chunk, taps read it at
+    their shift): the 64x64 ladder's deconv shapes (whole images per tile at 4x4 / 8x8, whole rows
+    at 16x16 / 32x32), every halo tile / ring depth that takes the shape, split-K over chunks,
+    bias, against the fp32 reference; splits bitwise reproducible; shapes whose window does not
+    fit are refused by both the Python policy and the C++ check."""
+    h = H()
+    Ho = 2 * Hi
+    x = bf(rnd(B, Hi, Hi, Ci, seed=242))
+    w = bf(rnd(5, 5, Co, Ci, scale=0.05, seed=243))
+    bias = rnd(Co, scale=0.1, seed=244)
+    ref = R.conv2d_transpose_same(x.float(), w.float(), (Ho, Ho), bias)
+    ran = 0
+    for cfg in HALO:
+        for splits in (1, 2, 4):
+            ok = h.halo_ok(cfg, 1, B, Ho, Ho, Ci, False, splits)
+            if not ok:
+                if splits == 1:
+                    with pytest.raises(RuntimeError):
+                        h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True,
+                                                cfg=cfg, splits=splits)
+                continue
+            y = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True, cfg=cfg,
+                                        splits=splits)
+            close(y, ref, 2e-3, "halo deconv cfg%d s%d" % (cfg, splits))
+            if splits > 1:
+                y2 = h.conv2d_transpose_same(x, w.reshape(25, Co, Ci), Co, (Ho, Ho), bias=bias, out_f32=True, cfg=cfg,
+                                             splits=splits)
+                assert torch.equal(y, y2), "nondeterministic cfg%d s%d" % (cfg, splits)
+            ran += 1
+    assert ran >= 4
+
+
+@pytest.mark.parametrize("cfg", [303, 305, 313, 315])
+def test_igemm3_halo_bn_backward_stats(cfg):
+    """The halo K loop feeding the fused BN-backward statistics store pass (D's data gradients);
+    its chunk-major k order rounds differently from the tap-major loops, so the stored gradient is
+    compared with the same cfg's plain GEMM."""
+    test_igemm_fused_bn_backward_stats(cfg, ref_cfg=cfg)
+
+
 @pytest.mark.parametrize("cfg", [200, 211, 213, 206, 216, 217, 218])
-def test_igemm_fused_bn_backward_stats(cfg):
+def test_igemm_fused_bn_backward_stats(cfg, ref_cfg=200):
     """Data-gradient GEMM with the BN-backward statistics fused into its store pass (epilogue.h
     vec_store_bnb): stored dL/da == the plain GEMM's, partials sum to (sum g, sum g * xhat) with
     g = dL/da * lrelu'(y), for 4- and 8-wave igemm3 tiles."""
@@ -258,7 +304,7 @@ def test_igemm_fused_bn_backward_stats(cfg):
         pytest.skip("tile has no LDS for the fused statistics")
     bm = h.tile_of(cfg)[0]
     mph = B * Hi * Hi
-    da_ref = h.conv2d_transpose_same(dy, w, Co, (Ho, Ho), cfg=200)
+    da_ref = h.conv2d_transpose_same(dy, w, Co, (Ho, Ho), cfg=ref_cfg)
     da = torch.empty_like(da_ref)
     mt = -(-mph // bm)
     st = torch.empty(mt * 4, 2, Co, device=dev)
