@@ -293,6 +293,20 @@ class Program {
       k.oy_off = q.oy_off; k.ox_off = q.ox_off; k.ntaps = q.ntaps; k.fd_hw = q.fd_hw; k.fd_w = q.fd_w;
       for (int t = 0; t < 25; ++t) k.tap[t] = q.tap[t];
     }
+    if (cfg >= 300) {
+      // halo K loop (igemm3.hip PP == 2): deconv phases, k-contiguous weights, whole 64-channel
+      // chunks (split-K over chunks); every phase tile covers whole images or whole rows of one
+      // image, and its input window (every tap's rows) fits the 224-pixel buffer (HALO_WPW x 4 x 8)
+      if (mode != 1 || bkn || Kc % 64 || splits > Kc / 64)
+        throw std::runtime_error("igemm halo cfg: deconv mode, k-contiguous weights, Kc % 64, splits <= Kc / 64");
+      for (auto& q : ph) {
+        const int hw = q.Hq * q.Wq;
+        const bool whole = bm % hw == 0, rows = hw % bm == 0 && bm % q.Wq == 0;
+        const int nimg = whole ? bm / hw : 1, R = whole ? q.Hq : bm / std::max(1, q.Wq);
+        if ((!whole && !rows) || nimg * (R + 2) * (q.Wq + 2) > 224)
+          throw std::runtime_error("igemm halo cfg: phase tile is not whole images / rows, or its window exceeds 224 pixels");
+      }
+    }
     int maxM = 0;
     for (auto& p : ph) maxM = std::max(maxM, p.M);
     const int mtiles = (maxM + bm - 1) / bm, ntiles = (N + bn - 1) / bn;

@@ -72,6 +72,15 @@ __device__ __forceinline__ void wait_vmcnt_n(int n) {
   wait_vmcnt<0>();
 }
 
+// vmcnt(n * L + X): the younger weight tiles plus the next chunk's X window pieces (halo K loop)
+template <int L, int NMAX, int X>
+__device__ __forceinline__ void wait_vmcnt_win(int n) {
+  if constexpr (NMAX >= 3) { if (n >= 3) { wait_vmcnt<3 * L + X>(); return; } }
+  if constexpr (NMAX >= 2) { if (n >= 2) { wait_vmcnt<2 * L + X>(); return; } }
+  if constexpr (NMAX >= 1) { if (n >= 1) { wait_vmcnt<L + X>(); return; } }
+  wait_vmcnt<X>();
+}
+
 __device__ __forceinline__ void pp_barrier() {
   // a raw s_barrier pinned in place: no MFMA / ds_read may be scheduled across it (hipcc moves
   // register-only MFMAs past an asm statement otherwise), and no vmcnt drain (the LDS-DMA of
@@ -87,6 +96,20 @@ template <int BM, int BN, int WM, int NS>
 constexpr int igemm3_lds_bytes() {
   constexpr int ring = NS * (BM + BN) * 128, epi = (BM + 2 * WM * BN) * 4 + BM * (BN + 8) * 2;
   return ring > epi ? ring : epi;
+}
+
+// HALO K loop (PP == 2; deconv phases, k-contiguous weights): the window of input pixels under a
+// phase tile (every tap's rows) is staged ONCE per 64-channel chunk, double-buffered, and each tap
+// reads its A fragments from it at the tap's (dy, dx) shift; only the weight tile is loaded per
+// tap. Window capacity: HALO_WPW 1 KiB pieces (8 pixels) per wave.
+constexpr int HALO_WPW = 7;
+
+template <int BM, int BN, int WM, int WN, int NS>
+constexpr int igemm3_halo_lds() {
+  constexpr int win = HALO_WPW * WM * WN * 8 * 128;  // one window buffer
+  constexpr int ops = 2 * win + NS * BN * 128;
+  constexpr int epi = (BM + 2 * WM * BN) * 4 + BM * (BN + 8) * 2;
+  return ops > epi ? ops : epi;
 }
 
 template <int BM, int BN, int WM, int WN, int BKN, int NS, int PL, int PP = 0>
@@ -235,7 +258,112 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
         acc[i][j] = DCG_MFMA_16x16x32(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
   };
 
-  if constexpr (PP) {
+  if constexpr (PP == 2) {
+    // ================================================================ halo K loop (deconv phases)
+    static_assert(!BKN && !PL, "halo: k-contiguous weights, conv / deconv modes");
+    constexpr int WPIX = HALO_WPW * NW * 8;              // window capacity (pixels)
+    constexpr int WBUF = WPIX * 128;                     // bytes per window buffer
+    const uint32_t ring_base = lds_base + 2 * WBUF;      // B ring after the two window buffers
+    // tile geometry (host-checked): whole images (BM % (Hq Wq) == 0) or whole rows of one image
+    const int Hq = ph.Hq, Wq = ph.Wq, HW = Hq * Wq, WC = Wq + 2;
+    const int nimg = BM >= HW ? BM / HW : 1, R = BM >= HW ? Hq : BM / Wq, WR = R + 2;
+    const int b0 = m0 / HW, qy0 = BM >= HW ? 0 : (m0 - b0 * HW) / Wq;
+    const int npix = nimg * WR * WC;
+    // per-lane window pieces (chunk-invariant byte offsets; invalid pixels -> zero fill)
+    uint32_t w_off[HALO_WPW];
+#pragma unroll
+    for (int j = 0; j < HALO_WPW; ++j) {
+      const int px = 8 * (wave + NW * j) + (lane >> 3);
+      const int img = px / (WR * WC), rem = px - img * (WR * WC);
+      const int wr = rem / WC, wc = rem - wr * WC;
+      const int iy = qy0 + wr - 2 + ph.iy0_off, ix = wc - 2 + ph.ix0_off;
+      const bool ok = px < npix && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && b0 + img < p.Bn;
+      const int gch = (lane & 7) ^ (px & 7);  // 16-byte slot lane&7 of the LDS row holds chunk gch
+      w_off[j] = oob_unless(ok, (uint32_t)((((b0 + img) * p.H + iy) * p.W + ix) * Kc + gch * 8) * 2u);
+    }
+    // A fragment rows of this lane: window pixel of tap (0, 0)
+    int pb[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * TM + i * 16 + fr;
+      const int img = BM >= HW ? r / HW : 0, rem = r - img * HW;
+      const int rr = rem / Wq, cc = rem - rr * Wq;
+      pb[i] = img * WR * WC + (rr + 2) * WC + cc + 2;
+    }
+    // k-steps: (chunk c, tap t), chunk-major; this split's chunks [c_lo, c_hi)
+    const int nch = Kc / BK, ntp = ph.ntaps;
+    const int cps = (nch + S - 1) / S;
+    const int c_lo = split * cps, c_hi = min(nch, c_lo + cps);
+    const int nsteps = max(0, c_hi - c_lo) * ntp;
+    auto issue_win = [&](int c) {
+      const uint32_t wb = lds_base + (c & 1) * WBUF;
+#pragma unroll
+      for (int j = 0; j < HALO_WPW; ++j) dma16_asm_la(ra, wb + (wave + NW * j) * 1024, w_off[j] + (uint32_t)(c * BK) * 2u);
+    };
+    auto issue_b = [&](int st) {  // weight tile of step st (local index) into ring slot st % NS
+      const int c = c_lo + st / ntp, t = st - (st / ntp) * ntp;
+      const int wt = ph.tap[t] >> 16;
+      const uint32_t sb = ring_base + (st % NS) * B_BYTES;
+#pragma unroll
+      for (int i = 0; i < PPW_B; ++i) {
+        const int q = wave + NW * i;
+        const int n = n0 + 8 * q + (lane >> 3);
+        const int cch = c * BK + a_chunk * 8;
+        dma16_asm_la(rb, sb + q * 1024, oob_unless(n < N, (uint32_t)((wt * N + n) * Kc + cch) * 2u));
+      }
+    };
+    if (nsteps > 0) {
+      issue_win(c_lo);
+#pragma unroll
+      for (int st = 0; st < NS - 1; ++st)
+        if (st < nsteps) issue_b(st);
+    }
+    for (int st = 0; st < nsteps; ++st) {
+      const int cl = st / ntp, t = st - cl * ntp, c = c_lo + cl;
+      // B(st) landed: the younger B tiles stay in flight, and -- on the last NS - 2 taps of a chunk
+      // -- the next chunk's window, issued right before the next chunk's first weight tile
+      const int ny = min(NS - 2, nsteps - 1 - st);
+      const bool wy = NS > 2 && t >= ntp - NS + 2 && c + 1 < c_hi;
+      if (wy) wait_vmcnt_win<PPW_B, NS - 2, HALO_WPW>(ny);
+      else wait_vmcnt_n<PPW_B, NS - 2>(ny);
+      asm volatile("s_barrier" ::: "memory");
+      if (st + NS - 1 < nsteps) {
+        // the next chunk's window goes out just before that chunk's first weight tile (its buffer
+        // was last read in chunk c - 1: every wave is past this step's barrier)
+        if ((st + NS - 1) % ntp == 0) issue_win(c + 1);
+        issue_b(st + NS - 1);
+      }
+      const int ti = ph.tap[t];
+      const int dy = (int)(signed char)(ti & 0xff), dx = (int)(signed char)((ti >> 8) & 0xff);
+      const lds_char* wbuf = lds3 + (c & 1) * WBUF;
+      const lds_char* sb = lds3 + 2 * WBUF + (st % NS) * B_BYTES;
+      const int sh = dy * WC + dx;
+      elem8 af[2][FM], bfr[2][FN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cq = ks * 4 + fq;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int px = pb[i] + sh;
+          af[ks][i] = *reinterpret_cast<const __attribute__((address_space(3))) elem8*>(wbuf + px * 128 + ((cq ^ (px & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * TN + j * 16 + fr;
+          bfr[ks][j] = *reinterpret_cast<const __attribute__((address_space(3))) elem8*>(sb + r * 128 + ((cq ^ (r & 7)) << 4));
+        }
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = DCG_MFMA_16x16x32(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else if constexpr (PP == 1) {
     // ================================================================ ping-pong K loop
     // 8 waves in two groups of 4 (G0 = waves 0-3 = the tile's first BM/2 rows, G1 = the rest);
     // waves w and w + 4 share a SIMD. Every k-tile t is two barrier-separated phases:
@@ -552,7 +680,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   float* red = reinterpret_cast<float*>(lds) + BM;
   constexpr int CPAD = BN + 8;
   elem_t* ctile = reinterpret_cast<elem_t*>(reinterpret_cast<float*>(lds) + BM + 2 * WM * BN);
-  constexpr int LDS_TOTAL = igemm3_lds_bytes<BM, BN, WM, NS>();
+  constexpr int LDS_TOTAL = PP == 2 ? igemm3_halo_lds<BM, BN, WM, WN, NS>() : igemm3_lds_bytes<BM, BN, WM, NS>();
   static_assert((BM + 2 * WM * BN) * 4 + BM * CPAD * 2 <= LDS_TOTAL, "epilogue LDS");
   for (int r = tid; r < BM; r += NT) {
     const int m = m0 + r;
@@ -643,7 +771,19 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
 
 static constexpr int kIgemm3Stages[6] = {3, 2, 4, 5, 3, 2};
 
+// halo K loop configs (deconv phases, k-contiguous weights): cfg 300 + 10 k + id, NS = {3, 2}[k],
+// 4-wave tiles only (id 0 / 3 / 4 / 5: 128x128, 128x64, 64x128, 64x64)
+static bool igemm3_halo_cfg(int cfg) { return cfg >= 300 && cfg < 320 && (cfg % 10 == 0 || (cfg % 10 >= 3 && cfg % 10 <= 5)); }
+
 extern "C" int DCG_API(dcg_igemm3_tile)(int cfg, int* bm, int* bn, int* ns) {
+  if (igemm3_halo_cfg(cfg)) {
+    const int id = cfg % 10;
+    *ns = cfg < 310 ? 3 : 2;
+    *bm = (id == 0 || id == 3) ? 128 : 64;
+    *bn = (id == 0 || id == 4) ? 128 : 64;
+    const size_t win = (size_t)dcg::HALO_WPW * 4 * 8 * 128, epi = (*bm + 2 * 2 * *bn) * 4 + *bm * (*bn + 8) * 2;
+    return std::max(2 * win + (size_t)*ns * *bn * 128, epi) <= 160 * 1024 ? 0 : -1;
+  }
   if (cfg < 200 || cfg >= 260) return -1;
   const int id = cfg % 10;
   if (cfg >= 240 && id < 6) return -1;  // ping-pong: 8-wave tiles only
@@ -674,9 +814,16 @@ static int launch_k(K k, size_t shm, unsigned blocks, unsigned threads, const dc
 
 template <int BM, int BN, int WM, int WN, int BKN, int NS, int PP>
 static int launch3(const dcg::IGemmArgs* a, unsigned blocks, hipStream_t s) {
-  constexpr size_t shm = (size_t)dcg::igemm3_lds_bytes<BM, BN, WM, NS>();
+  constexpr size_t shm = PP == 2 ? (size_t)dcg::igemm3_halo_lds<BM, BN, WM, WN, NS>()
+                                 : (size_t)dcg::igemm3_lds_bytes<BM, BN, WM, NS>();
   constexpr unsigned nt = 64 * WM * WN;
-  if constexpr (PP) {
+  if constexpr (PP == 2) {
+    if constexpr (WM * WN == 4 && !BKN && shm <= 160 * 1024) {
+      if (a->plain || a->Kc % 64) return -1;
+      return launch_k(dcg::igemm3_kernel<BM, BN, WM, WN, 0, NS, 0, 2>, shm, blocks, nt, a, s);
+    }
+    return -1;
+  } else if constexpr (PP) {
     if constexpr (WM * WN == 8) {
       if (a->plain || a->Kc % 64) return -1;  // conv / deconv with whole 64-channel k-tiles only
       return launch_k(dcg::igemm3_kernel<BM, BN, WM, WN, BKN, NS, 0, 1>, shm, blocks, nt, a, s);
@@ -712,6 +859,15 @@ extern "C" int DCG_API(dcg_igemm3_launch)(const dcg::IGemmArgs* a, int cfg, int 
   int bm, bn, ns;
   if (DCG_API(dcg_igemm3_tile)(cfg, &bm, &bn, &ns)) return -1;
   const int id = cfg % 10;
+  if (igemm3_halo_cfg(cfg)) {
+    if (bkn) return -1;
+#define XH(id_, BM_, BN_)                                                                          \
+    if (id == id_) return ns == 3 ? launch3<BM_, BN_, 2, 2, 0, 3, 2>(a, blocks, s)                  \
+                                  : launch3<BM_, BN_, 2, 2, 0, 2, 2>(a, blocks, s);
+    XH(0, 128, 128) XH(3, 128, 64) XH(4, 64, 128) XH(5, 64, 64)
+#undef XH
+    return -1;
+  }
   const bool pp = cfg >= 240;
 #define X(id_, BM_, BN_, WM_, WN_)                                                              \
   if (id == id_) {                                                                              \

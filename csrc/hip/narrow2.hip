@@ -320,25 +320,34 @@ __global__ __launch_bounds__(256) void nwgrad_kernel(NWGradArgs p) {
 
   u32x4 dv[NWG_PX * 8 / 256];  // 8 x 16 B of the next D tile
   elem_t xv[NWG_WPT][CIN];
+  // chunk-invariant addressing, computed once (round 6: the per-chunk divisions by Wd / wcols and
+  // bounds selects were most of the kernel's VALU, 13.8 VALU per MFMA in profiles/pmc/step_pmc_r5b.txt):
+  // a chunk's D tile is tyc full rows = one contiguous block; window pixel s sits at row wr(s),
+  // column wc(s) of every chunk's window, only the window's first input row changes per chunk
+  int w_off[NWG_WPT], w_row[NWG_WPT];
+#pragma unroll
+  for (int i = 0; i < NWG_WPT; ++i) {
+    const int s_ = tid + 256 * i;
+    const int wr = s_ / p.wcols, wc = s_ - wr * p.wcols, ix = wc - p.pl;
+    const bool col_ok = s_ < zero_pix && (unsigned)ix < (unsigned)p.W;
+    w_row[i] = col_ok ? wr : -(1 << 20);  // an invalid column fails every row test below
+    w_off[i] = (wr * p.W + ix) * CIN;
+  }
   auto fetch = [&](int y0) {
     const elem_t* dsrc = p.d + ((size_t)b * p.Hd + y0) * p.Wd * 64;
+    const int lim = min(p.tyc, p.Hd - y0) * p.Wd * 64;  // elements of the chunk inside the image
 #pragma unroll
     for (int i = 0; i < NWG_PX * 8 / 256; ++i) {
-      const int qd = tid + 256 * i, px = qd >> 3, j = qd & 7;
-      const int yy = px / p.Wd;
-      const bool ok = px < p.np && y0 + yy < p.Hd;
-      dv[i] = ok ? *reinterpret_cast<const u32x4*>(dsrc + (size_t)px * 64 + 8 * j) : (u32x4){0u, 0u, 0u, 0u};
+      const int e0 = (tid + 256 * i) * 8;
+      dv[i] = e0 < lim ? *reinterpret_cast<const u32x4*>(dsrc + e0) : (u32x4){0u, 0u, 0u, 0u};
     }
     const int iy0 = 2 * y0 - p.pl;
-#pragma unroll
+    const long long xbase = ((long long)b * p.H + iy0) * p.W * CIN;  // (row iy0 may be -1 / -2: only
+#pragma unroll                                                          //  valid rows are read)
     for (int i = 0; i < NWG_WPT; ++i) {
-      const int s = tid + 256 * i;
-      const int wr = s / p.wcols, wc = s - wr * p.wcols;
-      const int iy = iy0 + wr, ix = wc - p.pl;
-      const bool ok = s < zero_pix && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-      const elem_t* src = p.x + (((size_t)b * p.H + (ok ? iy : 0)) * p.W + (ok ? ix : 0)) * CIN;
+      const bool ok = (unsigned)(iy0 + w_row[i]) < (unsigned)p.H;
 #pragma unroll
-      for (int cc = 0; cc < CIN; ++cc) xv[i][cc] = ok ? src[cc] : (elem_t)0.f;
+      for (int cc = 0; cc < CIN; ++cc) xv[i][cc] = ok ? p.x[xbase + w_off[i] + cc] : (elem_t)0.f;
     }
   };
   auto commit = [&]() {

@@ -78,9 +78,48 @@ IGEMM3_WM = {0: 2, 1: 4, 2: 1, 3: 2, 4: 2, 5: 2, 6: 4, 7: 2, 8: 8, 9: 4}  # wave
 IGEMM3_STAGES = (3, 2, 4, 5, 3, 2)
 
 
+# halo K loop (igemm3.hip PP == 2, cfg 300 + 10 k + id, NS = (3, 2)[k], 4-wave tiles 0 / 3 / 4 / 5):
+# deconv phases with the input window of a phase tile staged once per 64-channel chunk
+HALO_IDS = (0, 3, 4, 5)
+HALO_PIXELS = 224  # window buffer capacity (igemm3.hip HALO_WPW x 4 waves x 8 pixels)
+
+
+def is_halo(cfg: int) -> bool:
+    return 300 <= cfg < 320 and cfg % 10 in HALO_IDS
+
+
+def igemm3_ns(cfg: int) -> int:
+    if cfg >= 300:
+        return 3 if cfg < 310 else 2
+    return IGEMM3_STAGES[(cfg - 200) // 10]
+
+
+def halo_ok(cfg: int, mode: int, Bn: int, Hout: int, Wout: int, Kc: int, bkn: bool = False, splits: int = 1) -> bool:
+    """Whether a halo cfg can run this GEMM (mirrors csrc/bindings.cpp igemm_ex): a deconv with
+    k-contiguous weights, whole 64-channel chunks (split-K over chunks), every phase tile covering
+    whole images or whole rows of one image with an input window of <= HALO_PIXELS pixels."""
+    if not is_halo(cfg) or mode != 1 or bkn or Kc % 64 or splits > Kc // 64:
+        return False
+    bm = IGEMM3_TILES[cfg % 10][0]
+    for py in (0, 1):
+        for px in (0, 1):
+            Hq, Wq = (Hout - py + 1) // 2, (Wout - px + 1) // 2
+            hw = Hq * Wq
+            if hw <= 0:
+                continue
+            whole, rows = bm % hw == 0, hw % bm == 0 and bm % Wq == 0
+            nimg, R = (bm // hw, Hq) if whole else (1, bm // max(1, Wq))
+            if not (whole or rows) or nimg * (R + 2) * (Wq + 2) > HALO_PIXELS:
+                return False
+    return True
+
+
 def igemm3_pp_ok(cfg: int, mode: int, Kc: int) -> bool:
     """Whether igemm3 cfg can run this GEMM: the ping-pong configs (240..259) need an 8-wave tile
-    and whole 64-channel k-tiles of a conv / deconv (no im2col plain mode)."""
+    and whole 64-channel k-tiles of a conv / deconv (no im2col plain mode); the halo configs
+    (300..319) are checked with the full geometry by halo_ok."""
+    if cfg >= 300:
+        return is_halo(cfg) and mode == 1 and Kc % 64 == 0
     if cfg < 240:
         return True
     return cfg % 10 in IGEMM3_WAVES and mode != 2 and Kc % 64 == 0
@@ -89,7 +128,9 @@ def igemm3_pp_ok(cfg: int, mode: int, Kc: int) -> bool:
 def igemm3_lds(cfg: int) -> int:
     """Operand-ring bytes of igemm3 cfg (the launch adds room when the epilogue needs more)."""
     bm, bn = IGEMM3_TILES[cfg % 10]
-    return IGEMM3_STAGES[(cfg - 200) // 10] * (bm + bn) * 128
+    if cfg >= 300:
+        return 2 * HALO_PIXELS * 128 + igemm3_ns(cfg) * bn * 128
+    return igemm3_ns(cfg) * (bm + bn) * 128
 
 
 # fp32 build (igemm_f32.hip): the only tile family of that element type, cfg 200..203
@@ -127,11 +168,11 @@ def bnb_fits(cfg: int) -> bool:
     bm, bn = tile_of(cfg)
     if cfg < 200:
         return (bm + 8 * bn) * 4 + bm * (bn + 8) * 2 + 16384 <= 2 * (bm + bn) * 128
-    ns = IGEMM3_STAGES[(cfg - 200) // 10]
     nt = 64 * IGEMM3_WAVES.get(cfg % 10, 4)
     wm = IGEMM3_WM[cfg % 10]
-    # igemm3: the row-lane scratch may alias the C tile (the store pass has read it by then)
-    lds = max(ns * (bm + bn) * 128, (bm + 2 * wm * bn) * 4 + bm * (bn + 8) * 2)  # igemm3_lds_bytes
+    # igemm3: the row-lane scratch may alias the C tile (the store pass has read it by then);
+    # (halo tiles have more LDS than this ring estimate, as csrc/bindings.cpp assumes too)
+    lds = max(igemm3_ns(cfg) * (bm + bn) * 128, (bm + 2 * wm * bn) * 4 + bm * (bn + 8) * 2)
     return (bm + 2 * wm * bn) * 4 + max(bm * (bn + 8) * 2, 64 * nt) <= lds
 
 
@@ -229,6 +270,8 @@ def igemm_cfg_for(mode: int, Bn: int, Hin: int, Win: int, Kc: int, Hout: int, Wo
     if ent is not None:
         cfg, sp = ent
         ok = (cfg >= 200 and igemm3_pp_ok(cfg, mode, Kc)) or (not bkn and sp == 1 and cfg % 100 in IGEMM_CFGS)
+        if cfg >= 300:
+            ok = halo_ok(cfg, mode, Bn, Hout, Wout, Kc, bkn, sp)
         if ok and (rows_per_group is None or rows_per_group % tile_of(cfg)[0] == 0):
             return cfg, sp
     if N % 8 == 0 and N >= 64:
