@@ -82,6 +82,11 @@ def candidates(mode, Bn, Hout, Wout, Kc, N, bkn):
             if sp > 1 and tiles >= 1024:
                 continue
             out.append((c, sp))
+    if mode == 1 and not bkn:  # the halo K loop (deconv phases): split-K over 64-channel chunks
+        for c in range(300, 320):
+            for sp in (1, 2, 4):
+                if H.halo_ok(c, mode, Bn, Hout, Wout, Kc, False, sp):
+                    out.append((c, sp))
     return out
 
 
