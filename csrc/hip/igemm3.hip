@@ -150,7 +150,9 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
   if (p.lpt && p.nphases > 1) {
     // longest processing time first: the phases (host-sorted, most taps first) are dispatched one
     // after the other, so the short phases fill in at the end; within a phase the same bijective
-    // XCD remap (the blocks of one XCD get a contiguous run of that phase's tiles)
+    // remap over the phase-local index u. The hardware XCD is blockIdx.x & 7, which equals u & 7
+    // only when T1 is a multiple of 8; otherwise a phase >= 1 sees its runs on rotated XCDs (still
+    // one contiguous run per residue class, so per-XCD L2 locality holds only approximately there)
     const int T1 = p.mtiles * ntn * S;
     phase = t / T1;
     int u = t - phase * T1;

@@ -18,3 +18,4 @@ for i in 1 2 3; do
   done
   r=$(timeout -k 10 120 python bench.py --steps 200 --warmup 20 2>/dev/null) || exit 1; echo "[fused] ${r:70:40}"
 done | tee gpurun_out/ab_ddp_shard_w1_r6.txt
+./scripts/gpu_ab_vals.sh DCGAN_GW_PLACE "aaaa aaac aaas"

@@ -118,7 +118,7 @@ def _shard_worker(rank, world, port, out_dir, shard):
 
 def test_sharded_update_matches_allreduce_two_ranks(tmp_path):
     """DDP default (eager segmented step, bf16): reduce-scatter the conv kernels' gradients, Adam
-    on this rank's half, all-gather the bf16 mirror. With DIFFERENT batches per rank, after 3 steps
+    on this rank's half, all-gather the bf16 mirror. With DIFFERENT batches per rank, after 4 steps
     and the pre-checkpoint gather, masters / Adam slots / mirrors / powers / losses equal the
     all-reduce step's bit for bit (a two-rank fp32 sum is exact in either order), on both ranks;
     before the gather the mirrors already agree."""
@@ -137,7 +137,9 @@ def test_sharded_update_matches_allreduce_two_ranks(tmp_path):
     for r in res["1"] + res["0"][1:]:
         for k in ("d", "g", "md", "vg", "wd", "wg", "pd"):
             assert torch.equal(r[k], ref[k]), (k, (r[k].float() - ref[k].float()).abs().max())
-        assert r["step"] == STEPS and r["L"] == ref["L"]
+        assert r["step"] == STEPS
+    for rank in range(2):  # the losses are rank-local (each rank's own batch)
+        assert res["1"][rank]["L"] == res["0"][rank]["L"], rank
 
 
 def _real(rank):
