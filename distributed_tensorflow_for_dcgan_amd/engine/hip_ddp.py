@@ -5,13 +5,16 @@ The reference trains asynchronously through a gRPC parameter server (``image_tra
 RCCL on a comm stream while both backward chains keep running:
 
   "concurrent"  the step cut into segments (forward, D chain top / rest, G chain / tail, update) with
-                the collectives issued between them -- by default the SHARDED update for the bf16
-                engine (``_run_sharded``): the conv kernels' gradients are reduce-scattered, each rank
+                per-slice all-reduces issued between them (fp32, or a copy-free bf16 wire) and Adam
+                after them. DCGAN_DDP_SHARD=1 (bf16 engine, eager replay): the SHARDED update
+                (``_run_sharded``) -- the conv kernels' gradients are reduce-scattered, each rank
                 runs Adam on its 1/W shard on the comm stream and the bf16 mirror is all-gathered
                 (0.75x the all-reduce's wire bytes at fp32 gradient precision, 1/W of the Adam
                 work); the tensors the step reads in fp32 (biases, BN, linear layers) are
-                all-reduced. DCGAN_DDP_SHARD=0 / fp16 / fp32 / hipGraph replay: per-slice
-                all-reduces (fp32 or a copy-free bf16 wire) and Adam after them.
+                all-reduced. Bit-identical to the all-reduce step, but slower under the RCCL-like
+                stand-in at W = 2 / 4 / 8 (1.37 vs 1.29 ms at W=8: twice the collectives, each with
+                its fixed latency, and g_h1's all-gather must wait for the G tail, its last reader;
+                profiles/r6/ab_ddp_shard_standin_r6.txt), hence opt-in.
   "ddp"         the fused schedule with the all-reduces inside ONE hipGraph (native RCCL)
   "serial"      forward + G chain, then the D chain (the G all-reduce under D's backward)
 """
@@ -38,7 +41,7 @@ class HipDDPMixin:
         (name, model, a, b) all-reduced slices of everything it reads in fp32 (biases, BN
         scale / offset, linear layers), or None where the sharded update does not apply."""
         if not (self.ddp and self.dt == 0 and not self.graph_requested and self._g_split is not None
-                and os.environ.get("DCGAN_DDP_SHARD", "1") != "0"):
+                and os.environ.get("DCGAN_DDP_SHARD", "0") == "1"):
             return None
         Dm, G = self.model.d, self.model.g
         first_w = lambda ps: min(off for k, (off, _) in ps.offsets.items() if k.endswith("/w"))  # noqa: E731

@@ -297,14 +297,14 @@ def test_bf16_wire_direct_path_is_used(monkeypatch):
     assert "adam_d" in names and {"adam_g_a", "adam_g_b", "adam_g_c"} <= set(names)
 
 
-
-
-
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_update_is_the_bf16_ddp_default_and_hazard_free(world):
-    """Segmented DDP step, bf16, eager: the conv kernels go reduce-scatter -> Adam on 1/W ->
-    all-gather of the bf16 mirror (4 slices), the fp32-read tensors through two all-reduces."""
+def test_sharded_update_is_hazard_free(world, monkeypatch):
+    """Segmented DDP step, bf16, eager, DCGAN_DDP_SHARD=1: the conv kernels go reduce-scatter ->
+    Adam on 1/W -> all-gather of the bf16 mirror (4 slices), the fp32-read tensors through two
+    all-reduces. (Opt-in: the per-slice all-reduce step measured faster under the stand-in,
+    profiles/r6/ab_ddp_shard_standin_r6.txt.)"""
     from distributed_tensorflow_for_dcgan_amd.engine.hip_engine import HipEngine
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "1")
     eng = HipEngine(DCGANConfig(), 4, torch.device("cpu"), world=world, dry_run=True, graph=False)
     assert eng._sharded() and sorted(eng._shards) == ["dw_rest", "dw_top", "g_a", "g_b"]
     assert [n for n, _, _, _ in eng._small] == ["d_small", "g_c"]
@@ -314,9 +314,10 @@ def test_sharded_update_is_the_bf16_ddp_default_and_hazard_free(world):
     assert n > 100 and hz == [], "\n".join(map(str, hz[:10]))
 
 
-def test_checker_finds_the_top_kernel_gather_before_its_last_reader():
+def test_checker_finds_the_top_kernel_gather_before_its_last_reader(monkeypatch):
     """The top D kernel's Adam + all-gather must follow the D chain's top-layer data gradient
     (it reads the old bf16 mirror): issued right after its reduce-scatter, the checker reports it."""
+    monkeypatch.setenv("DCGAN_DDP_SHARD", "1")
     eng = _dry(world=2)
     assert eng._sharded()
 
