@@ -195,8 +195,15 @@ class HipDDPMixin:
         if self._adam_g_split():
             lo, hi = self._g_split[3:]
             adam_g("adam_g_a", lo, hi)      # g_h1's slice: right after its own collective
-            self._c_split_a = prog.size()
+            # g_h2..g_h4's slice with it when its collective precedes g_h1's on the comm stream
+            # (issued from alt1 inside the G chain: _ddp_gw_alt); stand-in W=8 1.288-1.291 vs
+            # 1.302-1.303 ms (profiles/r6/ab_ddp_adam_order_r6.txt)
+            early_b = self._ddp_gw_alt()
+            if not early_b:
+                self._c_split_a = prog.size()
             adam_g("adam_g_b", hi, n)
+            if early_b:                     # (only the projection's Adam waits for the last collective)
+                self._c_split_a = prog.size()
             adam_g("adam_g_c", 0, lo)
         else:
             self._c_split_a = self._c_split
@@ -249,6 +256,14 @@ class HipDDPMixin:
         profiles/r5/ab_adam_g_split_r5.txt)."""
         return (self._schedule() == "concurrent" and self._g_split is not None and not self.f16
                 and os.environ.get("DCGAN_ADAM_G_SPLIT", "1") != "0")
+
+    def _adam_d_alt(self) -> bool:
+        """Segmented all-reduce DDP step, eager replay: Adam(D) on the D chain's stream as soon as
+        D's collectives have landed, beside the G tail, instead of on the main stream after it
+        (DCGAN_DDP_ADAM_D_ALT=0: after it). --force_ddp (W=1) 124.6-125.3k vs 122.2-122.4k img/s;
+        stand-in W=2/4/8 within +-0.6 % (profiles/r6/ab_ddp_adam_order_r6.txt)."""
+        return (self._ddp_gw_alt() and not self._sharded()
+                and os.environ.get("DCGAN_DDP_ADAM_D_ALT", "1") != "0")
 
     def _wire_direct(self) -> bool:
         """bf16 wire without copies (segmented DDP step, bf16 engine): cast kernels inside the
@@ -424,8 +439,9 @@ class HipDDPMixin:
             self._tick(2, alt)
             self._ar_launch(ex, "dtop", alt)
             gw = self._ddp_gw_alt()
+            gd = []                            # mark: the g_loss pass is done with D's parameters
             if gw:                             # the same segments with G's weight gradients on alt1
-                self._g_chain_gw_alt(ex, cs)
+                self._g_chain_gw_alt(ex, cs, on_gd=gd.append if self._adam_d_alt() else None)
             else:
                 self._seg(ex, 2, cs)           # G chain: g_loss through D(fake), G backward to g_h1's wgrad
             self._tick(3, cs)
@@ -443,24 +459,33 @@ class HipDDPMixin:
             # D's last bucket, then the rest of G's; Adam(D) runs while G's is in flight
             self._ar_launch(ex, "drest", alt)
             d_done = ex.mark(ex.comm) if self.ddp else None
+            i = 6 if self._adam_g_split() else 5  # the "adam_D" segment
+            d_alt = self._adam_d_alt()
+            if d_alt:                          # Adam(D) on the D chain's stream once D's collectives
+                if d_done is not None:         # have landed and the g_loss pass has left D, beside
+                    ex.wait_mark(alt, d_done)  # the G tail
+                ex.wait_mark(alt, gd[0])
+                self._segments()[i][1](ex, alt, ex.alt[1])
+                self._tick(i + 1, alt)
             if self._g_split is not None:
                 if not gw:                     # (else issued from alt1 inside the G chain)
                     self._ar_launch(ex, "gsplit_b", cs)
                 self._ar_launch(ex, "gsplit_c", cs)
             else:
                 self._ar_launch(ex, "g", cs)
-            i = 5
             if self._adam_g_split():
                 if a_done is not None:
                     ex.wait_mark(cs, a_done)   # g_h1's collective (dtop's too: comm-stream order)
-                self._seg(ex, i, cs)           # Adam over g_h1's slice, beside the other collectives
-                i += 1
-                self._tick(i, cs)
-            if d_done is not None:
-                ex.wait_mark(cs, d_done)       # dtop + drest (and g_h1's) collectives
-            ex.wait(cs, alt)                   # (W = 1, timed: the D chain itself)
-            self._seg(ex, i, cs)               # Adam D -> D mirror (overlaps G's all-reduce)
-            self._tick(i + 1, cs)
+                self._seg(ex, 5, cs)           # Adam over g_h1's slice, beside the other collectives
+                self._tick(6, cs)
+            if d_alt:
+                ex.wait(cs, alt)               # Adam(D) (before the step counter / beta powers)
+            else:
+                if d_done is not None:
+                    ex.wait_mark(cs, d_done)   # dtop + drest (and g_h1's) collectives
+                ex.wait(cs, alt)               # (W = 1, timed: the D chain itself)
+                self._seg(ex, i, cs)           # Adam D -> D mirror (overlaps G's all-reduce)
+                self._tick(i + 1, cs)
             self._ar_join(ex, cs)              # G's collectives
             self._seg(ex, i + 1, cs)           # Adam G (the rest), step counter, G mirror
             self._tick(i + 2, cs)
