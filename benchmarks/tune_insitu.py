@@ -108,7 +108,7 @@ def neighbours(key, cur, tiles=False, extra_tiles=(), extra_cfgs=()):
         mode, Kc = int(key.split(",")[0]), int(key.split(",")[4])
         N = int(key.split(",")[7])
         out += [(c, sp) for c in extra_cfgs if H.igemm3_pp_ok(c, mode, Kc) and H.IGEMM3_TILES[c % 10][1] <= max(N, 64)]
-    for s2 in (sp // 2, sp * 2, sp + 1, sp - 1):
+    for s2 in (sp // 2, sp * 2, sp * 4, sp + 1, sp - 1):
         if 1 <= s2 <= 32 and s2 != sp:
             out.append((cfg, s2))
     if key.startswith("w3,"):
