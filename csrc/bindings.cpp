@@ -316,6 +316,20 @@ class Program {
     last_nphases_ = a.nphases;
     a.kb_valid = kb_valid;
     a.splits = splits;
+    {
+      // XCD locality (igemm3): each of the 8 XCDs runs a contiguous eighth of the tiles. M slowest
+      // (default): a run spans whole tile rows -- 1/8 of the activations, all weight columns; N
+      // slowest: the reverse. Per-XCD footprint of a run of T/8 tiles (T = mtiles x ntiles):
+      //   M slowest: A/8 + B        (T/8 >= ntiles), else A/mtiles + B*mtiles/8
+      //   N slowest: A + B/8        (T/8 >= mtiles), else A*ntiles/8 + B/ntiles
+      // N slowest when that is clearly smaller (weight-heavy layers: G's 4x4 -> 8x8 deconv reads
+      // 6.5 MB of weights against 2 MB of input). DCGAN_IGEMM_NMAJOR=0 / 1 forces the order.
+      const double A_ = (double)a.a_bytes, B_ = (double)a.b_bytes, T8 = (double)mtiles * ntiles / 8.0;
+      const double fm = T8 >= ntiles ? A_ / 8 + B_ : A_ / mtiles + B_ * mtiles / 8.0;
+      const double fn = T8 >= mtiles ? A_ + B_ / 8 : A_ * ntiles / 8.0 + B_ / ntiles;
+      a.nmajor = fn < 0.8 * fm ? 1 : 0;
+      if (const char* e = std::getenv("DCGAN_IGEMM_NMAJOR")) a.nmajor = e[0] == '1' ? 1 : (e[0] == '0' ? 0 : a.nmajor);
+    }
     const size_t out_es = out_f32 ? 4 : es_;
     AccList acc;
     acc.r(A, a_elems * es_).r(Bw, b_elems * es_).r(bias, (size_t)N * 4)

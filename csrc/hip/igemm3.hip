@@ -160,8 +160,13 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     u = (f < rr ? f * (q + 1) : rr * (q + 1) + (f - rr) * q) + (u >> 3);
     split = u % S;
     const int r2 = u / S;
-    nt = r2 % ntn;
-    mt = r2 / ntn;
+    if (p.nmajor) {
+      mt = r2 % p.mtiles;
+      nt = r2 / p.mtiles;
+    } else {
+      nt = r2 % ntn;
+      mt = r2 / ntn;
+    }
   } else {
     {  // bijective XCD remap: workgroups b, b+8, b+16, ... (one XCD) get a contiguous run of t
       const int q = total >> 3, rr = total & 7, xcd = t & 7;
@@ -173,8 +178,13 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm3_kernel(IGemmArgs p) {
     int r_ = t / S;
     phase = r_ % p.nphases;
     r_ /= p.nphases;
-    nt = r_ % ntn;
-    mt = r_ / ntn;
+    if (p.nmajor) {
+      mt = r_ % p.mtiles;
+      nt = r_ / p.mtiles;
+    } else {
+      nt = r_ % ntn;
+      mt = r_ / ntn;
+    }
   }
   const int tile_id = (phase * p.mtiles + mt) * ntn + nt;
 

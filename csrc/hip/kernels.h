@@ -57,6 +57,9 @@ struct IGemmArgs {
   // igemm3: longest phase first (mode 1: phases host-sorted by decreasing tap count, dispatched
   // phase by phase, each phase's tiles XCD-contiguous) instead of the phases interleaved
   int lpt;
+  // igemm3: tile order with N slowest (each XCD's contiguous run of tiles shares weight columns)
+  // instead of M slowest (shares activation rows); the host picks the smaller per-XCD footprint
+  int nmajor;
 };
 
 
