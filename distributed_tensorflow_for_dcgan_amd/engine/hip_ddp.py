@@ -173,26 +173,9 @@ class HipDDPMixin:
 
     def _build_update_d_first(self, prog):
         """Adam(D) (progC[:_c_split]), then Adam(G) + beta powers / global step: the step counter
-        update must follow both Adams (each reads its model's beta powers). _adam_end_merged():
-        no separate Adam(D); Adam over g_h1..g_h4 after g_h1's collective, then ONE adam2 launch
-        over G's projection slice + all of D + powers + step once every collective has landed."""
+        update must follow both Adams (each reads its model's beta powers)."""
         gs = 1.0 / self.world
         od, og = self.opt_d, self.opt_g
-        if self._adam_end_merged():
-            G, Dm = self.model.g, self.model.d
-            lo, hi = self._g_split[3:]
-            es = self.wbf_g.flat.element_size()
-            self._c_split = prog.size()  # (empty "adam_D" segment)
-            for name, a, b in (("adam_g_a", lo, hi), ("adam_g_b", hi, G.flat.numel())):
-                prog.adam_bf(name, _p(G.flat) + 4 * a, _p(self.wbf_g.flat) + es * a, _p(self.grad_g.flat) + 4 * a,
-                             _p(og.m.flat) + 4 * a, _p(og.v.flat) + 4 * a, _p(og.powers), b - a, og.lr, og.beta1,
-                             og.beta2, og.eps, gs, 0, 0, 0)
-            self._c_split_a = prog.size()
-            prog.adam2("adam_gc_d", _p(G.flat), _p(self.wbf_g.flat), _p(self.grad_g.flat), _p(og.m.flat),
-                       _p(og.v.flat), _p(og.powers), lo, og.lr, og.beta1, og.beta2, og.eps, _p(Dm.flat),
-                       _p(self.wbf_d.flat), _p(self.grad_d.flat), _p(od.m.flat), _p(od.v.flat), _p(od.powers),
-                       Dm.flat.numel(), od.lr, od.beta1, od.beta2, od.eps, gs, _p(self.step_counter), 0)
-            return
         ls = _p(self.loss_scale)
         mg = 0 if self.f32 else _p(self.wbf_g.flat)
         md = 0 if self.f32 else _p(self.wbf_d.flat)
@@ -279,16 +262,8 @@ class HipDDPMixin:
         D's collectives have landed, beside the G tail, instead of on the main stream after it
         (DCGAN_DDP_ADAM_D_ALT=0: after it). --force_ddp (W=1) 124.6-125.3k vs 122.2-122.4k img/s;
         stand-in W=2/4/8 within +-0.6 % (profiles/r6/ab_ddp_adam_order_r6.txt)."""
-        return (self._ddp_gw_alt() and not self._sharded() and not self._adam_end_merged()
+        return (self._ddp_gw_alt() and not self._sharded()
                 and os.environ.get("DCGAN_DDP_ADAM_D_ALT", "1") != "0")
-
-    def _adam_end_merged(self) -> bool:
-        """DCGAN_DDP_ADAM_D_ALT=m (segmented all-reduce DDP step, bf16, fp32 wire, eager): Adam(D)
-        folded into one adam2 launch with the projection's Adam at the end of the step (the comm-
-        bound tail at large W: one launch and one cross-stream join less)."""
-        return (self._ddp_gw_alt() and not self._sharded() and self.dt == 0 and not self.f32
-                and self.wire_d is None and self._adam_g_split() and self._g_split[3] % 4 == 0
-                and os.environ.get("DCGAN_DDP_ADAM_D_ALT", "1") == "m")
 
     def _wire_direct(self) -> bool:
         """bf16 wire without copies (segmented DDP step, bf16 engine): cast kernels inside the

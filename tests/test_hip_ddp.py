@@ -89,33 +89,6 @@ def test_hip_ddp_two_ranks_match_single_process(tmp_path, graph, schedule):
     assert torch.equal(r0["g"], g), (r0["g"] - g).abs().max()
 
 
-def _worker_env(rank, world, port, graph, out_dir, schedule, env):
-    os.environ.update(env)
-    _worker(rank, world, port, graph, out_dir, schedule)
-
-
-def test_merged_end_adam_two_ranks_match_single_process(tmp_path):
-    """DCGAN_DDP_ADAM_D_ALT=m (Adam(D) + the projection's Adam + powers + step in one adam2 launch
-    at the end of the segmented step): two ranks on identical data reproduce the single-process
-    engine bit for bit, like the default placement."""
-    ctx = mp.get_context("spawn")
-    port = _free_port()
-    env = {"DCGAN_DDP_ADAM_D_ALT": "m"}
-    procs = [ctx.Process(target=_worker_env, args=(r, 2, port, False, str(tmp_path), "concurrent", env))
-             for r in range(2)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=600)
-        assert p.exitcode == 0, "rank exited with %s" % p.exitcode
-    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
-    assert torch.equal(r0["d"], r1["d"]) and torch.equal(r0["g"], r1["g"]) and r0["step"] == STEPS
-    d, g, _ = _run(_make(1, 0, False))
-    assert torch.equal(r0["d"], d), (r0["d"] - d).abs().max()
-    assert torch.equal(r0["g"], g), (r0["g"] - g).abs().max()
-
-
 def _shard_worker(rank, world, port, out_dir, shard):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -345,16 +345,3 @@ def test_checker_finds_the_top_kernel_gather_before_its_last_reader(monkeypatch)
     eng._run_step = early
     hz, _ = SC.check_engine(eng)
     assert any("all_gather" in h.a or "all_gather" in h.b for h in hz), "\n".join(map(str, hz[:10]))
-
-
-@pytest.mark.parametrize("world", [2, 8])
-def test_merged_end_adam_is_hazard_free(world, monkeypatch):
-    """DCGAN_DDP_ADAM_D_ALT=m: Adam(D) folded into one adam2 launch with the projection's Adam at
-    the end of the segmented all-reduce step (no Adam(D) of its own)."""
-    monkeypatch.setenv("DCGAN_DDP_ADAM_D_ALT", "m")
-    eng = _dry(world=world)
-    assert eng._adam_end_merged() and not eng._adam_d_alt()
-    names = [eng.progC.op_info(i)[0] for i in range(eng.progC.size())]
-    assert names == ["adam_g_a", "adam_g_b", "adam_gc_d"] and eng._c_split == 0
-    hz, n = SC.check_engine(eng)
-    assert n > 100 and hz == [], "\n".join(map(str, hz[:10]))
