@@ -37,6 +37,17 @@ __device__ __forceinline__ int w5_swz(int r) {  // 8-byte-chunk XOR of k-major r
   else return 4 * ((r >> 3) & 1);
 }
 
+// the window (A operand) swizzle. One ds_read_tr16_b64 half-wave reads the pixels q4 + 20 g4'
+// (g4' = 0, 1) apart for WD = 8 (window rows of W2 = 20) and q4 + 8 g4' for WD = 16: the rows of
+// one parity must take four distinct 8-byte-chunk groups of their 32-bank half. Bits 1 + 3 do
+// that for the +8 spacing; for +20 (= 4 mod 8) bits 1 + 2 do (the rows are then four distinct
+// residues mod 8 of one parity). Round 6: 64x8 tiles measured a 0.43 LDS bank-conflict ratio.
+template <int S, int WD>
+__device__ __forceinline__ int w5_swz_a(int r) {
+  if constexpr (S == 128 && WD == 8) return 4 * (((r >> 1) & 1) | (((r >> 2) & 1) << 1));
+  else return w5_swz<S>(r);
+}
+
 template <int N_>
 __device__ __forceinline__ void w5_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
@@ -107,7 +118,7 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
     const int c = jj < W2 / 2 ? 2 * jj : 2 * (jj - W2 / 2) + 1;  // its column: even ones first, then odd
     a_ry[i] = ry;
     a_ix[i] = c - p.pl;
-    a_m[i] = m0 + ((lane % CA) ^ (w5_swz<SA>(wp) >> 1)) * 8;
+    a_m[i] = m0 + ((lane % CA) ^ (w5_swz_a<SA, WD>(wp) >> 1)) * 8;
     a_ok[i] = ry < R && c < 2 * WD + 3 && (unsigned)(c - p.pl) < (unsigned)p.Wg;
   }
   int b_row[PPW_B], b_n[PPW_B];
@@ -183,7 +194,7 @@ __global__ __launch_bounds__(256) void wgrad5_kernel(WGrad3Args p) {
           for (int i = 0; i < FM; ++i) {
             const int c8 = (wm * TM + i * 16) / 4 + p4;
             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                LDS_PTR(s16x4, sa + wr * SA + ((c8 ^ w5_swz<SA>(wr)) * 8)));
+                LDS_PTR(s16x4, sa + wr * SA + ((c8 ^ w5_swz_a<SA, WD>(wr)) * 8)));
             const elem4 vb = __builtin_bit_cast(elem4, v);
 #pragma unroll
             for (int e = 0; e < 4; ++e) af[x][i][4 * h + e] = vb[e];
